@@ -1,0 +1,139 @@
+/*
+ * srpde.h -- C ABI of libsrpde_hip.so, the MI355X (gfx950) kernels behind the
+ * superresolution_for_pdes_amd drop-in for tahmidawal/Superresolution_for_PDEs.
+ *
+ * The reference is pure Python (no FFI layer); its hot path dispatches PyTorch aten ops
+ * from src/models.py and SciPy's SuperLU from src/data_generation.py.  Each entry point
+ * below replaces the aten / SciPy call(s) cited next to it.  The Python binding is
+ * superresolution_for_pdes_amd/_lib.py (ctypes); INTEGRATION.md shows the stub a
+ * maintainer would add on the reference side.
+ *
+ * Conventions
+ *  - All tensor arguments are caller-owned DEVICE pointers; the library never allocates,
+ *    frees or synchronises the host.  Scratch is passed in as (workspace, ws_bytes), its
+ *    size queried with the matching *_workspace_size() function.
+ *  - Activations are NHWC fp32 ("channels-last").  A view is (pointer, ld): ld = floats
+ *    between consecutive pixels, so channel slices of a wider tensor (virtual concat) need
+ *    no copy.  Channel counts and ld must be multiples of 4; pointers 16-byte aligned.
+ *  - Every call is stream-ordered on `stream` (on ROCm torch.cuda.current_stream().cuda_stream).
+ *  - Return: 0 on success, negative on a bad argument (-1 arg, -2 shape, -3 alignment,
+ *    -4 workspace too small), positive hipError_t on a launch failure.  srpde_last_error()
+ *    returns the thread-local message of the last failure.
+ */
+#ifndef SRPDE_H_
+#define SRPDE_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+const char* srpde_last_error(void);
+int srpde_version(void);
+
+/* ---- convolution: nn.Conv2d 3x3 (dilation 1|2) / 1x1 -------------------------------
+ * replaces aten::convolution (fwd) and aten::convolution_backward (dgrad, wgrad) for
+ * ConvBlock.conv1/conv2 (src/models.py:16,18,22-23), bridge[0]/[3] (models.py:43,46),
+ * out_conv1/out_conv2 (models.py:57,59).  torch.cat (models.py:87,90,93) is absorbed as
+ * the (x1, c1) second input.  stats (nullable): per row-block (mean, M2) float2
+ * partials for the train-mode BatchNorm that follows; srpde_conv_stats_blocks() blocks
+ * of srpde_conv_stats_rows_per_block() rows each. */
+int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout, int cin, int cin_real,
+                            int ksize, hipStream_t stream);
+int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const float* wpack,
+                   const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
+                   int sign, int accumulate, float* stats, hipStream_t stream);
+size_t srpde_conv_stats_blocks(int n, int h, int w, int cout);
+int srpde_conv_stats_rows_per_block(int cout);
+size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, int ksize);
+int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                     int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
+                     int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* ---- BatchNorm2d + ReLU -------------------------------------------------------------
+ * replaces aten::native_batch_norm / native_batch_norm_backward and relu /
+ * threshold_backward for every nn.BatchNorm2d (src/models.py:17,19,44,47,58,60) and the
+ * F.relu / nn.ReLU after it (models.py:22-23,45,48,96-97). */
+int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long long P, int C,
+                            float* running_mean, float* running_var, long long* num_batches_tracked,
+                            float momentum, float eps, float* mean_out, float* invstd_out, hipStream_t stream);
+int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, int C, float eps, float* mean_out,
+                          float* invstd_out, hipStream_t stream);
+int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, float* out, int ldo, long long P, int C, int relu, hipStream_t stream);
+size_t srpde_bn_relu_bwd_workspace_size(long long P, int C);
+int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                      const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
+                      float* dbias, long long P, int C, int relu, void* workspace, size_t ws_bytes,
+                      hipStream_t stream);
+
+/* ---- input staging: NCHW model input -> NHWC (channel-padded) ----------------------- */
+int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w, int cpad, hipStream_t stream);
+
+/* ---- nn.MaxPool2d(2)  (src/models.py:69, used :79-80) -------------------------------- */
+int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int c,
+                         hipStream_t stream);
+int srpde_maxpool2x2_bwd(const float* x, int ldx, const float* dout, int lddo, float* dx, int lddx, int n, int h,
+                         int w, int c, int accumulate, hipStream_t stream);
+
+/* ---- bilinear, align_corners=True: nn.Upsample(2) (models.py:70, :89-93) and the
+ *      F.interpolate(size=(40,40)) of PDEDataset (models.py:182-187) ------------------ */
+int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho, int wo,
+                                int c, hipStream_t stream);
+int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
+                                int wo, int c, int accumulate, hipStream_t stream);
+
+/* ---- AttentionGate.forward / backward (src/models.py:103-130) ----------------------- */
+int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,
+                  const float* b1, const float* w2, const float* b2, const float* wg, const float* bg, float* m,
+                  float* hbuf, float* ca, float* sa, float* out, int ldo, hipStream_t stream);
+size_t srpde_att_bwd_workspace_size(int n, int hw, int c, int gc);
+int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const float* g, int ldg, int n, int hw,
+                  int c, int gc, const float* w1, const float* w2, const float* wg, const float* m, const float* hbuf,
+                  const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
+                  int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
+                  void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* ---- output head: final 1x1 conv + residual x[:,0:1] (models.py:61,74,98,101) ------- */
+int srpde_head_fwd(const float* z, int ldz, int c, const float* wf, const float* bf, const float* xin, int xin_c,
+                   int n, int hw, float* out, hipStream_t stream);
+size_t srpde_head_bwd_workspace_size(int n, int hw, int c);
+int srpde_head_bwd(const float* dout, const float* z, int ldz, int c, const float* wf, int n, int hw, float* dz,
+                   int lddz, float* dwf, float* dbf, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* ---- nn.MSELoss (src/train_enhanced.py:70,307) --------------------------------------- */
+size_t srpde_mse_workspace_size(void);
+int srpde_mse_fwd(const float* y, const float* t, long long n, float* loss, void* workspace, size_t ws_bytes,
+                  hipStream_t stream);
+int srpde_mse_bwd(const float* y, const float* t, long long n, const float* gout, float* dy, hipStream_t stream);
+
+/* ---- clip_grad_norm_ + AdamW on one flat buffer (src/train_enhanced.py:74-75,308) ---- */
+size_t srpde_grad_norm_workspace_size(void);
+int srpde_clip_coef(const float* g, long long n, float grad_scale, float max_norm, float* coef, void* workspace,
+                    size_t ws_bytes, hipStream_t stream);
+int srpde_adamw_step(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                     float eps, float weight_decay, int step, const float* coef, float grad_scale,
+                     hipStream_t stream);
+
+/* ---- Poisson: replaces scipy.sparse.linalg.spsolve(diag(theta) @ L, f)
+ *      (src/data_generation.py:79-104, src/enhanced_data_generation.py:47-68) -------- */
+int srpde_poisson_lds_max_n(void);
+size_t srpde_poisson_workspace_size(int B, int n);
+int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
+                         int* iters, double* resid, hipStream_t stream);
+int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,
+                               hipStream_t stream);
+int srpde_poisson_cg_grid_iterate(int B, int n, double rtol, int k_begin, int k_count, int maxit, void* ws,
+                                  size_t ws_bytes, hipStream_t stream);
+size_t srpde_poisson_cg_grid_done_offset(int B, int n);
+int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit, void* ws, size_t ws_bytes,
+                                 hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRPDE_H_ */

@@ -1,0 +1,345 @@
+// BatchNorm2d (train / eval) + ReLU for NHWC fp32, gfx950.
+//
+// Reference semantics (src/models.py:17,19,44-48,58,60 -> nn.BatchNorm2d defaults, then
+// F.relu / nn.ReLU): train mode normalises with the biased batch variance, updates
+// running_mean / running_var (unbiased) with momentum 0.1 and num_batches_tracked += 1;
+// eval mode uses the running statistics.  eps = 1e-5.
+//
+// Batch statistics come from the conv epilogue's per-row-block (mean, M2) partials
+// (conv.hip) merged here with Chan's parallel formula in fp64, in a fixed tree order
+// (deterministic).  The backward recomputes x_hat and the ReLU mask from the conv
+// output y instead of storing them.
+#include "common.h"
+
+namespace srpde {
+
+struct Chan {
+  double n, mean, m2;
+};
+__device__ __forceinline__ Chan chan_merge(Chan a, Chan b) {
+  if (b.n == 0.0) return a;
+  if (a.n == 0.0) return b;
+  const double n = a.n + b.n, d = b.mean - a.mean;
+  Chan r;
+  r.n = n;
+  r.mean = a.mean + d * (b.n / n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+  return r;
+}
+
+// one block per channel
+__global__ __launch_bounds__(256) void bn_train_finalize_kernel(
+    const float2* __restrict__ stats, int nblk, int rows_per_blk, long long P, int C,
+    float* running_mean, float* running_var, float momentum, float eps,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+  const int c = blockIdx.x;
+  __shared__ double sn[256], sm[256], s2[256];
+  Chan acc{0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nblk; b += 256) {
+    const float2 v = stats[(size_t)b * C + c];
+    const long long rem = P - (long long)b * rows_per_blk;
+    const double cnt = (double)(rem < rows_per_blk ? rem : rows_per_blk);
+    acc = chan_merge(acc, Chan{cnt, (double)v.x, (double)v.y});
+  }
+  sn[threadIdx.x] = acc.n; sm[threadIdx.x] = acc.mean; s2[threadIdx.x] = acc.m2;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      Chan a{sn[threadIdx.x], sm[threadIdx.x], s2[threadIdx.x]};
+      Chan b{sn[threadIdx.x + s], sm[threadIdx.x + s], s2[threadIdx.x + s]};
+      a = chan_merge(a, b);
+      sn[threadIdx.x] = a.n; sm[threadIdx.x] = a.mean; s2[threadIdx.x] = a.m2;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double n = sn[0], mean = sm[0], m2 = s2[0];
+    const double var_b = m2 / n;
+    const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)(1.0 / sqrt(var_b + (double)eps));
+    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    if (running_var) running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)var_u;
+  }
+}
+
+__global__ void bn_eval_prepare_kernel(const float* rm, const float* rv, int C, float eps, float* mean_out,
+                                       float* invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    mean_out[c] = rm[c];
+    invstd_out[c] = 1.0f / sqrtf(rv[c] + eps);
+  }
+}
+
+__global__ void increment_i64_kernel(long long* p) { *p += 1; }
+
+// out = relu((y - mean) * invstd * gamma + beta)
+__global__ __launch_bounds__(256) void bn_relu_fwd_kernel(const float* __restrict__ y, int ldy,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ out,
+                                                          int ldo, long long P, int C, int relu) {
+  const int C4 = C >> 2;
+  const long long total = P * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / C4;
+    const int c = (int)(e - p * C4) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    float4 o;
+    o.x = (v.x - mu.x) * is.x * g.x + b.x;
+    o.y = (v.y - mu.y) * is.y * g.y + b.y;
+    o.z = (v.z - mu.z) * is.z * g.z + b.z;
+    o.w = (v.w - mu.w) * is.w * g.w + b.w;
+    if (relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    *reinterpret_cast<float4*>(out + p * ldo + c) = o;
+  }
+}
+
+// Generic per-channel column reduction layout used by the backward passes:
+// block b owns rows [b*rows_per_blk, ...), threads tile (row, channel-quad).
+__device__ __forceinline__ void thread_rc(int C, int* c4, int* r0, int* rstride) {
+  const int C4 = C >> 2;
+  *c4 = threadIdx.x % C4;
+  *r0 = threadIdx.x / C4;
+  *rstride = blockDim.x / C4;
+}
+
+// partial sums of dz and dz*xhat per (block, channel); dz = da * [bn_out > 0]
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ y, int ldy,
+                                                            const float* __restrict__ da, int ldda,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, long long P, int C,
+                                                            int rows_per_blk, int relu,
+                                                            float2* __restrict__ part) {
+  extern __shared__ float4 red4[];  // [2][256]
+  int c4, r0, rs;
+  thread_rc(C, &c4, &r0, &rs);
+  const int active = (C >> 2) * rs;
+  const int c = c4 * 4;
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  if ((int)threadIdx.x < active) {
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    const long long pb = (long long)blockIdx.x * rows_per_blk;
+    const long long pe = min(P, pb + rows_per_blk);
+    for (long long p = pb + r0; p < pe; p += rs) {
+      const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
+      const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+      float xh, dz;
+#define BN_ACC(X)                                              \
+  xh = (v.X - mu.X) * is.X;                                    \
+  dz = (!relu || xh * g.X + b.X > 0.f) ? d.X : 0.f;            \
+  s1.X += dz;                                                  \
+  s2.X += dz * xh;
+      BN_ACC(x) BN_ACC(y) BN_ACC(z) BN_ACC(w)
+#undef BN_ACC
+    }
+  }
+  red4[threadIdx.x] = s1;
+  red4[256 + threadIdx.x] = s2;
+  __syncthreads();
+  if ((int)threadIdx.x < (C >> 2)) {
+    float4 t1 = make_float4(0.f, 0.f, 0.f, 0.f), t2 = t1;
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red4[r * (C >> 2) + threadIdx.x], b2 = red4[256 + r * (C >> 2) + threadIdx.x];
+      t1.x += a.x; t1.y += a.y; t1.z += a.z; t1.w += a.w;
+      t2.x += b2.x; t2.y += b2.y; t2.z += b2.z; t2.w += b2.w;
+    }
+    float2* o = part + (size_t)blockIdx.x * C + c;
+    o[0] = make_float2(t1.x, t2.x); o[1] = make_float2(t1.y, t2.y);
+    o[2] = make_float2(t1.z, t2.z); o[3] = make_float2(t1.w, t2.w);
+  }
+}
+
+// fp64 column sums of [nblk][C] float2 partials -> out0[C], out1[C]; one block per channel
+__global__ __launch_bounds__(256) void colsum2_kernel(const float2* __restrict__ part, int nblk, int C,
+                                                      float* out0, float* out1, double* keep0, double* keep1) {
+  const int c = blockIdx.x;
+  __shared__ double a[256], b[256];
+  double x = 0.0, yv = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 256) {
+    const float2 v = part[(size_t)k * C + c];
+    x += v.x; yv += v.y;
+  }
+  a[threadIdx.x] = x; b[threadIdx.x] = yv;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) { a[threadIdx.x] += a[threadIdx.x + s]; b[threadIdx.x] += b[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out0) out0[c] = (float)a[0];
+    if (out1) out1[c] = (float)b[0];
+    if (keep0) keep0[c] = a[0];
+    if (keep1) keep1[c] = b[0];
+  }
+}
+
+// dy = gamma*invstd*(dz - sum(dz)/P - xhat*sum(dz*xhat)/P); partial column sums of dy (conv bias grad)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ y, int ldy,
+                                                           const float* __restrict__ da, int ldda,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const double* __restrict__ sdz,
+                                                           const double* __restrict__ sdzx, long long P, int C,
+                                                           int rows_per_blk, int relu, float* __restrict__ dy,
+                                                           int lddy, float2* __restrict__ bias_part) {
+  extern __shared__ float4 red4[];
+  int c4, r0, rs;
+  thread_rc(C, &c4, &r0, &rs);
+  const int active = (C >> 2) * rs;
+  const int c = c4 * 4;
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((int)threadIdx.x < active) {
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    const double invP = 1.0 / (double)P;
+    float4 m1, m2, k;
+    m1.x = (float)(sdz[c] * invP); m1.y = (float)(sdz[c + 1] * invP);
+    m1.z = (float)(sdz[c + 2] * invP); m1.w = (float)(sdz[c + 3] * invP);
+    m2.x = (float)(sdzx[c] * invP); m2.y = (float)(sdzx[c + 1] * invP);
+    m2.z = (float)(sdzx[c + 2] * invP); m2.w = (float)(sdzx[c + 3] * invP);
+    k.x = g.x * is.x; k.y = g.y * is.y; k.z = g.z * is.z; k.w = g.w * is.w;
+    const long long pb = (long long)blockIdx.x * rows_per_blk;
+    const long long pe = min(P, pb + rows_per_blk);
+    for (long long p = pb + r0; p < pe; p += rs) {
+      const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
+      const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+      float4 o;
+      float xh, dz;
+#define BN_APPLY(X)                                            \
+  xh = (v.X - mu.X) * is.X;                                    \
+  dz = (!relu || xh * g.X + b.X > 0.f) ? d.X : 0.f;            \
+  o.X = (dz - m1.X - xh * m2.X) * k.X;                         \
+  sb.X += o.X;
+      BN_APPLY(x) BN_APPLY(y) BN_APPLY(z) BN_APPLY(w)
+#undef BN_APPLY
+      *reinterpret_cast<float4*>(dy + p * lddy + c) = o;
+    }
+  }
+  if (bias_part == nullptr) return;
+  red4[threadIdx.x] = sb;
+  __syncthreads();
+  if ((int)threadIdx.x < (C >> 2)) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red4[r * (C >> 2) + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    float2* o = bias_part + (size_t)blockIdx.x * C + c;
+    o[0] = make_float2(t.x, 0.f); o[1] = make_float2(t.y, 0.f);
+    o[2] = make_float2(t.z, 0.f); o[3] = make_float2(t.w, 0.f);
+  }
+}
+
+static int bwd_blocks(long long P, int C, int* rows_per_blk) {
+  // ~1024 blocks; rows per block a multiple of the rows a block covers per sweep
+  const int rs = 256 / (C >> 2);
+  long long rpb = (P + 1023) / 1024;
+  rpb = (rpb + rs - 1) / rs * rs;
+  if (rpb < rs) rpb = rs;
+  *rows_per_blk = (int)rpb;
+  return (int)((P + rpb - 1) / rpb);
+}
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long long P, int C,
+                            float* running_mean, float* running_var, long long* num_batches_tracked,
+                            float momentum, float eps, float* mean_out, float* invstd_out, hipStream_t stream) {
+  SRPDE_CHECK_ARG(stats && mean_out && invstd_out && C > 0 && nblk > 0, "srpde_bn_train_finalize: bad args");
+  hipLaunchKernelGGL(bn_train_finalize_kernel, dim3(C), dim3(256), 0, stream,
+                     reinterpret_cast<const float2*>(stats), nblk, rows_per_blk, P, C, running_mean, running_var,
+                     momentum, eps, mean_out, invstd_out);
+  SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize");
+  if (num_batches_tracked) {
+    hipLaunchKernelGGL(increment_i64_kernel, dim3(1), dim3(1), 0, stream, num_batches_tracked);
+    SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize(nbt)");
+  }
+  return 0;
+}
+
+int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, int C, float eps, float* mean_out,
+                          float* invstd_out, hipStream_t stream) {
+  SRPDE_CHECK_ARG(running_mean && running_var && mean_out && invstd_out, "srpde_bn_eval_prepare: null");
+  hipLaunchKernelGGL(bn_eval_prepare_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, stream, running_mean,
+                     running_var, C, eps, mean_out, invstd_out);
+  SRPDE_LAUNCH_CHECK("srpde_bn_eval_prepare");
+  return 0;
+}
+
+int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, float* out, int ldo, long long P, int C, int relu, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out, "srpde_bn_relu_fwd: null");
+  SRPDE_CHECK_ARG(C % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0, "srpde_bn_relu_fwd: C/ld must be multiples of 4");
+  const long long total = P * (C / 4);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
+                     out, ldo, P, C, relu);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_fwd");
+  return 0;
+}
+
+size_t srpde_bn_relu_bwd_workspace_size(long long P, int C) {
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  return (size_t)nblk * C * sizeof(float2) * 2 + (size_t)C * sizeof(double) * 2;
+}
+
+int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                      const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
+                      float* dbias, long long P, int C, int relu, void* workspace, size_t ws_bytes,
+                      hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && dy && workspace, "srpde_bn_relu_bwd: null");
+  SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0 && lddy % 4 == 0,
+                  "srpde_bn_relu_bwd: C/ld must be multiples of 4 (C<=1024)");
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  const size_t need = srpde_bn_relu_bwd_workspace_size(P, C);
+  if (ws_bytes < need) {
+    set_error("srpde_bn_relu_bwd: workspace %zu < %zu", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  float2* part = static_cast<float2*>(workspace);
+  float2* bpart = part + (size_t)nblk * C;
+  double* sdz = reinterpret_cast<double*>(bpart + (size_t)nblk * C);
+  double* sdzx = sdz + C;
+  const size_t lds = 2 * 256 * sizeof(float4);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd,
+                     gamma, beta, P, C, rpb, relu, part);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(reduce)");
+  hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, part, nblk, C, dbeta, dgamma, sdz, sdzx);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(colsum)");
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd,
+                     gamma, beta, sdz, sdzx, P, C, rpb, relu, dy, lddy, dbias ? bpart : nullptr);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(apply)");
+  if (dbias) {
+    hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, bpart, nblk, C, dbias, (float*)nullptr,
+                       (double*)nullptr, (double*)nullptr);
+    SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(bias)");
+  }
+  return 0;
+}
+
+}  // extern "C"

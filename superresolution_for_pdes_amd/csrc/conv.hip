@@ -1,0 +1,854 @@
+// Implicit-GEMM 3x3 / 1x1 convolution for gfx950 on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the aten convolution / convolution_backward calls that reference
+// src/models.py makes through nn.Conv2d (ConvBlock.conv1/conv2 models.py:16,18;
+// bridge[0],[3] models.py:43,46 with dilation 2; out_conv1/2 models.py:57,59).
+//
+//   forward :  Y[p][n] = bias[n] + sum_{t,c} X[p + sign*off(t)][c] * Wp[n][t][c]
+//   dgrad   :  the same kernel with sign = -1 and Wd[c][t][n] = W[n][c][t]
+//   wgrad   :  dW[n][t][c] = sum_p dY[p][n] * X[p + off(t)][c]   (split-K over pixels,
+//              deterministic slab reduction -- no float atomics)
+//
+// X may be a *virtual concat* of two NHWC views (x0: c0 channels, x1: c1 channels) so
+// torch.cat in UNet.forward (models.py:87,90,93) never materialises.  The forward
+// epilogue adds the bias, stores Y and emits per-(row-block, channel) BatchNorm
+// partial statistics (block mean, block M2) for the train-mode BN that always follows
+// (models.py:22-23,44,47,96-97): the batch statistics never re-read Y from HBM.
+#include "common.h"
+
+namespace srpde {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct ConvParams {
+  const float* x0; int c0; int ldx0;
+  const float* x1; int c1; int ldx1;
+  const float* w;       // [Cout][taps][Cin] packed, Cin = c0 + c1
+  const float* bias;    // [Cout] or null
+  float* y; int ldy;    // output view
+  float2* stats;        // [mblocks][Cout] (mean, M2) or null
+  int N, H, W, Cout, ksize, dil, sign, accumulate;
+  int P, K, Cin;
+};
+
+constexpr int BK = 16;      // k (tap*Cin + c) per stage
+constexpr int LDK = BK + 4; // padded LDS row: conflict-free ds_read_b128 over 32 rows
+
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  // bijective: blocks that share an A row-panel land on one XCD (MI355X L2 per XCD)
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_igemm_fwd_kernel(ConvParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int A_LOADS = BM / 64;                         // float4 per thread per stage
+  constexpr int B_ROWS_PER_PASS = 64;
+  constexpr int B_LOADS = BN >= 64 ? BN / 64 : 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                        // [2][BM][LDK]
+  float* Bs = smem + 2 * BM * LDK;         // [2][BN][LDK]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nbm * nbn);
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+  const int kc = p.ksize >> 1;
+
+  // per-thread A rows (pixel coordinates), fixed for the whole K loop
+  const int col4 = tid & 3;
+  int a_nb[A_LOADS], a_y[A_LOADS], a_x[A_LOADS];
+#pragma unroll
+  for (int i = 0; i < A_LOADS; ++i) {
+    const int m = m0 + (tid >> 2) + i * 64;
+    if (m < p.P) {
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W;
+      a_nb[i] = n * HW; a_y[i] = yy; a_x[i] = rem - yy * p.W;
+    } else {
+      a_nb[i] = -1; a_y[i] = 0; a_x[i] = 0;
+    }
+  }
+
+  float4 ra[A_LOADS], rb[B_LOADS];
+  auto load_stage = [&](int s) {
+    const int k = s * BK + col4 * 4;
+    int tap = 0, c = 0;
+    bool kin = k < p.K;
+    if (kin) { tap = k / p.Cin; c = k - tap * p.Cin; }
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    const int oy = (ky - kc) * p.dil * p.sign, ox = (kx - kc) * p.dil * p.sign;
+    const float* src; int ld, cc;
+    if (c < p.c0) { src = p.x0; ld = p.ldx0; cc = c; } else { src = p.x1; ld = p.ldx1; cc = c - p.c0; }
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int iy = a_y[i] + oy, ix = a_x[i] + ox;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kin && a_nb[i] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+        v = *reinterpret_cast<const float4*>(src + (size_t)(a_nb[i] + iy * p.W + ix) * ld + cc);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j) {
+      const int row = (tid >> 2) + j * B_ROWS_PER_PASS;
+      const int nn = n0 + row;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < BN && nn < p.Cout && kin)
+        v = *reinterpret_cast<const float4*>(p.w + (size_t)nn * p.K + k);
+      rb[j] = v;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* a = As + buf * BM * LDK;
+    float* b = Bs + buf * BN * LDK;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i)
+      *reinterpret_cast<float4*>(a + ((tid >> 2) + i * 64) * LDK + col4 * 4) = ra[i];
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j) {
+      const int row = (tid >> 2) + j * B_ROWS_PER_PASS;
+      if (row < BN) *reinterpret_cast<float4*>(b + row * LDK + col4 * 4) = rb[j];
+    }
+  };
+
+  floatx16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (p.K + BK - 1) / BK;
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load_stage(s + 1);
+    const float* a = As + buf * BM * LDK;
+    const float* b = Bs + buf * BN * LDK;
+    // two-level accumulation: each stage's 16-term MFMA chain starts from zero and is
+    // then added into the running sum, so fp32 rounding grows ~sqrt(16)+sqrt(K/16)
+    // instead of ~sqrt(K) (matches mkldnn's blocked accumulation accuracy)
+    floatx16 part[TI][TJ];
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int kk = g * 8 + lh * 4;
+      float4 av[TI], bv[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) av[i] = *reinterpret_cast<const float4*>(a + (wm0 + i * 32 + lr) * LDK + kk);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bv[j] = *reinterpret_cast<const float4*>(b + (wn0 + j * 32 + lr) * LDK + kk);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const floatx16 c0 = g == 0 ? floatx16{} : part[i][j];
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].x, bv[j].x, c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].y, bv[j].y, part[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].z, bv[j].z, part[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, part[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+    if (s + 1 < nsteps) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: bias, store, BN partial statistics -----------------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float v = acc[i][j][r] + bcol[j];
+        acc[i][j][r] = v;
+        if (row < p.P && col < p.Cout) {
+          float* dst = p.y + (size_t)row * p.ldy + col;
+          *dst = p.accumulate ? *dst + v : v;
+        }
+      }
+    }
+  if (p.stats == nullptr) return;
+
+  float* red = smem;  // [WM][BN] -- the K loop ended with a barrier, LDS is free
+  const int cnt = min(BM, p.P - m0);
+  float mean[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        s += (row < p.P) ? acc[i][j][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) s += red[w * BN + wn0 + j * 32 + lr];
+    mean[j] = s / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float d = acc[i][j][r] - mean[j];
+        s += (row < p.P) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+  if (wmi == 0 && lh == 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + cl];
+      if (col < p.Cout) p.stats[(size_t)mt * p.Cout + col] = make_float2(mean[j], s);
+    }
+  }
+}
+
+// ---------------------- forward v2: LDS-DMA staged, BK = 32 ----------------------
+// For Cin % 32 == 0 (every layer but enc1.conv1 fwd and out_conv2 dgrad).  Operand tiles
+// go HBM/L2 -> LDS with buffer_load ... lds (no VGPR staging, no ds_write): each wave
+// instruction fills 1 KiB lane-linearly; the 16-B chunk a lane fetches is pre-swizzled
+// on the SOURCE side (chunk c of row r sits in slot c ^ ((r>>1)&7)) so the ds_read_b128
+// operand reads are bank-conflict free.  Out-of-image taps (zero padding) and rows past
+// P / Cout use an out-of-range buffer offset: the hardware range check returns zeros.
+typedef int int32x4 __attribute__((ext_vector_type(4)));
+
+__device__ void llvm_raw_buffer_load_lds(int32x4 rsrc, __attribute__((address_space(3))) unsigned* lds, int size,
+                                         int voffset, int soffset, int offset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ int32x4 make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  int32x4 r;
+  r.x = (int)(unsigned)(a & 0xffffffffu);
+  r.y = (int)(unsigned)((a >> 32) & 0xffffu);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+
+constexpr int BK2 = 32;                 // k per stage (one tap, 32 channels)
+constexpr int ROW2 = BK2 * 4;           // 128-byte LDS rows
+constexpr unsigned OOB = 0x80000000u;   // beyond num_records -> zero fill
+
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+template <int BM, int BN, int WM, int WN, int HP>
+__global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int AI = BM / 32;   // A wave-instructions (1 KiB each) per wave per stage
+  constexpr int BI = BN / 32;   // B wave-instructions per wave per stage
+  constexpr int STAGE = (BM + BN) * ROW2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nbm * nbn);
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+  const int kc = p.ksize >> 1;
+
+  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
+  const int32x4 rsw = make_rsrc(p.w, (unsigned)((size_t)p.Cout * p.K * 4));
+
+  // per-lane A rows and chunks (fixed over the K loop)
+  int a_nb[AI], a_yx[AI], a_c[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int q = (wave * AI + i) * 64 + lane;
+    const int r = q >> 3;
+    a_c[i] = swz(r, q & 7) * 4;
+    const int m = m0 + r;
+    if (m < p.P) {
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W;
+      a_nb[i] = n * HW;
+      a_yx[i] = (yy << 16) | (rem - yy * p.W);
+    } else {
+      a_nb[i] = -1;
+      a_yx[i] = 0;
+    }
+  }
+  int b_off[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int q = (wave * BI + j) * 64 + lane;
+    const int r = q >> 3;
+    const int nn = n0 + r;
+    b_off[j] = nn < p.Cout ? (nn * p.K + swz(r, q & 7) * 4) * 4 : -1;
+  }
+
+  auto issue = [&](int s, int buf) {
+    const int k0 = s * BK2;
+    const int tap = k0 / p.Cin, ch0 = k0 - tap * p.Cin;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    const int dy = (ky - kc) * p.dil * p.sign, dx = (kx - kc) * p.dil * p.sign;
+    const bool second = ch0 >= p.c0;
+    const int32x4 rs = second ? rs1 : rs0;
+    const int ld = second ? p.ldx1 : p.ldx0;
+    const int cb = second ? ch0 - p.c0 : ch0;
+    char* abase = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int iy = (a_yx[i] >> 16) + dy, ix = (a_yx[i] & 0xffff) + dx;
+      const bool ok = a_nb[i] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      const unsigned off = ok ? (unsigned)(((a_nb[i] + iy * p.W + ix) * ld + cb + a_c[i]) * 4) : OOB;
+      llvm_raw_buffer_load_lds(rs, (__attribute__((address_space(3))) unsigned*)(abase + (wave * AI + i) * 1024),
+                               16, (int)off, 0, 0, 0);
+    }
+    char* bbase = abase + BM * ROW2;
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 4) : OOB;
+      llvm_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) unsigned*)(bbase + (wave * BI + j) * 1024),
+                               16, (int)off, 0, 0, 0);
+    }
+  };
+
+  floatx16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = p.K / BK2;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  issue(0, 0);
+  __syncthreads();
+  // two-level accumulation: an MFMA chain of HP stages (32*HP products) starts from zero
+  // and is then added into acc -- fp32 error ~sqrt(32 HP) + sqrt(K/(32 HP)) instead of
+  // ~sqrt(K); HP*32 ~ sqrt(K) balances both (mkldnn-level accuracy).
+  floatx16 part[TI][TJ];
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) issue(s + 1, buf ^ 1);
+    const char* a = lds + buf * STAGE;
+    const char* b = a + BM * ROW2;
+    const bool fresh = (s % HP) == 0;
+#pragma unroll
+    for (int g = 0; g < BK2 / 8; ++g) {
+      const int c = 2 * g + lh;
+      float4 av[TI], bv[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm0 + i * 32 + lr;
+        av[i] = *reinterpret_cast<const float4*>(a + r * ROW2 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 32 + lr;
+        bv[j] = *reinterpret_cast<const float4*>(b + r * ROW2 + swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const floatx16 c0 = (g == 0 && fresh) ? floatx16{} : part[i][j];
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].x, bv[j].x, c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].y, bv[j].y, part[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].z, bv[j].z, part[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, part[i][j], 0, 0, 0);
+        }
+    }
+    if ((s + 1) % HP == 0 || s + 1 == nsteps) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+    }
+    __syncthreads();  // hipcc emits vmcnt(0) here: the stage-(s+1) DMA has landed for every wave
+  }
+
+  // ---------------- epilogue: bias, store, BN partial statistics -----------------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float v = acc[i][j][r] + bcol[j];
+        acc[i][j][r] = v;
+        if (row < p.P && col < p.Cout) {
+          float* dst = p.y + (size_t)row * p.ldy + col;
+          *dst = p.accumulate ? *dst + v : v;
+        }
+      }
+    }
+  if (p.stats == nullptr) return;
+  float* red = smem;
+  const int cnt = min(BM, p.P - m0);
+  float mean[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        s += (row < p.P) ? acc[i][j][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) s += red[w * BN + wn0 + j * 32 + lr];
+    mean[j] = s / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float d = acc[i][j][r] - mean[j];
+        s += (row < p.P) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+  if (wmi == 0 && lh == 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + cl];
+      if (col < p.Cout) p.stats[(size_t)mt * p.Cout + col] = make_float2(mean[j], s);
+    }
+  }
+}
+
+// ------------------------------ weight gradient --------------------------------
+struct WgradParams {
+  const float* dy; int lddy;          // [P][Cout] view
+  const float* x0; int c0; int ldx0;  // forward input (virtual concat)
+  const float* x1; int c1; int ldx1;
+  float* part;                        // [splits][Cout][K]
+  int N, H, W, Cout, ksize, dil;
+  int P, K, Cin, chunk, splits;
+};
+
+constexpr int BKP = 16;  // pixels per stage
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int A_V4_ROW = BM / 4, B_V4_ROW = BN / 4;
+  constexpr int A_TOTAL = BKP * A_V4_ROW, B_TOTAL = BKP * B_V4_ROW;
+  constexpr int A_LOADS = (A_TOTAL + 255) / 256, B_LOADS = (B_TOTAL + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                    // [2][BKP][LDA]
+  float* Bs = smem + 2 * BKP * LDA;    // [2][BKP][LDB]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbm = (p.Cout + BM - 1) / BM, nbn = (p.K + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int split = blockIdx.x / ntile;
+  const int tile = blockIdx.x - split * ntile;
+  const int mt = tile / nbn, nt = tile - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = split * p.chunk;
+  const int pend = min(p.P, pbeg + p.chunk);
+  const int HW = p.H * p.W;
+  const int kc = p.ksize >> 1;
+
+  // B columns handled by this thread are fixed: decode (tap, channel source) once
+  int b_oy[B_LOADS], b_ox[B_LOADS], b_cc[B_LOADS], b_src[B_LOADS];
+  bool b_ok[B_LOADS];
+#pragma unroll
+  for (int j = 0; j < B_LOADS; ++j) {
+    const int e = tid + j * 256;
+    const int c4 = e % B_V4_ROW;
+    const int k = n0 + c4 * 4;
+    b_ok[j] = (e < B_TOTAL) && (k < p.K);
+    const int tap = b_ok[j] ? k / p.Cin : 0;
+    const int c = b_ok[j] ? k - tap * p.Cin : 0;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    b_oy[j] = (ky - kc) * p.dil; b_ox[j] = (kx - kc) * p.dil;
+    b_src[j] = c < p.c0 ? 0 : 1;
+    b_cc[j] = c < p.c0 ? c : c - p.c0;
+  }
+
+  float4 ra[A_LOADS], rb[B_LOADS];
+  auto load_stage = [&](int pbase) {
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int e = tid + i * 256;
+      const int c4 = e % A_V4_ROW, pr = e / A_V4_ROW;
+      const int px = pbase + pr, col = m0 + c4 * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < A_TOTAL && px < pend && col < p.Cout)
+        v = *reinterpret_cast<const float4*>(p.dy + (size_t)px * p.lddy + col);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j) {
+      const int e = tid + j * 256;
+      const int pr = e / B_V4_ROW;
+      const int px = pbase + pr;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (b_ok[j] && px < pend) {
+        const int n = px / HW, rem = px - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+        const int iy = yy + b_oy[j], ix = xx + b_ox[j];
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) {
+          const size_t q = (size_t)(n * HW + iy * p.W + ix);
+          v = b_src[j] == 0 ? *reinterpret_cast<const float4*>(p.x0 + q * p.ldx0 + b_cc[j])
+                            : *reinterpret_cast<const float4*>(p.x1 + q * p.ldx1 + b_cc[j]);
+        }
+      }
+      rb[j] = v;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* a = As + buf * BKP * LDA;
+    float* b = Bs + buf * BKP * LDB;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int e = tid + i * 256;
+      if (e < A_TOTAL) *reinterpret_cast<float4*>(a + (e / A_V4_ROW) * LDA + (e % A_V4_ROW) * 4) = ra[i];
+    }
+#pragma unroll
+    for (int j = 0; j < B_LOADS; ++j) {
+      const int e = tid + j * 256;
+      if (e < B_TOTAL) *reinterpret_cast<float4*>(b + (e / B_V4_ROW) * LDB + (e % B_V4_ROW) * 4) = rb[j];
+    }
+  };
+
+  floatx16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (pend - pbeg + BKP - 1) / BKP;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  if (nsteps > 0) {
+    load_stage(pbeg);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load_stage(pbeg + (s + 1) * BKP);
+    const float* a = As + buf * BKP * LDA;
+    const float* b = Bs + buf * BKP * LDB;
+#pragma unroll
+    for (int kq = 0; kq < BKP / 2; ++kq) {
+      const int kr = kq * 2 + lh;
+      float av[TI], bv[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) av[i] = a[kr * LDA + wm0 + i * 32 + lr];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bv[j] = b[kr * LDB + wn0 + j * 32 + lr];
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row < p.Cout && col < p.K) out[(size_t)row * p.K + col] = acc[i][j][r];
+      }
+    }
+}
+
+// sum the split-K slabs in fixed order, write dW in torch layout [Cout][Cin_real][k][k]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, int splits,
+                                    int cout, int cin, int cin_real, int taps, int accumulate) {
+  // iterate in slab (k-contiguous) order so the split reads coalesce; the transposed
+  // store into torch's [Cout][Cin][kh][kw] layout is the scattered side (written once)
+  // block = 64 consecutive slab elements x 4 split groups; fixed-order combine
+  __shared__ float red[4][64];
+  const long long K = (long long)taps * cin;
+  const long long total = (long long)cout * K;
+  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + el;
+  float s = 0.f;
+  if (e < total)
+    for (int q = grp; q < splits; q += 4) s += part[(size_t)q * cout * K + e];
+  red[grp][el] = s;
+  __syncthreads();
+  if (grp == 0 && e < total) {
+    const float v = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
+    const int n = (int)(e / K);
+    const int k = (int)(e - (long long)n * K);
+    const int t = k / cin, c = k - t * cin;
+    if (c < cin_real) {
+      const long long dst = ((long long)n * cin_real + c) * taps + t;
+      dw[dst] = accumulate ? dw[dst] + v : v;
+    }
+  }
+}
+
+// W[Cout][Cin_real][k][k] -> Wf[Cout][taps][Cin] and Wd[Cin][taps][Cout] (Cin >= Cin_real, zero pad)
+__global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wf, float* __restrict__ wd,
+                                    int cout, int cin, int cin_real, int taps) {
+  const long long total = (long long)cout * taps * cin;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % cin);
+    const long long r = e / cin;
+    const int t = (int)(r % taps);
+    const int n = (int)(r / taps);
+    const float v = c < cin_real ? w[((long long)n * cin_real + c) * taps + t] : 0.f;
+    if (wf) wf[e] = v;
+    if (wd) wd[((long long)c * taps + t) * cout + n] = v;
+  }
+}
+
+// -------------------------------- host side ------------------------------------
+template <int BM, int BN, int WM, int WN>
+static int launch_fwd(const ConvParams& p, hipStream_t st) {
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(float);
+  hipLaunchKernelGGL((conv_igemm_fwd_kernel<BM, BN, WM, WN>), dim3(nbm * nbn), dim3(256), lds, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd");
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int HP>
+static int launch_fwd_v2(const ConvParams& p, hipStream_t st) {
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const size_t lds = (size_t)2 * (BM + BN) * ROW2;
+  hipLaunchKernelGGL((conv_fwd_v2_kernel<BM, BN, WM, WN, HP>), dim3(nbm * nbn), dim3(256), lds, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd(v2)");
+  return 0;
+}
+
+// stages per partial MFMA chain (SRPDE_CONV_HP, tuning/diagnostics only; 1000 = no split)
+static int conv_hp() {
+  static int hp = [] {
+    const char* e = getenv("SRPDE_CONV_HP");
+    return e ? atoi(e) : 4;
+  }();
+  return hp;
+}
+
+static bool v2_ok(const ConvParams& p) {
+  const long long maxld = std::max(p.ldx0, p.c1 ? p.ldx1 : 0);
+  return p.c0 % 32 == 0 && p.c1 % 32 == 0 && (long long)p.P * maxld * 4 < (1LL << 31) &&
+         (long long)p.Cout * p.K * 4 < (1LL << 31);
+}
+
+static int fwd_config(int cout) { return cout % 128 == 0 ? 0 : (cout % 64 == 0 ? 1 : 2); }
+static int fwd_bm(int cfg) { return cfg == 0 ? 128 : 256; }
+
+template <int BM, int BN, int WM, int WN>
+static int launch_wgrad(const WgradParams& p, hipStream_t st) {
+  const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
+  const size_t lds = (size_t)2 * BKP * ((BM + 4) + (BN + 4)) * sizeof(float);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN>), dim3(nb), dim3(256), lds, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad");
+  return 0;
+}
+
+static void wgrad_tiles(int cout, int K, int* bm, int* bn) {
+  if (cout >= 128) { *bm = 128; *bn = 128; }
+  else if (cout >= 64) { *bm = 64; *bn = 256; }
+  else { *bm = 32; *bn = 256; }
+  (void)K;
+}
+
+static void wgrad_split(int P, int cout, int K, int* chunk, int* splits) {
+  int bm, bn;
+  wgrad_tiles(cout, K, &bm, &bn);
+  const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
+  long long want = (2048 + tiles - 1) / tiles;           // ~8 blocks per CU in flight
+  long long c = (P + want - 1) / want;
+  c = (c + BKP - 1) / BKP * BKP;
+  if (c < 256) c = 256;
+  *chunk = (int)c;
+  *splits = ceil_div(P, c);
+}
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+size_t srpde_conv_stats_blocks(int n, int h, int w, int cout) {
+  return (size_t)ceil_div((long long)n * h * w, fwd_bm(fwd_config(cout)));
+}
+
+int srpde_conv_stats_rows_per_block(int cout) { return fwd_bm(fwd_config(cout)); }
+
+int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1,
+                   const float* wpack, const float* bias, float* y, int ldy,
+                   int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
+                   float* stats, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x0 && wpack && y, "srpde_conv_fwd: null pointer");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd: bad shape");
+  SRPDE_CHECK_ARG(ksize == 1 || ksize == 3, "srpde_conv_fwd: ksize must be 1 or 3");
+  SRPDE_CHECK_ARG(sign == 1 || sign == -1, "srpde_conv_fwd: sign must be +-1");
+  SRPDE_CHECK_ARG(c0 % 4 == 0 && c1 % 4 == 0 && ldx0 % 4 == 0 && (c1 == 0 || ldx1 % 4 == 0),
+                  "srpde_conv_fwd: channel counts / strides must be multiples of 4 (c0=%d c1=%d)", c0, c1);
+  SRPDE_CHECK_ARG(c1 == 0 || x1 != nullptr, "srpde_conv_fwd: x1 null with c1>0");
+  SRPDE_CHECK_ARG(aligned16(x0) && aligned16(wpack) && (c1 == 0 || aligned16(x1)),
+                  "srpde_conv_fwd: inputs must be 16-byte aligned");
+  SRPDE_CHECK_ARG((long long)n * h * w < (1LL << 31), "srpde_conv_fwd: too many pixels");
+  ConvParams p;
+  p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0;
+  p.x1 = x1; p.c1 = c1; p.ldx1 = ldx1 > 0 ? ldx1 : 4;
+  p.w = wpack; p.bias = bias; p.y = y; p.ldy = ldy;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  if (v2_ok(p)) {
+    switch (fwd_config(cout)) {
+      case 0:
+        switch (conv_hp()) {
+          case 1: return launch_fwd_v2<128, 128, 2, 2, 1>(p, stream);
+          case 2: return launch_fwd_v2<128, 128, 2, 2, 2>(p, stream);
+          case 1000: return launch_fwd_v2<128, 128, 2, 2, 1000000>(p, stream);
+          default: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream);
+        }
+      case 1: return launch_fwd_v2<256, 64, 4, 1, 4>(p, stream);
+      default: return launch_fwd_v2<256, 32, 4, 1, 4>(p, stream);
+    }
+  }
+  switch (fwd_config(cout)) {
+    case 0: return launch_fwd<128, 128, 2, 2>(p, stream);
+    case 1: return launch_fwd<256, 64, 4, 1>(p, stream);
+    default: return launch_fwd<256, 32, 4, 1>(p, stream);
+  }
+}
+
+size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, int ksize) {
+  const int P = n * h * w, K = ksize * ksize * cin;
+  int chunk, splits;
+  wgrad_split(P, cout, K, &chunk, &splits);
+  return (size_t)splits * cout * K * sizeof(float);
+}
+
+int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                     int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
+                     int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dy && x0 && dw && workspace, "srpde_conv_wgrad: null pointer");
+  SRPDE_CHECK_ARG(c0 % 4 == 0 && c1 % 4 == 0 && lddy % 4 == 0 && ldx0 % 4 == 0 && cout % 4 == 0,
+                  "srpde_conv_wgrad: channel counts / strides must be multiples of 4");
+  SRPDE_CHECK_ARG(c1 == 0 || (x1 && ldx1 % 4 == 0), "srpde_conv_wgrad: bad x1");
+  SRPDE_CHECK_ARG(cin_real <= c0 + c1, "srpde_conv_wgrad: cin_real > cin");
+  WgradParams p;
+  p.dy = dy; p.lddy = lddy; p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0; p.x1 = x1; p.c1 = c1;
+  p.ldx1 = ldx1 > 0 ? ldx1 : 4;
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  wgrad_split(p.P, cout, p.K, &p.chunk, &p.splits);
+  const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
+  if (ws_bytes < need) {
+    set_error("srpde_conv_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  p.part = static_cast<float*>(workspace);
+  int bm, bn, rc;
+  wgrad_tiles(cout, p.K, &bm, &bn);
+  if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream);
+  else if (bm == 64) rc = launch_wgrad<64, 256, 1, 4>(p, stream);
+  else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
+  if (rc) return rc;
+  const int taps = ksize * ksize;
+  const long long total = (long long)cout * p.K;
+  const int blocks = (int)((total + 63) / 64);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, p.part, dw, p.splits, cout,
+                     p.Cin, cin_real, taps, accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce)");
+  return 0;
+}
+
+int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout, int cin, int cin_real, int ksize,
+                            hipStream_t stream) {
+  SRPDE_CHECK_ARG(w && (wfwd || wdgrad), "srpde_pack_conv_weights: null pointer");
+  SRPDE_CHECK_ARG(cin >= cin_real && cin % 4 == 0, "srpde_pack_conv_weights: bad cin");
+  const int taps = ksize * ksize;
+  const long long total = (long long)cout * taps * cin;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks), dim3(256), 0, stream, w, wfwd, wdgrad, cout, cin, cin_real,
+                     taps);
+  SRPDE_LAUNCH_CHECK("srpde_pack_conv_weights");
+  return 0;
+}
+
+}  // extern "C"

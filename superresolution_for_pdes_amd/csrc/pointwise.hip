@@ -1,0 +1,814 @@
+// Memory-bound U-Net ops for NHWC fp32 on gfx950: input staging, 2x2 max-pool,
+// bilinear x2 upsample (align_corners=True), attention gate, output head + residual,
+// MSE loss.  All reductions are deterministic (fixed-order partial sums, no atomics).
+//
+// Reference anchors (src/models.py): pool :69,:79-80; up :70,:89-93; AttentionGate
+// :103-130; final 1x1 + residual :61,:74,:98,:101; nn.MSELoss src/train_enhanced.py:307.
+#include "common.h"
+
+namespace srpde {
+
+// ------------------------------- input staging ---------------------------------
+// x NCHW [N][Cin][H][W] -> NHWC [N][H][W][Cpad] (extra channels zero)
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, float* __restrict__ out, int N, int Cin, int HW,
+                                    int Cpad) {
+  const long long total = (long long)N * HW;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long n = e / HW;
+    const int p = (int)(e - n * HW);
+    float* o = out + e * Cpad;
+    for (int c = 0; c < Cpad; ++c) o[c] = c < Cin ? x[(n * Cin + c) * HW + p] : 0.f;
+  }
+}
+
+// --------------------------------- max pool ------------------------------------
+// nn.MaxPool2d(2): first maximum in (0,0),(0,1),(1,0),(1,1) order wins (strict >), as aten.
+__global__ void maxpool2_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int ldo, int N,
+                                    int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C4 = C >> 2;
+  const long long total = (long long)N * Ho * Wo * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C4) * 4;
+    const long long q = e / C4;
+    const int ox = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int oy = (int)(t % Ho);
+    const long long n = t / Ho;
+    const long long p00 = (n * H + 2 * oy) * W + 2 * ox;
+    const float4 a = *reinterpret_cast<const float4*>(x + p00 * ldx + c);
+    const float4 b = *reinterpret_cast<const float4*>(x + (p00 + 1) * ldx + c);
+    const float4 d = *reinterpret_cast<const float4*>(x + (p00 + W) * ldx + c);
+    const float4 f = *reinterpret_cast<const float4*>(x + (p00 + W + 1) * ldx + c);
+    float4 m;
+#define MX(X) { float v = a.X; if (b.X > v) v = b.X; if (d.X > v) v = d.X; if (f.X > v) v = f.X; m.X = v; }
+    MX(x) MX(y) MX(z) MX(w)
+#undef MX
+    *reinterpret_cast<float4*>(out + q * ldo + c) = m;
+  }
+}
+
+__global__ void maxpool2_bwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ dout, int lddo,
+                                    float* __restrict__ dx, int lddx, int N, int H, int W, int C, int accumulate) {
+  const int Ho = H >> 1, Wo = W >> 1, C4 = C >> 2;
+  const long long total = (long long)N * Ho * Wo * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C4) * 4;
+    const long long q = e / C4;
+    const int ox = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int oy = (int)(t % Ho);
+    const long long n = t / Ho;
+    const long long p[4] = {(n * H + 2 * oy) * W + 2 * ox, (n * H + 2 * oy) * W + 2 * ox + 1,
+                            (n * H + 2 * oy + 1) * W + 2 * ox, (n * H + 2 * oy + 1) * W + 2 * ox + 1};
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(x + p[k] * ldx + c);
+    const float4 g = *reinterpret_cast<const float4*>(dout + q * lddo + c);
+    float4 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (accumulate) o[k] = *reinterpret_cast<const float4*>(dx + p[k] * lddx + c);
+      else o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#define ARG(X)                                                     \
+  {                                                                \
+    int am = 0; float mv = v[0].X;                                 \
+    if (v[1].X > mv) { mv = v[1].X; am = 1; }                      \
+    if (v[2].X > mv) { mv = v[2].X; am = 2; }                      \
+    if (v[3].X > mv) { mv = v[3].X; am = 3; }                      \
+    o[am].X += g.X;                                                \
+  }
+    ARG(x) ARG(y) ARG(z) ARG(w)
+#undef ARG
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(dx + p[k] * lddx + c) = o[k];
+  }
+}
+
+// ----------------------------- bilinear upsample x2 ------------------------------
+// align_corners=True: src = dst * (in-1)/(out-1) (float, as aten area_pixel_compute_scale),
+// i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
+struct Lerp { int i0, i1; float l0, l1; };
+__device__ __forceinline__ Lerp lerp_index(int o, int in, int out) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float src = scale * (float)o;
+  Lerp r;
+  r.i0 = (int)src;
+  r.i1 = r.i0 + (r.i0 < in - 1 ? 1 : 0);
+  r.l1 = src - (float)r.i0;
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+__global__ void upsample_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int ldo, int N,
+                                    int H, int W, int Ho, int Wo, int C) {
+  const int C4 = C >> 2;
+  const long long total = (long long)N * Ho * Wo * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C4) * 4;
+    const long long q = e / C4;
+    const int ox = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int oy = (int)(t % Ho);
+    const long long n = t / Ho;
+    const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
+    const float* base = x + n * H * W * (long long)ldx;
+    const float4 a = *reinterpret_cast<const float4*>(base + ((long long)ly.i0 * W + lx.i0) * ldx + c);
+    const float4 b = *reinterpret_cast<const float4*>(base + ((long long)ly.i0 * W + lx.i1) * ldx + c);
+    const float4 d = *reinterpret_cast<const float4*>(base + ((long long)ly.i1 * W + lx.i0) * ldx + c);
+    const float4 f = *reinterpret_cast<const float4*>(base + ((long long)ly.i1 * W + lx.i1) * ldx + c);
+    float4 o;
+#define UP(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
+    UP(x) UP(y) UP(z) UP(w)
+#undef UP
+    *reinterpret_cast<float4*>(out + q * ldo + c) = o;
+  }
+}
+
+// scalar-channel variant (any C): single-channel fields of PDEDataset / the cascade
+__global__ void upsample_fwd_scalar_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int ldo,
+                                           int N, int H, int W, int Ho, int Wo, int C) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long q = e / C;
+    const int ox = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int oy = (int)(t % Ho);
+    const long long n = t / Ho;
+    const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
+    const float* base = x + n * H * W * (long long)ldx + c;
+    const float a = base[((long long)ly.i0 * W + lx.i0) * ldx], b = base[((long long)ly.i0 * W + lx.i1) * ldx];
+    const float d = base[((long long)ly.i1 * W + lx.i0) * ldx], f = base[((long long)ly.i1 * W + lx.i1) * ldx];
+    out[q * ldo + c] = ly.l0 * (lx.l0 * a + lx.l1 * b) + ly.l1 * (lx.l0 * d + lx.l1 * f);
+  }
+}
+
+// backward as a deterministic gather: every input pixel sums the output pixels whose
+// 4-tap stencil touches it (scale < 1 => at most ~5 candidates per axis).
+__device__ __forceinline__ int gather_weights(int i, int in, int out, int* idx, float* wt) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  int lo = 0, hi = out - 1;
+  if (scale > 0.f) {
+    lo = max(0, (int)floorf((float)(i - 1) / scale) - 1);
+    hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
+  }
+  int cnt = 0;
+  for (int o = lo; o <= hi && cnt < 8; ++o) {
+    const Lerp l = lerp_index(o, in, out);
+    float w = 0.f;
+    if (l.i0 == i) w += l.l0;
+    if (l.i1 == i) w += l.l1;
+    if (l.i0 == i || l.i1 == i) { idx[cnt] = o; wt[cnt] = w; ++cnt; }
+  }
+  return cnt;
+}
+
+__global__ void upsample_bwd_kernel(const float* __restrict__ dout, int lddo, float* __restrict__ dx, int lddx,
+                                    int N, int H, int W, int Ho, int Wo, int C, int accumulate) {
+  const int C4 = C >> 2;
+  const long long total = (long long)N * H * W * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C4) * 4;
+    const long long q = e / C4;
+    const int ix = (int)(q % W);
+    const long long t = q / W;
+    const int iy = (int)(t % H);
+    const long long n = t / H;
+    int oyi[8], oxi[8];
+    float wy[8], wx[8];
+    const int ny = gather_weights(iy, H, Ho, oyi, wy);
+    const int nx = gather_weights(ix, W, Wo, oxi, wx);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* base = dout + n * Ho * Wo * (long long)lddo;
+    for (int a = 0; a < ny; ++a) {
+      float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int b = 0; b < nx; ++b) {
+        const float4 g = *reinterpret_cast<const float4*>(base + ((long long)oyi[a] * Wo + oxi[b]) * lddo + c);
+        r.x += wx[b] * g.x; r.y += wx[b] * g.y; r.z += wx[b] * g.z; r.w += wx[b] * g.w;
+      }
+      s.x += wy[a] * r.x; s.y += wy[a] * r.y; s.z += wy[a] * r.z; s.w += wy[a] * r.w;
+    }
+    float* o = dx + q * lddx + c;
+    if (accumulate) {
+      const float4 old = *reinterpret_cast<const float4*>(o);
+      s.x += old.x; s.y += old.y; s.z += old.z; s.w += old.w;
+    }
+    *reinterpret_cast<float4*>(o) = s;
+  }
+}
+
+// ------------------------------- attention gate ----------------------------------
+// channel branch: m = mean_hw(x); h = relu(W1 m + b1); ca = sigmoid(W2 h + b2)  (models.py:106-112)
+// one block per sample
+__global__ __launch_bounds__(256) void att_channel_fwd_kernel(const float* __restrict__ x, int ldx, int HW, int C,
+                                                              int Cr, const float* __restrict__ w1,
+                                                              const float* __restrict__ b1,
+                                                              const float* __restrict__ w2,
+                                                              const float* __restrict__ b2, float* __restrict__ m,
+                                                              float* __restrict__ h, float* __restrict__ ca) {
+  extern __shared__ float sh[];  // [256*4] partials, then m[C], h[Cr]
+  const int n = blockIdx.x, C4 = C >> 2;
+  const int c4 = threadIdx.x % C4, r0 = threadIdx.x / C4, rs = blockDim.x / C4;
+  const int active = C4 * rs;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((int)threadIdx.x < active) {
+    const float* base = x + (long long)n * HW * ldx + c4 * 4;
+    for (int p = r0; p < HW; p += rs) {
+      const float4 v = *reinterpret_cast<const float4*>(base + (long long)p * ldx);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  float4* red = reinterpret_cast<float4*>(sh);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  float* ms = sh + 4 * 256;
+  float* hs = ms + C;
+  if ((int)threadIdx.x < C4) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red[r * C4 + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    const float inv = 1.f / (float)HW;
+    const int c = threadIdx.x * 4;
+    ms[c] = t.x * inv; ms[c + 1] = t.y * inv; ms[c + 2] = t.z * inv; ms[c + 3] = t.w * inv;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) m[(long long)n * C + j] = ms[j];
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float a = b1[r];
+    for (int c = 0; c < C; ++c) a += w1[r * C + c] * ms[c];
+    a = fmaxf(a, 0.f);
+    hs[r] = a;
+    h[(long long)n * Cr + r] = a;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = b2[c];
+    for (int r = 0; r < Cr; ++r) a += w2[c * Cr + r] * hs[r];
+    ca[(long long)n * C + c] = 1.f / (1.f + expf(-a));
+  }
+}
+
+// spatial branch: sa[p] = sigmoid(sum_c g[p][c] wg[c] + bg), 8 lanes per pixel  (models.py:114-117)
+__global__ __launch_bounds__(256) void att_spatial_fwd_kernel(const float* __restrict__ g, int ldg, long long P,
+                                                              int G, const float* __restrict__ wg,
+                                                              const float* __restrict__ bg, float* __restrict__ sa) {
+  const int sub = threadIdx.x & 7;
+  for (long long p = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 3; p < P;
+       p += ((long long)gridDim.x * blockDim.x) >> 3) {
+    float acc = 0.f;
+    const float* row = g + p * ldg;
+    for (int c = sub * 4; c < G; c += 32) {
+      const float4 v = *reinterpret_cast<const float4*>(row + c);
+      const float4 w = *reinterpret_cast<const float4*>(wg + c);
+      acc += v.x * w.x + v.y * w.y + v.z * w.z + v.w * w.w;
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (sub == 0) sa[p] = 1.f / (1.f + expf(-(acc + bg[0])));
+  }
+}
+
+// out[p][c] = (x[p][c] * ca[n][c]) * sa[p]   (models.py:122, :128)
+__global__ void att_apply_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ ca,
+                                 const float* __restrict__ sa, float* __restrict__ out, int ldo, long long P, int HW,
+                                 int C) {
+  const int C4 = C >> 2;
+  const long long total = P * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / C4;
+    const int c = (int)(e - p * C4) * 4;
+    const long long n = p / HW;
+    const float4 v = *reinterpret_cast<const float4*>(x + p * ldx + c);
+    const float4 a = *reinterpret_cast<const float4*>(ca + n * C + c);
+    const float s = sa[p];
+    float4 o;
+    o.x = (v.x * a.x) * s; o.y = (v.y * a.y) * s; o.z = (v.z * a.z) * s; o.w = (v.w * a.w) * s;
+    *reinterpret_cast<float4*>(out + p * ldo + c) = o;
+  }
+}
+
+// backward, pass 1 (per pixel): dsa_pre[p] = sigmoid'(sa) * sum_c dout * (x * ca)
+__global__ __launch_bounds__(256) void att_bwd_pixel_kernel(const float* __restrict__ dout, int lddo,
+                                                            const float* __restrict__ x, int ldx,
+                                                            const float* __restrict__ ca,
+                                                            const float* __restrict__ sa, long long P, int HW, int C,
+                                                            float* __restrict__ dsa_pre) {
+  const int sub = threadIdx.x & 7;
+  for (long long p = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 3; p < P;
+       p += ((long long)gridDim.x * blockDim.x) >> 3) {
+    const long long n = p / HW;
+    float acc = 0.f;
+    for (int c = sub * 4; c < C; c += 32) {
+      const float4 d = *reinterpret_cast<const float4*>(dout + p * lddo + c);
+      const float4 v = *reinterpret_cast<const float4*>(x + p * ldx + c);
+      const float4 a = *reinterpret_cast<const float4*>(ca + n * C + c);
+      acc += d.x * (v.x * a.x) + d.y * (v.y * a.y) + d.z * (v.z * a.z) + d.w * (v.w * a.w);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (sub == 0) {
+      const float s = sa[p];
+      dsa_pre[p] = acc * (1.f - s) * s;
+    }
+  }
+}
+
+// backward, pass 2 (one block per sample): dca[c] = sum_hw dout*sa*x; MLP backward;
+// writes dm[n][c] (grad of the spatial mean) and per-sample weight-grad rows.
+__global__ __launch_bounds__(256) void att_bwd_channel_kernel(
+    const float* __restrict__ dout, int lddo, const float* __restrict__ x, int ldx, const float* __restrict__ sa,
+    int HW, int C, int Cr, const float* __restrict__ w1, const float* __restrict__ w2, const float* __restrict__ m,
+    const float* __restrict__ h, const float* __restrict__ ca, float* __restrict__ dm,
+    float* __restrict__ dw1_rows, float* __restrict__ db1_rows, float* __restrict__ dw2_rows,
+    float* __restrict__ db2_rows) {
+  extern __shared__ float sh[];
+  const int n = blockIdx.x, C4 = C >> 2;
+  const int c4 = threadIdx.x % C4, r0 = threadIdx.x / C4, rs = blockDim.x / C4;
+  const int active = C4 * rs;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if ((int)threadIdx.x < active) {
+    const long long pb = (long long)n * HW;
+    for (int p = r0; p < HW; p += rs) {
+      const float4 d = *reinterpret_cast<const float4*>(dout + (pb + p) * lddo + c4 * 4);
+      const float4 v = *reinterpret_cast<const float4*>(x + (pb + p) * ldx + c4 * 4);
+      const float q = sa[pb + p];
+      s.x += (d.x * q) * v.x; s.y += (d.y * q) * v.y; s.z += (d.z * q) * v.z; s.w += (d.w * q) * v.w;
+    }
+  }
+  float4* red = reinterpret_cast<float4*>(sh);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  float* dpre = sh + 4 * 256;  // [C] grad of pre-sigmoid channel logits
+  float* dh = dpre + C;        // [Cr]
+  if ((int)threadIdx.x < C4) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red[r * C4 + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    const int c = threadIdx.x * 4;
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = ca[(long long)n * C + c + k];
+      dpre[c + k] = tv[k] * (1.f - a) * a;
+    }
+  }
+  __syncthreads();
+  // per-sample vectors only; the weight grads are batch reductions (outer_sum_kernel)
+  for (int c = threadIdx.x; c < C; c += blockDim.x) db2_rows[(long long)n * C + c] = dpre[c];
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float a = 0.f;
+    for (int c = 0; c < C; ++c) a += w2[c * Cr + r] * dpre[c];
+    a = h[(long long)n * Cr + r] > 0.f ? a : 0.f;
+    dh[r] = a;
+    db1_rows[(long long)n * Cr + r] = a;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f;
+    for (int r = 0; r < Cr; ++r) a += w1[r * C + c] * dh[r];
+    dm[(long long)n * C + c] = a / (float)HW;
+  }
+}
+
+// backward, pass 3 (elementwise): dx = (dout*sa)*ca + dm[n][c]  (write or accumulate)
+__global__ void att_bwd_dx_kernel(const float* __restrict__ dout, int lddo, const float* __restrict__ ca,
+                                  const float* __restrict__ sa, const float* __restrict__ dm, float* __restrict__ dx,
+                                  int lddx, long long P, int HW, int C, int accumulate) {
+  const int C4 = C >> 2;
+  const long long total = P * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / C4;
+    const int c = (int)(e - p * C4) * 4;
+    const long long n = p / HW;
+    const float4 d = *reinterpret_cast<const float4*>(dout + p * lddo + c);
+    const float4 a = *reinterpret_cast<const float4*>(ca + n * C + c);
+    const float4 g = *reinterpret_cast<const float4*>(dm + n * C + c);
+    const float s = sa[p];
+    float4 o;
+    o.x = (d.x * s) * a.x + g.x; o.y = (d.y * s) * a.y + g.y;
+    o.z = (d.z * s) * a.z + g.z; o.w = (d.w * s) * a.w + g.w;
+    float* dst = dx + p * lddx + c;
+    if (accumulate) {
+      const float4 old = *reinterpret_cast<const float4*>(dst);
+      o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+    }
+    *reinterpret_cast<float4*>(dst) = o;
+  }
+}
+
+// backward, gating: dg[p][c] (+)= dsa_pre[p] * wg[c]
+__global__ void att_bwd_gating_kernel(const float* __restrict__ dsa_pre, const float* __restrict__ wg,
+                                      float* __restrict__ dg, int lddg, long long P, int G, int accumulate) {
+  const int G4 = G >> 2;
+  const long long total = P * G4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / G4;
+    const int c = (int)(e - p * G4) * 4;
+    const float s = dsa_pre[p];
+    const float4 w = *reinterpret_cast<const float4*>(wg + c);
+    float4 o = make_float4(s * w.x, s * w.y, s * w.z, s * w.w);
+    float* dst = dg + p * lddg + c;
+    if (accumulate) {
+      const float4 old = *reinterpret_cast<const float4*>(dst);
+      o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+    }
+    *reinterpret_cast<float4*>(dst) = o;
+  }
+}
+
+// column partial sums of v[p][c]*s[p] over a row block, plus sum s[p] in column C (float2 .x).
+// Used for the spatial-gate weight grad (v = gating, s = dsa_pre) and for the head (v = z, s = dout).
+__global__ __launch_bounds__(256) void weighted_colsum_kernel(const float* __restrict__ v, int ldv,
+                                                              const float* __restrict__ s, long long P, int C,
+                                                              int rows_per_blk, float2* __restrict__ part) {
+  extern __shared__ float4 red4[];
+  const int C4 = C >> 2;
+  const int c4 = threadIdx.x % C4, r0 = threadIdx.x / C4, rs = blockDim.x / C4;
+  const int active = C4 * rs;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float sacc = 0.f;
+  const long long pb = (long long)blockIdx.x * rows_per_blk;
+  const long long pe = min(P, pb + rows_per_blk);
+  if ((int)threadIdx.x < active) {
+    for (long long p = pb + r0; p < pe; p += rs) {
+      const float4 a = *reinterpret_cast<const float4*>(v + p * ldv + c4 * 4);
+      const float w = s[p];
+      acc.x += a.x * w; acc.y += a.y * w; acc.z += a.z * w; acc.w += a.w * w;
+      if (c4 == 0) sacc += w;
+    }
+  }
+  red4[threadIdx.x] = acc;
+  red4[256 + threadIdx.x] = make_float4(sacc, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if ((int)threadIdx.x < C4) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ts = 0.f;
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red4[r * C4 + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+      if (threadIdx.x == 0) ts += red4[256 + r * C4].x;
+    }
+    float2* o = part + (size_t)blockIdx.x * (C + 1);
+    const int c = threadIdx.x * 4;
+    o[c] = make_float2(t.x, 0.f); o[c + 1] = make_float2(t.y, 0.f);
+    o[c + 2] = make_float2(t.z, 0.f); o[c + 3] = make_float2(t.w, 0.f);
+    if (threadIdx.x == 0) o[C] = make_float2(ts, 0.f);
+  }
+}
+
+// out[i][j] = sum_n a[n][i] * b[n][j]  (a or b null => 1): the 1x1 channel-MLP weight and
+// bias grads as batch reductions.  grid (la, ceil(lb/64)), 1024 threads = 64 j-lanes x 16
+// sample groups, fp64 partials combined in fixed order (deterministic).
+__global__ __launch_bounds__(1024) void outer_sum_kernel(const float* __restrict__ a, int la,
+                                                         const float* __restrict__ b, int lb, int n,
+                                                         float* __restrict__ out) {
+  __shared__ double red[16][64];
+  const int i = blockIdx.x, jl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = blockIdx.y * 64 + jl;
+  double s = 0.0;
+  if (j < lb) {
+    for (int k = grp; k < n; k += 16) {
+      const double av = a ? (double)a[(long long)k * la + i] : 1.0;
+      const double bv = b ? (double)b[(long long)k * lb + j] : 1.0;
+      s += av * bv;
+    }
+  }
+  red[grp][jl] = s;
+  __syncthreads();
+  if (grp == 0 && j < lb) {
+    double t = 0.0;
+    for (int g = 0; g < 16; ++g) t += red[g][jl];
+    out[(long long)i * lb + j] = (float)t;
+  }
+}
+
+// fixed-order fp64 sum of rows [n][len] -> out[len]  (per-sample bias-grad rows)
+__global__ void rowsum_kernel(const float* __restrict__ rows, int n, int len, float* __restrict__ out, int stride_in,
+                              int accumulate) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= len) return;
+  double s = 0.0;
+  for (int k = 0; k < n; ++k) s += rows[(long long)k * stride_in + j];
+  out[j] = accumulate ? out[j] + (float)s : (float)s;
+}
+
+// fp64 sums over blocks of float2 partials [nblk][len] (.x) -> out[len]
+__global__ void partsum_kernel(const float2* __restrict__ part, int nblk, int len, float* __restrict__ out) {
+  const int j = blockIdx.x;
+  __shared__ double a[256];
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 256) s += part[(size_t)k * len + j].x;
+  a[threadIdx.x] = s;
+  __syncthreads();
+  for (int t = 128; t > 0; t >>= 1) {
+    if ((int)threadIdx.x < t) a[threadIdx.x] += a[threadIdx.x + t];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = (float)a[0];
+}
+
+// -------------------------------- output head ------------------------------------
+// out[p] = (bf + sum_c z[p][c] wf[c]) + x_in[n][0][p]   (final 1x1 conv + residual)
+__global__ void head_fwd_kernel(const float* __restrict__ z, int ldz, int C, const float* __restrict__ wf,
+                                const float* __restrict__ bf, const float* __restrict__ xin, int xin_c, int HW,
+                                long long P, float* __restrict__ out) {
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < P; p += (long long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int c = 0; c < C; c += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(z + p * ldz + c);
+      acc += v.x * wf[c] + v.y * wf[c + 1] + v.z * wf[c + 2] + v.w * wf[c + 3];
+    }
+    const long long n = p / HW;
+    const int q = (int)(p - n * HW);
+    out[p] = (acc + bf[0]) + xin[(n * xin_c) * HW + q];
+  }
+}
+
+// dz[p][c] = dout[p] * wf[c]
+__global__ void head_bwd_dz_kernel(const float* __restrict__ dout, const float* __restrict__ wf, int C,
+                                   float* __restrict__ dz, int lddz, long long P) {
+  const int C4 = C >> 2;
+  const long long total = P * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long p = e / C4;
+    const int c = (int)(e - p * C4) * 4;
+    const float d = dout[p];
+    *reinterpret_cast<float4*>(dz + p * lddz + c) = make_float4(d * wf[c], d * wf[c + 1], d * wf[c + 2], d * wf[c + 3]);
+  }
+}
+
+// ----------------------------------- MSE ------------------------------------------
+__global__ __launch_bounds__(256) void mse_partial_kernel(const float* __restrict__ y, const float* __restrict__ t,
+                                                          long long n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float d = y[i] - t[i];
+    s += (double)(d * d);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void mse_final_kernel(const double* __restrict__ part, int nblk, long long n, float* __restrict__ loss) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 256) s += part[k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] / (double)n);
+}
+
+// dy = 2 (y - t) / n * gout
+__global__ void mse_bwd_kernel(const float* __restrict__ y, const float* __restrict__ t, long long n,
+                               const float* __restrict__ gout, float* __restrict__ dy) {
+  const float g = gout ? gout[0] : 1.f;
+  const float norm = 2.f / (float)n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dy[i] = norm * (y[i] - t[i]) * g;
+}
+
+static int grid_for(long long total, int cap = 8192) {
+  long long b = (total + 255) / 256;
+  if (b < 1) b = 1;
+  return (int)std::min<long long>(b, cap);
+}
+
+static int colsum_blocks(long long P, int C, int* rpb) {
+  const int rs = 256 / (C >> 2);
+  long long r = (P + 1023) / 1024;
+  r = (r + rs - 1) / rs * rs;
+  if (r < rs) r = rs;
+  *rpb = (int)r;
+  return (int)((P + r - 1) / r);
+}
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w, int cpad, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && out && cpad >= cin, "srpde_nchw_to_nhwc: bad args");
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)n * h * w)), dim3(256), 0, stream, x, out, n, cin,
+                     h * w, cpad);
+  SRPDE_LAUNCH_CHECK("srpde_nchw_to_nhwc");
+  return 0;
+}
+
+int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int c,
+                         hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && out && c % 4 == 0 && h % 2 == 0 && w % 2 == 0, "srpde_maxpool2x2_fwd: bad args");
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for((long long)n * (h / 2) * (w / 2) * (c / 4))), dim3(256), 0,
+                     stream, x, ldx, out, ldo, n, h, w, c);
+  SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_fwd");
+  return 0;
+}
+
+int srpde_maxpool2x2_bwd(const float* x, int ldx, const float* dout, int lddo, float* dx, int lddx, int n, int h,
+                         int w, int c, int accumulate, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && dout && dx && c % 4 == 0 && h % 2 == 0 && w % 2 == 0, "srpde_maxpool2x2_bwd: bad args");
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)n * (h / 2) * (w / 2) * (c / 4))), dim3(256), 0,
+                     stream, x, ldx, dout, lddo, dx, lddx, n, h, w, c, accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_bwd");
+  return 0;
+}
+
+int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho, int wo,
+                                int c, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && out && c > 0, "srpde_upsample_bilinear_fwd: bad args");
+  if (c % 4 != 0 || ldx % 4 != 0 || ldo % 4 != 0) {
+    hipLaunchKernelGGL(upsample_fwd_scalar_kernel, dim3(grid_for((long long)n * ho * wo * c)), dim3(256), 0, stream,
+                       x, ldx, out, ldo, n, h, w, ho, wo, c);
+    SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
+    return 0;
+  }
+  hipLaunchKernelGGL(upsample_fwd_kernel, dim3(grid_for((long long)n * ho * wo * (c / 4))), dim3(256), 0, stream, x,
+                     ldx, out, ldo, n, h, w, ho, wo, c);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
+  return 0;
+}
+
+int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
+                                int wo, int c, int accumulate, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && dx && c % 4 == 0 && ho >= h && wo >= w, "srpde_upsample_bilinear_bwd: bad args");
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for((long long)n * h * w * (c / 4))), dim3(256), 0, stream, dout,
+                     lddo, dx, lddx, n, h, w, ho, wo, c, accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd");
+  return 0;
+}
+
+int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,
+                  const float* b1, const float* w2, const float* b2, const float* wg, const float* bg, float* m,
+                  float* hbuf, float* ca, float* sa, float* out, int ldo, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && g && w1 && b1 && w2 && b2 && wg && bg && m && hbuf && ca && sa && out,
+                  "srpde_att_fwd: null");
+  SRPDE_CHECK_ARG(c % 32 == 0 && gc % 4 == 0 && c <= 1024, "srpde_att_fwd: channel counts");
+  const int cr = c / 8;
+  const size_t lds = (4 * 256 + c + cr) * sizeof(float);
+  hipLaunchKernelGGL(att_channel_fwd_kernel, dim3(n), dim3(256), lds, stream, x, ldx, hw, c, cr, w1, b1, w2, b2, m,
+                     hbuf, ca);
+  SRPDE_LAUNCH_CHECK("srpde_att_fwd(channel)");
+  const long long P = (long long)n * hw;
+  hipLaunchKernelGGL(att_spatial_fwd_kernel, dim3(grid_for(P * 8)), dim3(256), 0, stream, g, ldg, P, gc, wg, bg, sa);
+  SRPDE_LAUNCH_CHECK("srpde_att_fwd(spatial)");
+  hipLaunchKernelGGL(att_apply_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, x, ldx, ca, sa, out, ldo,
+                     P, hw, c);
+  SRPDE_LAUNCH_CHECK("srpde_att_fwd(apply)");
+  return 0;
+}
+
+size_t srpde_att_bwd_workspace_size(int n, int hw, int c, int gc) {
+  const long long P = (long long)n * hw;
+  const int cr = c / 8;
+  int rpb;
+  const int nb = colsum_blocks(P, gc, &rpb);
+  size_t f = (size_t)P                          // dsa_pre
+             + (size_t)n * c                    // dm
+             + (size_t)n * cr * c * 2           // dw1 rows, dw2 rows
+             + (size_t)n * (cr + c)             // db1, db2 rows
+             + (size_t)nb * (gc + 1) * 2;       // float2 partials
+  return f * sizeof(float) + 256;
+}
+
+int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const float* g, int ldg, int n, int hw,
+                  int c, int gc, const float* w1, const float* w2, const float* wg, const float* m, const float* hbuf,
+                  const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
+                  int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
+                  void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && x && g && dx && dg && workspace, "srpde_att_bwd: null");
+  SRPDE_CHECK_ARG(c % 32 == 0 && gc % 4 == 0, "srpde_att_bwd: channel counts");
+  if (ws_bytes < srpde_att_bwd_workspace_size(n, hw, c, gc)) {
+    set_error("srpde_att_bwd: workspace too small");
+    return kErrWorkspace;
+  }
+  const long long P = (long long)n * hw;
+  const int cr = c / 8;
+  float* dsa = static_cast<float*>(workspace);
+  float* dm = dsa + P;
+  float* dw1r = dm + (size_t)n * c;
+  float* dw2r = dw1r + (size_t)n * cr * c;
+  float* db1r = dw2r + (size_t)n * cr * c;
+  float* db2r = db1r + (size_t)n * cr;
+  float2* part = reinterpret_cast<float2*>(db2r + (size_t)n * c + 2);
+  part = reinterpret_cast<float2*>((reinterpret_cast<uintptr_t>(part) + 15) & ~uintptr_t(15));
+
+  hipLaunchKernelGGL(att_bwd_pixel_kernel, dim3(grid_for(P * 8)), dim3(256), 0, stream, dout, lddo, x, ldx, ca, sa,
+                     P, hw, c, dsa);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(pixel)");
+  const size_t lds = (4 * 256 + c + cr) * sizeof(float);
+  hipLaunchKernelGGL(att_bwd_channel_kernel, dim3(n), dim3(256), lds, stream, dout, lddo, x, ldx, sa, hw, c, cr, w1,
+                     w2, m, hbuf, ca, dm, dw1r, db1r, dw2r, db2r);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(channel)");
+  hipLaunchKernelGGL(att_bwd_dx_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, lddo, ca, sa, dm,
+                     dx, lddx, P, hw, c, dx_accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(dx)");
+  hipLaunchKernelGGL(att_bwd_gating_kernel, dim3(grid_for(P * (gc / 4))), dim3(256), 0, stream, dsa, wg, dg, lddg, P,
+                     gc, dg_accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(gating)");
+  // parameter grads: fixed-order sums over samples / pixel blocks
+  (void)dw1r; (void)dw2r;
+  // dW1[r][c] = sum_n dh[n][r] m[n][c];  dW2[c][r] = sum_n dpre[n][c] h[n][r]
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(cr, ceil_div(c, 64)), dim3(1024), 0, stream, db1r, cr, m, c, n, dw1);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(c, ceil_div(cr, 64)), dim3(1024), 0, stream, db2r, c, hbuf, cr, n, dw2);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(cr, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
+                     db1r, cr, n, db1);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(c, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
+                     db2r, c, n, db2);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(rowsum)");
+  int rpb;
+  const int nb = colsum_blocks(P, gc, &rpb);
+  hipLaunchKernelGGL(weighted_colsum_kernel, dim3(nb), dim3(256), 2 * 256 * sizeof(float4), stream, g, ldg, dsa, P,
+                     gc, rpb, part);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(colsum)");
+  hipLaunchKernelGGL(partsum_kernel, dim3(gc), dim3(256), 0, stream, part, nb, gc + 1, dwg);
+  hipLaunchKernelGGL(partsum_kernel, dim3(1), dim3(256), 0, stream, part + gc, nb, gc + 1, dbg);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd(partsum)");
+  return 0;
+}
+
+int srpde_head_fwd(const float* z, int ldz, int c, const float* wf, const float* bf, const float* xin, int xin_c,
+                   int n, int hw, float* out, hipStream_t stream) {
+  SRPDE_CHECK_ARG(z && wf && bf && xin && out && c % 4 == 0, "srpde_head_fwd: bad args");
+  const long long P = (long long)n * hw;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(P)), dim3(256), 0, stream, z, ldz, c, wf, bf, xin, xin_c, hw, P,
+                     out);
+  SRPDE_LAUNCH_CHECK("srpde_head_fwd");
+  return 0;
+}
+
+size_t srpde_head_bwd_workspace_size(int n, int hw, int c) {
+  int rpb;
+  const int nb = colsum_blocks((long long)n * hw, c, &rpb);
+  return (size_t)nb * (c + 1) * sizeof(float2);
+}
+
+int srpde_head_bwd(const float* dout, const float* z, int ldz, int c, const float* wf, int n, int hw, float* dz,
+                   int lddz, float* dwf, float* dbf, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && z && wf && dz && dwf && dbf && workspace && c % 4 == 0, "srpde_head_bwd: bad args");
+  if (ws_bytes < srpde_head_bwd_workspace_size(n, hw, c)) {
+    set_error("srpde_head_bwd: workspace too small");
+    return kErrWorkspace;
+  }
+  const long long P = (long long)n * hw;
+  hipLaunchKernelGGL(head_bwd_dz_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, wf, c, dz, lddz, P);
+  SRPDE_LAUNCH_CHECK("srpde_head_bwd(dz)");
+  int rpb;
+  const int nb = colsum_blocks(P, c, &rpb);
+  float2* part = static_cast<float2*>(workspace);
+  hipLaunchKernelGGL(weighted_colsum_kernel, dim3(nb), dim3(256), 2 * 256 * sizeof(float4), stream, z, ldz, dout, P,
+                     c, rpb, part);
+  hipLaunchKernelGGL(partsum_kernel, dim3(c), dim3(256), 0, stream, part, nb, c + 1, dwf);
+  hipLaunchKernelGGL(partsum_kernel, dim3(1), dim3(256), 0, stream, part + c, nb, c + 1, dbf);
+  SRPDE_LAUNCH_CHECK("srpde_head_bwd(reduce)");
+  return 0;
+}
+
+size_t srpde_mse_workspace_size(void) { return 1024 * sizeof(double); }
+
+int srpde_mse_fwd(const float* y, const float* t, long long n, float* loss, void* workspace, size_t ws_bytes,
+                  hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && t && loss && workspace && ws_bytes >= 1024 * sizeof(double), "srpde_mse_fwd: bad args");
+  const int nb = (int)std::min<long long>(1024, std::max<long long>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(mse_partial_kernel, dim3(nb), dim3(256), 0, stream, y, t, n, static_cast<double*>(workspace));
+  hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(256), 0, stream, static_cast<const double*>(workspace), nb, n,
+                     loss);
+  SRPDE_LAUNCH_CHECK("srpde_mse_fwd");
+  return 0;
+}
+
+int srpde_mse_bwd(const float* y, const float* t, long long n, const float* gout, float* dy, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && t && dy, "srpde_mse_bwd: bad args");
+  hipLaunchKernelGGL(mse_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, stream, y, t, n, gout, dy);
+  SRPDE_LAUNCH_CHECK("srpde_mse_bwd");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,350 @@
+// Batched matrix-free conjugate-gradient Poisson solver (fp64) for gfx950.
+//
+// Reference: PoissonSolver._create_laplacian + solve_poisson (src/data_generation.py:35-58,
+// :79-104) assemble diag(theta) @ L (5-point, all n^2 nodes are unknowns, zero ghost ring
+// outside the grid, h = 1/(n-1)) and call scipy spsolve (SuperLU).  theta only scales rows,
+// so the system is equivalent to the SPD problem
+//           (-L) u = -f / theta
+// which is solved here by CG on a matrix-free stencil, for B independent problems at once.
+//
+// * n <= 128  : one workgroup per problem; the search direction p (with its zero ghost
+//               ring) lives in LDS, x / r / q stay in registers (NPT points per lane);
+//               3 barriers per iteration, deterministic fixed-order block reductions.
+// * n  > 128  : grid CG, 2 launches per iteration (A: beta, p <- r + beta p, q = A p, <p,q>
+//               partials;  B: alpha, x += alpha p, r -= alpha A p, <r,r> partials); every
+//               block re-reduces the previous launch's partials in the same order, so all
+//               blocks agree on alpha/beta without a grid barrier or host round trip.
+//               A sticky per-problem `done` flag makes extra launches no-ops.
+#include "common.h"
+
+namespace srpde {
+
+constexpr int CG_MAXT = 1024;
+
+__device__ __forceinline__ double block_sum_uniform(double v, double* slots) {
+  // every thread returns the same value (fixed reduction order)
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) slots[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < nw; ++k) s += slots[k];
+  return s;
+}
+
+template <int NPT>
+__global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restrict__ f,
+                                                         const double* __restrict__ theta, double* __restrict__ u,
+                                                         int n, double rtol, int maxit, int* __restrict__ iters,
+                                                         double* __restrict__ resid) {
+  extern __shared__ double sp[];
+  const int N2 = n * n, ld = n + 2;
+  double* pl = sp;                       // (n+2)^2
+  double* slotA = sp + ld * ld;          // 16
+  double* slotB = slotA + 16;            // 16
+  const size_t off = (size_t)blockIdx.x * N2;
+  const double inv_h2 = (double)(n - 1) * (double)(n - 1);
+  const int T = blockDim.x;
+
+  for (int e = threadIdx.x; e < ld * ld; e += T) pl[e] = 0.0;
+  double x[NPT], r[NPT], p[NPT], q[NPT];
+  int li[NPT];
+  double rr_l = 0.0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = threadIdx.x + k * T;
+    x[k] = 0.0; q[k] = 0.0;
+    if (i < N2) {
+      const int yy = i / n, xx = i - yy * n;
+      li[k] = (yy + 1) * ld + xx + 1;
+      r[k] = -f[off + i] / theta[off + i];
+    } else {
+      li[k] = -1;
+      r[k] = 0.0;
+    }
+    p[k] = r[k];
+    rr_l += r[k] * r[k];
+  }
+  __syncthreads();  // ghost ring zeroed before interior writes
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (li[k] >= 0) pl[li[k]] = p[k];
+  double rr = block_sum_uniform(rr_l, slotB);  // includes a barrier: p visible
+  const double stop = rtol * rtol * rr;
+  int it = 0;
+  while (rr > stop && it < maxit) {
+    double pq_l = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (li[k] >= 0) {
+        const int c = li[k];
+        q[k] = (4.0 * p[k] - pl[c - 1] - pl[c + 1] - pl[c - ld] - pl[c + ld]) * inv_h2;
+        pq_l += p[k] * q[k];
+      }
+    }
+    const double pq = block_sum_uniform(pq_l, slotA);
+    const double alpha = rr / pq;
+    double rr_n = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      x[k] += alpha * p[k];
+      r[k] -= alpha * q[k];
+      rr_n += r[k] * r[k];
+    }
+    const double rrn = block_sum_uniform(rr_n, slotB);
+    const double beta = rrn / rr;
+    rr = rrn;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      p[k] = r[k] + beta * p[k];
+      if (li[k] >= 0) pl[li[k]] = p[k];
+    }
+    __syncthreads();
+    ++it;
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = threadIdx.x + k * T;
+    if (i < N2) u[off + i] = x[k];
+  }
+  if (threadIdx.x == 0) {
+    if (iters) iters[blockIdx.x] = it;
+    if (resid) resid[blockIdx.x] = sqrt(rr / (stop > 0.0 ? stop / (rtol * rtol) : 1.0));
+  }
+}
+
+// ------------------------------- grid CG (n > 128) --------------------------------
+struct GridCG {
+  double *x, *r, *p0, *p1;  // [B][N2]
+  double *rrp0, *rrp1, *pqp, *bbp;  // [B][nb]
+  int* done;    // [B]
+  int* iters;   // [B]
+  int n, nb, B;
+  double rtol;
+};
+
+constexpr int GCG_T = 256, GCG_NPT = 4, GCG_PTS = GCG_T * GCG_NPT;
+
+__device__ __forceinline__ double sum_parts(const double* part, int nb, double* sh) {
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) s += part[k];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double t = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ void write_part(double v, double* sh, double* dst) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+    *dst = t;
+  }
+}
+
+__global__ __launch_bounds__(GCG_T) void gcg_init_kernel(const double* __restrict__ f,
+                                                         const double* __restrict__ theta, GridCG g) {
+  __shared__ double sh[8];
+  const int b = blockIdx.y, N2 = g.n * g.n;
+  const size_t off = (size_t)b * N2;
+  double s = 0.0;
+  for (int k = 0; k < GCG_NPT; ++k) {
+    const int i = blockIdx.x * GCG_PTS + k * GCG_T + threadIdx.x;
+    if (i < N2) {
+      const double rv = -f[off + i] / theta[off + i];
+      g.x[off + i] = 0.0; g.r[off + i] = rv; g.p0[off + i] = 0.0; g.p1[off + i] = 0.0;
+      s += rv * rv;
+    }
+  }
+  write_part(s, sh, g.rrp0 + (size_t)b * g.nb + blockIdx.x);
+  if (threadIdx.x == 0) g.bbp[(size_t)b * g.nb + blockIdx.x] = 0.0;  // filled by copy below
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.done[b] = 0; g.iters[b] = 0; }
+}
+
+__global__ void gcg_copy_bb_kernel(GridCG g) {
+  const int b = blockIdx.y;
+  for (int k = threadIdx.x; k < g.nb; k += blockDim.x) g.bbp[(size_t)b * g.nb + k] = g.rrp0[(size_t)b * g.nb + k];
+}
+
+// launch A of iteration k
+__global__ __launch_bounds__(GCG_T) void gcg_a_kernel(GridCG g, int k, int maxit) {
+  __shared__ double sh[8];
+  const int b = blockIdx.y, n = g.n, N2 = n * n;
+  if (g.done[b]) return;
+  const double* rr_cur = (k & 1) ? g.rrp1 : g.rrp0;
+  const double* rr_old = (k & 1) ? g.rrp0 : g.rrp1;
+  const double rr = sum_parts(rr_cur + (size_t)b * g.nb, g.nb, sh);
+  const double bb = sum_parts(g.bbp + (size_t)b * g.nb, g.nb, sh);
+  if (rr <= g.rtol * g.rtol * bb || k >= maxit) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) { g.done[b] = 1; g.iters[b] = k; }
+    return;
+  }
+  const double beta = k == 0 ? 0.0 : rr / sum_parts(rr_old + (size_t)b * g.nb, g.nb, sh);
+  const size_t off = (size_t)b * N2;
+  const double* po = ((k & 1) ? g.p1 : g.p0) + off;
+  double* pn = ((k & 1) ? g.p0 : g.p1) + off;
+  const double* rv = g.r + off;
+  const double inv_h2 = (double)(n - 1) * (double)(n - 1);
+  double s = 0.0;
+  for (int kk = 0; kk < GCG_NPT; ++kk) {
+    const int i = blockIdx.x * GCG_PTS + kk * GCG_T + threadIdx.x;
+    if (i < N2) {
+      const int yy = i / n, xx = i - yy * n;
+      auto pv = [&](int j) { return rv[j] + beta * po[j]; };
+      const double pc = pv(i);
+      double nb = 0.0;
+      if (xx > 0) nb += pv(i - 1);
+      if (xx < n - 1) nb += pv(i + 1);
+      if (yy > 0) nb += pv(i - n);
+      if (yy < n - 1) nb += pv(i + n);
+      const double qv = (4.0 * pc - nb) * inv_h2;
+      pn[i] = pc;
+      s += pc * qv;
+    }
+  }
+  write_part(s, sh, g.pqp + (size_t)b * g.nb + blockIdx.x);
+}
+
+// launch B of iteration k
+__global__ __launch_bounds__(GCG_T) void gcg_b_kernel(GridCG g, int k) {
+  __shared__ double sh[8];
+  const int b = blockIdx.y, n = g.n, N2 = n * n;
+  if (g.done[b]) return;
+  const double* rr_cur = (k & 1) ? g.rrp1 : g.rrp0;
+  double* rr_next = (k & 1) ? g.rrp0 : g.rrp1;
+  const double rr = sum_parts(rr_cur + (size_t)b * g.nb, g.nb, sh);
+  const double pq = sum_parts(g.pqp + (size_t)b * g.nb, g.nb, sh);
+  const double alpha = rr / pq;
+  const size_t off = (size_t)b * N2;
+  const double* pn = ((k & 1) ? g.p0 : g.p1) + off;
+  double* xv = g.x + off;
+  double* rv = g.r + off;
+  const double inv_h2 = (double)(n - 1) * (double)(n - 1);
+  double s = 0.0;
+  for (int kk = 0; kk < GCG_NPT; ++kk) {
+    const int i = blockIdx.x * GCG_PTS + kk * GCG_T + threadIdx.x;
+    if (i < N2) {
+      const int yy = i / n, xx = i - yy * n;
+      double nb = 0.0;
+      if (xx > 0) nb += pn[i - 1];
+      if (xx < n - 1) nb += pn[i + 1];
+      if (yy > 0) nb += pn[i - n];
+      if (yy < n - 1) nb += pn[i + n];
+      const double pc = pn[i];
+      const double qv = (4.0 * pc - nb) * inv_h2;
+      xv[i] += alpha * pc;
+      const double rn = rv[i] - alpha * qv;
+      rv[i] = rn;
+      s += rn * rn;
+    }
+  }
+  write_part(s, sh, rr_next + (size_t)b * g.nb + blockIdx.x);
+}
+
+__global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restrict__ iters, int maxit) {
+  const int b = blockIdx.y, N2 = g.n * g.n;
+  const size_t off = (size_t)b * N2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N2; i += gridDim.x * blockDim.x) u[off + i] = g.x[off + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && iters) iters[b] = g.done[b] ? g.iters[b] : maxit;
+}
+
+static GridCG carve(void* ws, int B, int n) {
+  GridCG g;
+  const size_t N2 = (size_t)n * n;
+  g.n = n; g.B = B; g.nb = (int)((N2 + GCG_PTS - 1) / GCG_PTS);
+  double* d = static_cast<double*>(ws);
+  g.x = d; d += B * N2;
+  g.r = d; d += B * N2;
+  g.p0 = d; d += B * N2;
+  g.p1 = d; d += B * N2;
+  g.rrp0 = d; d += (size_t)B * g.nb;
+  g.rrp1 = d; d += (size_t)B * g.nb;
+  g.pqp = d; d += (size_t)B * g.nb;
+  g.bbp = d; d += (size_t)B * g.nb;
+  g.done = reinterpret_cast<int*>(d);
+  g.iters = g.done + B;
+  g.rtol = 0.0;
+  return g;
+}
+
+static size_t grid_ws_bytes(int B, int n) {
+  const size_t N2 = (size_t)n * n;
+  const size_t nb = (N2 + GCG_PTS - 1) / GCG_PTS;
+  return (4 * B * N2 + 4 * (size_t)B * nb) * sizeof(double) + 2 * (size_t)B * sizeof(int) + 64;
+}
+
+static int lds_npt(int n) { return n <= 24 ? 4 : (n <= 80 ? 8 : 16); }
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+int srpde_poisson_lds_max_n(void) { return 128; }
+
+size_t srpde_poisson_workspace_size(int B, int n) { return n <= 128 ? 0 : grid_ws_bytes(B, n); }
+
+int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
+                         int* iters, double* resid, hipStream_t stream) {
+  SRPDE_CHECK_ARG(f && theta && u && B > 0 && n >= 2 && n <= 128, "srpde_poisson_cg_lds: bad args (n<=128)");
+  const int npt = lds_npt(n);
+  int T = ceil_div((long long)n * n, npt);
+  T = (T + 63) / 64 * 64;
+  SRPDE_CHECK_ARG(T <= CG_MAXT, "srpde_poisson_cg_lds: n too large");
+  const size_t lds = ((size_t)(n + 2) * (n + 2) + 32) * sizeof(double);
+  switch (npt) {
+    case 4: hipLaunchKernelGGL(cg_lds_kernel<4>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
+    case 8: hipLaunchKernelGGL(cg_lds_kernel<8>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
+    default: hipLaunchKernelGGL(cg_lds_kernel<16>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
+  }
+  SRPDE_LAUNCH_CHECK("srpde_poisson_cg_lds");
+  return 0;
+}
+
+int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,
+                               hipStream_t stream) {
+  SRPDE_CHECK_ARG(f && theta && ws && B > 0 && n >= 2, "srpde_poisson_cg_grid_init: bad args");
+  if (ws_bytes < grid_ws_bytes(B, n)) { set_error("srpde_poisson_cg_grid_init: workspace too small"); return kErrWorkspace; }
+  GridCG g = carve(ws, B, n);
+  hipLaunchKernelGGL(gcg_init_kernel, dim3(g.nb, B), dim3(GCG_T), 0, stream, f, theta, g);
+  hipLaunchKernelGGL(gcg_copy_bb_kernel, dim3(1, B), dim3(256), 0, stream, g);
+  SRPDE_LAUNCH_CHECK("srpde_poisson_cg_grid_init");
+  return 0;
+}
+
+int srpde_poisson_cg_grid_iterate(int B, int n, double rtol, int k_begin, int k_count, int maxit, void* ws,
+                                  size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(ws && ws_bytes >= grid_ws_bytes(B, n), "srpde_poisson_cg_grid_iterate: bad workspace");
+  GridCG g = carve(ws, B, n);
+  g.rtol = rtol;
+  for (int k = k_begin; k < k_begin + k_count; ++k) {
+    hipLaunchKernelGGL(gcg_a_kernel, dim3(g.nb, B), dim3(GCG_T), 0, stream, g, k, maxit);
+    hipLaunchKernelGGL(gcg_b_kernel, dim3(g.nb, B), dim3(GCG_T), 0, stream, g, k);
+  }
+  SRPDE_LAUNCH_CHECK("srpde_poisson_cg_grid_iterate");
+  return 0;
+}
+
+// byte offset of the int32 done-flag vector [B] inside the workspace: lets the host poll convergence
+size_t srpde_poisson_cg_grid_done_offset(int B, int n) {
+  return (size_t)(reinterpret_cast<char*>(carve(nullptr, B, n).done) - static_cast<char*>(nullptr));
+}
+
+int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit, void* ws, size_t ws_bytes,
+                                 hipStream_t stream) {
+  SRPDE_CHECK_ARG(u && ws && ws_bytes >= grid_ws_bytes(B, n), "srpde_poisson_cg_grid_finish: bad args");
+  GridCG g = carve(ws, B, n);
+  const int nbx = std::min(ceil_div((long long)n * n, 256), 1024);
+  hipLaunchKernelGGL(gcg_finish_kernel, dim3(nbx, B), dim3(256), 0, stream, g, u, iters, maxit);
+  SRPDE_LAUNCH_CHECK("srpde_poisson_cg_grid_finish");
+  return 0;
+}
+
+}  // extern "C"

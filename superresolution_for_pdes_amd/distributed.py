@@ -1,0 +1,137 @@
+"""Data-parallel training over RCCL (torch.distributed backend "nccl" == RCCL on ROCm).
+
+New relative to the reference (which is single-process): one process per
+GPU, each rank runs the HIP U-Net on its own minibatch shard, and the flat gradient
+buffer is all-reduced in buckets *while the backward is still running*:
+
+* the executor writes gradients into one flat buffer laid out in backward-completion
+  order (unet_exec.FLAT_GROUPS), and calls ``ready(offset)`` whenever a module group's
+  gradients are final -- a growing prefix;
+* ``GradReducer`` records an event on the compute stream, makes its side stream wait on
+  it, and issues ``all_reduce`` of every finished ``bucket_bytes`` chunk on that side
+  stream, so RCCL traffic over xGMI overlaps the remaining dgrad/wgrad kernels;
+* ``finish()`` flushes the tail and makes the compute stream wait for the side stream.
+
+Averaging uses ReduceOp.AVG on RCCL (SUM + scale on gloo, which lacks AVG), so the
+gradients handed back to autograd are the global mean, exactly what a single process
+with the concatenated batch would see for a sum-decomposable loss.  BatchNorm stays
+per-rank (the reference has no SyncBN); running statistics are broadcast from rank 0
+each step (``broadcast_buffers``), as torch DDP does by default.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class GradReducer:
+    def __init__(self, process_group=None, bucket_bytes: int = 8 << 20):
+        self.pg = process_group
+        self.bucket = max(1, bucket_bytes // 4)
+        self.world = dist.get_world_size(process_group)
+        self.backend = dist.get_backend(process_group)
+        self.use_avg = self.backend == "nccl"
+        self.flat = None
+        self.launched = 0
+        self.works = []
+        self.stream = None
+        self.n_buckets = 0
+
+    def _side_stream(self, dev):
+        if dev.type != "cuda":
+            return None
+        if self.stream is None or self.stream.device != dev:
+            self.stream = torch.cuda.Stream(device=dev)
+        return self.stream
+
+    def begin(self, flat):
+        self.flat = flat
+        self.launched = 0
+        self.works = []
+        self.n_buckets = 0
+
+    def _launch(self, lo, hi):
+        chunk = self.flat[lo:hi]
+        st = self._side_stream(self.flat.device)
+        if st is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.flat.device))
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
+                op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+                self.works.append((dist.all_reduce(chunk, op=op, group=self.pg, async_op=True), chunk))
+        else:
+            self.works.append((dist.all_reduce(chunk, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), chunk))
+        self.n_buckets += 1
+
+    def ready(self, upto: int):
+        while upto - self.launched >= self.bucket:
+            self._launch(self.launched, self.launched + self.bucket)
+            self.launched += self.bucket
+
+    def finish(self):
+        total = self.flat.numel()
+        if self.launched < total:
+            self._launch(self.launched, total)
+            self.launched = total
+        cur = torch.cuda.current_stream(self.flat.device) if self.flat.is_cuda else None
+        for work, chunk in self.works:
+            if cur is not None:
+                with torch.cuda.stream(self.stream):
+                    work.wait()
+            else:
+                work.wait()
+            if not self.use_avg:
+                chunk.div_(self.world)
+        if cur is not None:
+            cur.wait_stream(self.stream)
+        self.works = []
+
+
+class DataParallel(torch.nn.Module):
+    """Wrap a UNet for one-process-per-GPU data parallelism (replaces nothing in the
+    reference; see module docstring).  ``forward`` broadcasts BN buffers from rank 0 and
+    runs the wrapped model; its backward all-reduces gradients bucket by bucket."""
+
+    def __init__(self, module, process_group=None, bucket_bytes: int = 8 << 20, broadcast_buffers: bool = True):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.broadcast_buffers = broadcast_buffers
+        module._grad_reducer = GradReducer(process_group, bucket_bytes)
+        self._sync_params()
+
+    @torch.no_grad()
+    def _sync_params(self):
+        for p in self.module.parameters():
+            dist.broadcast(p.data, 0, group=self.pg)
+        self._sync_buffers()
+
+    @torch.no_grad()
+    def _sync_buffers(self):
+        bufs = [b for b in self.module.buffers()]
+        if not bufs:
+            return
+        flat = torch.cat([b.reshape(-1).to(torch.float64) for b in bufs])
+        dist.broadcast(flat, 0, group=self.pg)
+        off = 0
+        for b in bufs:
+            b.copy_(flat[off:off + b.numel()].view_as(b).to(b.dtype))
+            off += b.numel()
+
+    def forward(self, x):
+        if self.broadcast_buffers and self.module.training and dist.get_world_size(self.pg) > 1:
+            self._sync_buffers()
+        return self.module(x)
+
+
+def shard_indices(n: int, rank: int, world: int, seed: int, epoch: int = 0, shuffle: bool = True):
+    """DistributedSampler semantics: a seeded permutation padded to a multiple of world,
+    rank r takes elements r, r+world, ...  (every rank sees n_per_rank samples)."""
+    g = torch.Generator().manual_seed(seed + epoch)
+    idx = torch.randperm(n, generator=g) if shuffle else torch.arange(n)
+    per = (n + world - 1) // world
+    total = per * world
+    if total > n:
+        idx = torch.cat([idx, idx[: total - n]])
+    return idx[rank:total:world]

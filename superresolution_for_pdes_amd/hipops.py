@@ -1,0 +1,234 @@
+"""Thin torch-tensor wrappers over the C ABI (include/srpde.h).
+
+Activations are 2-D ``[P, C]`` fp32 tensor *views* of NHWC memory (P = N*H*W): a view's
+``data_ptr()`` and ``stride(0)`` are exactly the (pointer, ld) pair the kernels take,
+so channel slices of a wider buffer (virtual concat, gradient slices) cost nothing.
+No function here computes anything on the host; all math runs in libsrpde_hip.so.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, query, stream_ptr
+
+F32 = torch.float32
+
+
+def _pl(t):
+    """(pointer, ld) of a 2-D row-major view."""
+    assert t.dim() == 2 and (t.stride(1) == 1 or t.shape[1] == 1), "expected a [P, C] row-major view"
+    assert t.dtype == F32 and t.is_cuda, "expected a CUDA fp32 tensor"
+    return t.data_ptr(), t.stride(0)
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def empty(*shape, device):
+    return torch.empty(*shape, dtype=F32, device=device)
+
+
+# ---------------------------------- convolution ------------------------------------
+def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
+    cout, cin_real, kh, _ = w.shape
+    taps = kh * kh
+    wf = empty(cout * taps * cin_pad, device=w.device) if want_fwd else None
+    wd = empty(cout * taps * cin_pad, device=w.device) if want_dgrad else None
+    call("srpde_pack_conv_weights", w.data_ptr(), _p(wf), _p(wd), cout, cin_pad, cin_real, kh, stream_ptr())
+    return wf, wd
+
+
+def conv_stats_buffer(n, h, w, cout, device):
+    nblk = int(query("srpde_conv_stats_blocks", n, h, w, cout))
+    return empty(nblk, cout, 2, device=device), nblk, int(query("srpde_conv_stats_rows_per_block", cout))
+
+
+def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None):
+    p0, ld0 = _pl(x0)
+    if x1 is not None:
+        p1, ld1 = _pl(x1)
+        c1 = x1.shape[1]
+    else:
+        p1, ld1, c1 = 0, 0, 0
+    py, ldy = _pl(y)
+    call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
+         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), stream_ptr())
+
+
+def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
+    cout = dy.shape[1]
+    pdy, lddy = _pl(dy)
+    p0, ld0 = _pl(x0)
+    if x1 is not None:
+        p1, ld1 = _pl(x1)
+        c1 = x1.shape[1]
+    else:
+        p1, ld1, c1 = 0, 0, 0
+    cin = x0.shape[1] + c1
+    cin_real = dw.shape[1]
+    ws_bytes = int(query("srpde_conv_wgrad_workspace_size", n, h, w, cout, cin, ksize))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dy.device)
+    call("srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1, dw.data_ptr(), cin_real,
+         int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
+
+
+# ---------------------------------- batch norm -------------------------------------
+def bn_train_finalize(stats, nblk, rows_per_blk, P, running_mean, running_var, nbt, momentum, eps):
+    C = stats.shape[1]
+    mean = empty(C, device=stats.device)
+    invstd = empty(C, device=stats.device)
+    call("srpde_bn_train_finalize", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
+         _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), stream_ptr())
+    return mean, invstd
+
+
+def bn_eval_prepare(running_mean, running_var, eps):
+    C = running_mean.numel()
+    mean = empty(C, device=running_mean.device)
+    invstd = empty(C, device=running_mean.device)
+    call("srpde_bn_eval_prepare", running_mean.data_ptr(), running_var.data_ptr(), C, float(eps),
+         mean.data_ptr(), invstd.data_ptr(), stream_ptr())
+    return mean, invstd
+
+
+def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True):
+    py, ldy = _pl(y)
+    po, ldo = _pl(out)
+    call("srpde_bn_relu_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         po, ldo, y.shape[0], y.shape[1], int(relu), stream_ptr())
+
+
+def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True):
+    P, C = y.shape
+    py, ldy = _pl(y)
+    pda, ldda = _pl(da)
+    pdy, lddy = _pl(dy)
+    ws_bytes = int(query("srpde_bn_relu_bwd_workspace_size", P, C))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
+    call("srpde_bn_relu_bwd", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), pdy, lddy, _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), ws.data_ptr(), ws_bytes,
+         stream_ptr())
+
+
+# ------------------------------ pool / upsample / misc -----------------------------
+def nchw_to_nhwc(x, cpad):
+    n, c, h, w = x.shape
+    out = empty(n * h * w, cpad, device=x.device)
+    call("srpde_nchw_to_nhwc", x.data_ptr(), out.data_ptr(), n, c, h, w, cpad, stream_ptr())
+    return out
+
+
+def maxpool_fwd(x, n, h, w):
+    c = x.shape[1]
+    out = empty(n * (h // 2) * (w // 2), c, device=x.device)
+    px, ldx = _pl(x)
+    call("srpde_maxpool2x2_fwd", px, ldx, out.data_ptr(), c, n, h, w, c, stream_ptr())
+    return out
+
+
+def maxpool_bwd(x, dout, dx, n, h, w, accumulate):
+    px, ldx = _pl(x)
+    pdo, lddo = _pl(dout)
+    pdx, lddx = _pl(dx)
+    call("srpde_maxpool2x2_bwd", px, ldx, pdo, lddo, pdx, lddx, n, h, w, x.shape[1], int(accumulate), stream_ptr())
+
+
+def upsample_fwd(x, n, h, w, ho, wo, out=None):
+    c = x.shape[1]
+    if out is None:
+        out = empty(n * ho * wo, c, device=x.device)
+    px, ldx = _pl(x)
+    po, ldo = _pl(out)
+    call("srpde_upsample_bilinear_fwd", px, ldx, po, ldo, n, h, w, ho, wo, c, stream_ptr())
+    return out
+
+
+def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate):
+    pdo, lddo = _pl(dout)
+    pdx, lddx = _pl(dx)
+    call("srpde_upsample_bilinear_bwd", pdo, lddo, pdx, lddx, n, h, w, ho, wo, dx.shape[1], int(accumulate),
+         stream_ptr())
+
+
+# ----------------------------------- attention -------------------------------------
+def att_fwd(x, g, n, hw, w1, b1, w2, b2, wg, bg, out=None):
+    c, gc = x.shape[1], g.shape[1]
+    dev = x.device
+    m = empty(n, c, device=dev)
+    hb = empty(n, c // 8, device=dev)
+    ca = empty(n, c, device=dev)
+    sa = empty(n * hw, device=dev)
+    if out is None:
+        out = empty(n * hw, c, device=dev)
+    px, ldx = _pl(x)
+    pg, ldg = _pl(g)
+    po, ldo = _pl(out)
+    call("srpde_att_fwd", px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+         b2.data_ptr(), wg.data_ptr(), bg.data_ptr(), m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(),
+         po, ldo, stream_ptr())
+    return out, (m, hb, ca, sa)
+
+
+def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg):
+    m, hb, ca, sa = saved
+    c, gc = x.shape[1], g.shape[1]
+    ws_bytes = int(query("srpde_att_bwd_workspace_size", n, hw, c, gc))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+    pdo, lddo = _pl(dout)
+    px, ldx = _pl(x)
+    pg, ldg = _pl(g)
+    pdx, lddx = _pl(dx)
+    pdg, lddg = _pl(dg)
+    call("srpde_att_bwd", pdo, lddo, px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), w2.data_ptr(), wg.data_ptr(),
+         m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(), pdx, lddx, int(dx_acc), pdg, lddg, int(dg_acc),
+         dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr(),
+         ws.data_ptr(), ws_bytes, stream_ptr())
+
+
+# ------------------------------------- head ----------------------------------------
+def head_fwd(z, wf, bf, xin, n, hw):
+    out = empty(n * hw, device=z.device)
+    pz, ldz = _pl(z)
+    call("srpde_head_fwd", pz, ldz, z.shape[1], wf.data_ptr(), bf.data_ptr(), xin.data_ptr(), xin.shape[1],
+         n, hw, out.data_ptr(), stream_ptr())
+    return out
+
+
+def head_bwd(dout, z, wf, n, hw, dz, dwf, dbf):
+    pz, ldz = _pl(z)
+    pdz, lddz = _pl(dz)
+    c = z.shape[1]
+    ws_bytes = int(query("srpde_head_bwd_workspace_size", n, hw, c))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=z.device)
+    call("srpde_head_bwd", dout.data_ptr(), pz, ldz, c, wf.data_ptr(), n, hw, pdz, lddz, dwf.data_ptr(),
+         dbf.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
+
+
+# -------------------------------------- MSE ----------------------------------------
+def mse_fwd(y, t):
+    ws_bytes = int(query("srpde_mse_workspace_size"))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
+    loss = torch.empty((), dtype=F32, device=y.device)
+    call("srpde_mse_fwd", y.data_ptr(), t.data_ptr(), y.numel(), loss.data_ptr(), ws.data_ptr(), ws_bytes,
+         stream_ptr())
+    return loss
+
+
+def mse_bwd(y, t, gout):
+    dy = torch.empty_like(y)
+    call("srpde_mse_bwd", y.data_ptr(), t.data_ptr(), y.numel(), _p(gout), dy.data_ptr(), stream_ptr())
+    return dy
+
+
+# ----------------------------------- optimizer -------------------------------------
+def clip_coef(flat_grad, grad_scale, max_norm, coef):
+    ws_bytes = int(query("srpde_grad_norm_workspace_size"))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=flat_grad.device)
+    call("srpde_clip_coef", flat_grad.data_ptr(), flat_grad.numel(), float(grad_scale), float(max_norm),
+         coef.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
+
+
+def adamw_step(p, g, m, v, lr, beta1, beta2, eps, wd, step, coef, grad_scale):
+    call("srpde_adamw_step", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr),
+         float(beta1), float(beta2), float(eps), float(wd), int(step), _p(coef), float(grad_scale), stream_ptr())

@@ -1,0 +1,281 @@
+"""Whole-network HIP executor for the attention U-Net (forward + backward).
+
+Restates reference ``UNet.forward`` (src/models.py:72-101) as an explicit schedule of
+libsrpde_hip.so launches over NHWC ``[P, C]`` buffers, and its autograd backward as the
+reverse schedule.  Design points:
+
+* torch.cat never materialises: the decoder convs read ``(x0, x1)`` as a virtual
+  concat, and their dgrad writes one ``[P, C0+C1]`` gradient whose two slices are the
+  gradients of the two concat inputs (the attention-gating gradient accumulates into
+  the first slice in place).
+* ``up(d3)`` / ``up(d2)`` are computed once (the reference computes each twice,
+  models.py:89-93; the values are identical).
+* BatchNorm batch statistics come from the conv epilogue; the backward recomputes x_hat
+  and the ReLU mask from the saved conv output.
+* Parameter gradients are written straight into one flat buffer laid out in
+  *backward-completion order*, so a data-parallel reducer can all-reduce finished
+  prefixes while the rest of the backward still runs (``grad_ready`` hook).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import hipops as H
+
+# forward-pass module groups; the flat parameter buffer uses the REVERSE of this order
+FORWARD_GROUPS = ["enc1", "enc2", "enc3", "bridge", "att3", "dec3", "att2", "dec2", "att1", "dec1",
+                  "out_conv1", "out_bn1", "out_conv2", "out_bn2", "final"]
+FLAT_GROUPS = list(reversed(FORWARD_GROUPS))
+
+
+def flat_layout(model):
+    """[(name, param, offset, numel)] in flat (backward-completion) order."""
+    named = dict(model.named_parameters())
+    out, off = [], 0
+    for grp in FLAT_GROUPS:
+        for name, p in named.items():
+            if name == grp or name.startswith(grp + "."):
+                out.append((name, p, off, p.numel()))
+                off += p.numel()
+    assert off == sum(p.numel() for p in named.values()), "flat layout does not cover every parameter"
+    return out
+
+
+def _group_end_offsets(layout):
+    ends = {}
+    for name, _, off, n in layout:
+        grp = next(g for g in FLAT_GROUPS if name == g or name.startswith(g + "."))
+        ends[grp] = max(ends.get(grp, 0), off + n)
+    return ends
+
+
+class _Saved:
+    pass
+
+
+# bench/profiling hook: {conv module name: list} -> (start, end) HIP events recorded on the
+# compute stream around that layer's forward conv launch
+TIMED_LAYERS = {}
+
+
+def _conv_launch(conv, *args):
+    sink = TIMED_LAYERS.get(getattr(conv, "_srpde_name", None)) if TIMED_LAYERS else None
+    if sink is None:
+        H.conv_fwd(*args)
+        return
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    H.conv_fwd(*args)
+    b.record()
+    sink.append((a, b))
+
+
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, cin_pad=None):
+    """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48)."""
+    dev = x0.device
+    cout = conv.out_channels
+    cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    wf, _ = H.pack_conv_weights(conv.weight, cin)
+    P = n * h * w
+    y = H.empty(P, cout, device=dev)
+    if training:
+        stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev)
+        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats)
+        mom = bn.momentum if bn.momentum is not None else 0.0
+        mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
+                                           bn.num_batches_tracked, mom, bn.eps)
+    else:
+        H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
+        mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
+    a = H.empty(P, cout, device=dev)
+    H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a)
+    return a, (x0, x1, y, mean, invstd)
+
+
+def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, dx=None, dx_accumulate=False):
+    x0, x1, y, mean, invstd = saved
+    P, cout = y.shape
+    dy = H.empty(P, cout, device=y.device)
+    H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias])
+    H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
+    if dx is not None:
+        cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
+        _, wd = H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)
+        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None)
+
+
+def _block_fwd(blk, x0, x1, n, h, w, training):
+    a1, s1 = _cbr_fwd(blk.conv1, blk.bn1, x0, x1, n, h, w, training, 1)
+    a2, s2 = _cbr_fwd(blk.conv2, blk.bn2, a1, None, n, h, w, training, 1)
+    return a2, (s1, s2)
+
+
+def _block_bwd(blk, saved, da, n, h, w, grads, dx, dx_accumulate=False):
+    s1, s2 = saved
+    P = n * h * w
+    da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
+    _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, da1)
+    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, dx, dx_accumulate)
+
+
+def _att_params(att):
+    c1, c3, s0 = att.channel_attention[1], att.channel_attention[3], att.spatial_attention[0]
+    return c1, c3, s0
+
+
+def _att_fwd(att, x, g, n, hw):
+    c1, c3, s0 = _att_params(att)
+    out, saved = H.att_fwd(x, g, n, hw, c1.weight, c1.bias, c3.weight, c3.bias, s0.weight, s0.bias)
+    return out, saved
+
+
+def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc):
+    c1, c3, s0 = _att_params(att)
+    H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
+              grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight], grads[s0.bias])
+
+
+def check_input(x):
+    if x.dim() != 4 or x.shape[1] != 3:
+        raise ValueError(f"UNet expects [B, 3, H, W] input, got {tuple(x.shape)}")
+    if x.shape[2] % 4 or x.shape[3] % 4:
+        raise ValueError("UNet needs H and W divisible by 4 (two 2x2 pools)")
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise RuntimeError("the HIP U-Net runs on a ROCm device in float32 (no CPU fallback)")
+
+
+def unet_forward(m, x, training, save=False):
+    """UNet.forward (models.py:72-101).  Returns (out [B,1,H,W], saved-or-None)."""
+    check_input(x)
+    x = x.contiguous()
+    n, _, h, w = x.shape
+    h2, w2, h3, w3 = h // 2, w // 2, h // 4, w // 4
+    hw1, hw2, hw3 = h * w, h2 * w2, h3 * w3
+    S = _Saved()
+    S.shape = (n, h, w)
+    S.x = x
+    x4 = H.nchw_to_nhwc(x, 4)
+    S.x4 = x4
+    # encoder
+    e1, S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training)
+    p1 = H.maxpool_fwd(e1, n, h, w)
+    e2, S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training)
+    p2 = H.maxpool_fwd(e2, n, h2, w2)
+    e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training)
+    # bridge (dilated)
+    ab1, S.br1 = _cbr_fwd(m.bridge[0], m.bridge[1], e3, None, n, h3, w3, training, 2)
+    b, S.br2 = _cbr_fwd(m.bridge[3], m.bridge[4], ab1, None, n, h3, w3, training, 2)
+    # decoder with attention, virtual concat
+    e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3)
+    d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training)
+    u3 = H.upsample_fwd(d3, n, h3, w3, h2, w2)
+    e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2)
+    d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training)
+    u2 = H.upsample_fwd(d2, n, h2, w2, h, w)
+    e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1)
+    d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training)
+    # multi-scale head + residual
+    o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1)
+    o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1)
+    out = H.head_fwd(o2, m.final.weight, m.final.bias, x, n, hw1)
+    if not save:
+        return out.view(n, 1, h, w), None
+    S.e1, S.e2, S.e3, S.b, S.u3, S.u2, S.o2 = e1, e2, e3, b, u3, u2, o2
+    return out.view(n, 1, h, w), S
+
+
+def unet_backward(m, S, dout, grads, grad_ready=None):
+    """Reverse schedule.  ``grads``: param -> writable view (every one is fully written).
+    ``grad_ready(group)`` is called as soon as a module group's gradients are final."""
+    n, h, w = S.shape
+    h2, w2, h3, w3 = h // 2, w // 2, h // 4, w // 4
+    hw1, hw2, hw3 = h * w, h2 * w2, h3 * w3
+    dev = dout.device
+    P1, P2, P3 = n * hw1, n * hw2, n * hw3
+    ready = grad_ready or (lambda g: None)
+    dout = dout.contiguous().view(-1)
+    # head
+    do2 = H.empty(P1, 16, device=dev)
+    H.head_bwd(dout, S.o2, m.final.weight, n, hw1, do2, grads[m.final.weight], grads[m.final.bias])
+    ready("final")
+    do1 = H.empty(P1, m.out_conv1.out_channels, device=dev)
+    _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, do1)
+    ready("out_bn2"); ready("out_conv2")
+    dd1 = H.empty(P1, 64, device=dev)
+    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, dd1)
+    ready("out_bn1"); ready("out_conv1")
+    # dec1: grad of cat[u2 (128), e1a (64)]
+    dcat1 = H.empty(P1, 192, device=dev)
+    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, dcat1)
+    ready("dec1")
+    de1 = H.empty(P1, 64, device=dev)
+    _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, dcat1[:, :128], True)
+    ready("att1")
+    dd2 = H.empty(P2, 128, device=dev)
+    H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False)
+    # dec2: grad of cat[u3 (256), e2a (128)]
+    dcat2 = H.empty(P2, 384, device=dev)
+    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, dcat2)
+    ready("dec2")
+    de2 = H.empty(P2, 128, device=dev)
+    _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, dcat2[:, :256], True)
+    ready("att2")
+    dd3 = H.empty(P3, 256, device=dev)
+    H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False)
+    # dec3: grad of cat[b (512), e3a (256)]
+    dcat3 = H.empty(P3, 768, device=dev)
+    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, dcat3)
+    ready("dec3")
+    de3 = H.empty(P3, 256, device=dev)
+    _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True)
+    ready("att3")
+    # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
+    dab1 = H.empty(P3, 512, device=dev)
+    _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, dab1)
+    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, de3, True)
+    ready("bridge")
+    # encoder
+    dp2 = H.empty(P3, 128, device=dev)
+    _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, dp2)
+    ready("enc3")
+    H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
+    dp1 = H.empty(P2, 64, device=dev)
+    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, dp1)
+    ready("enc2")
+    H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, None)
+    ready("enc1")
+
+
+class UNetFunction(torch.autograd.Function):
+    """One autograd node for the whole network: forward/backward are the HIP schedules."""
+
+    @staticmethod
+    def forward(ctx, x, model, *params):
+        out, saved = unet_forward(model, x, model.training, save=True)
+        ctx.model = model
+        ctx.saved = saved
+        ctx.n_params = len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        model = ctx.model
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("gradient w.r.t. the U-Net input is not provided by the HIP path")
+        layout = model._flat_layout()
+        total = layout[-1][2] + layout[-1][3]
+        flat = torch.empty(total, dtype=torch.float32, device=dout.device)
+        views = {p: flat[off:off + nn].view_as(p) for _, p, off, nn in layout}
+        reducer = getattr(model, "_grad_reducer", None)
+        ends = _group_end_offsets(layout)
+        hook = None
+        if reducer is not None:
+            reducer.begin(flat)
+            hook = lambda grp: reducer.ready(ends[grp])  # noqa: E731
+        unet_backward(model, ctx.saved, dout, views, hook)
+        if reducer is not None:
+            reducer.finish()
+        ctx.saved = None
+        grads = [views[p] for p in model._param_list()]
+        return (None, None, *grads)

@@ -1,0 +1,251 @@
+"""Per-kernel parity: libsrpde_hip.so vs plain PyTorch fp32 (CPU) of the same op.
+
+Tolerances are relative to the op's magnitude; the fp32 MFMA conv sums in a different
+order than mkldnn, so agreement is ~1e-6 relative, not bitwise.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rows(x):  # NCHW -> [P, C] NHWC rows
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c).contiguous()
+
+
+def unrows(r, n, h, w):
+    return r.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+@pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
+    (2, 64, 0, 64, 40, 1), (3, 128, 0, 256, 10, 1), (2, 256, 0, 512, 10, 2), (2, 512, 256, 256, 10, 1),
+    (2, 128, 64, 64, 40, 1), (2, 32, 0, 16, 40, 1), (2, 64, 0, 32, 40, 1), (1, 4, 0, 64, 40, 1),
+    (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1)])
+def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil):
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(n * 1000 + cout + cin0)
+    cin = cin0 + cin1
+    x = torch.randn(n, cin, h, h, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cin)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    y_ref = F.conv2d(x, wt, b, padding=dil, dilation=dil)
+    xr = rows(x).to(DEV)
+    x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
+    wd = wt.to(DEV)
+    wf, wdg = H.pack_conv_weights(wd, cin, want_dgrad=True)
+    y = H.empty(n * h * h, cout, device=DEV)
+    stats, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV)
+    H.conv_fwd(x0, x1, wf, b.to(DEV), y, n, h, h, cout, 3, dil, 1, False, stats)
+    torch.cuda.synchronize()
+    assert rel(unrows(y, n, h, h), y_ref) < 2e-6
+    # BN statistics from the epilogue partials
+    mean, invstd = H.bn_train_finalize(stats, nblk, rpb, n * h * h, None, None, None, 0.1, 1e-5)
+    yr = y_ref.double()
+    m_ref = yr.mean(dim=(0, 2, 3))
+    v_ref = yr.var(dim=(0, 2, 3), unbiased=False)
+    assert rel(mean, m_ref) < 1e-5
+    assert rel(invstd, 1.0 / torch.sqrt(v_ref + 1e-5)) < 1e-5
+    # dgrad + wgrad against autograd
+    dy = torch.randn(n, cout, h, h, generator=g)
+    xg = x.clone().requires_grad_(True)
+    wg = wt.clone().requires_grad_(True)
+    F.conv2d(xg, wg, None, padding=dil, dilation=dil).backward(dy)
+    dyr = rows(dy).to(DEV)
+    dx = H.empty(n * h * h, cin, device=DEV)
+    H.conv_fwd(dyr, None, wdg, None, dx, n, h, h, cin, 3, dil, -1, False, None)
+    dw = torch.empty_like(wd)
+    H.conv_wgrad(dyr, x0, x1, dw, n, h, h, 3, dil)
+    torch.cuda.synchronize()
+    assert rel(unrows(dx, n, h, h), xg.grad) < 2e-6
+    assert rel(dw, wg.grad) < 2e-6
+
+
+def test_conv_cin_pad_and_accumulate():
+    """enc1.conv1: 3 real input channels padded to 4; accumulate flag adds into the output."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(3)
+    n, h = 2, 40
+    x = torch.randn(n, 3, h, h, generator=g)
+    wt = torch.randn(64, 3, 3, 3, generator=g) * 0.3
+    b = torch.randn(64, generator=g)
+    xr = H.nchw_to_nhwc(x.to(DEV), 4)
+    wf, _ = H.pack_conv_weights(wt.to(DEV), 4)
+    y = torch.ones(n * h * h, 64, device=DEV)
+    H.conv_fwd(xr, None, wf, b.to(DEV), y, n, h, h, 64, 3, 1, 1, True, None)
+    ref = F.conv2d(x, wt, b, padding=1) + 1.0
+    assert rel(unrows(y, n, h, h), ref) < 2e-6
+    dy = torch.randn(n, 64, h, h, generator=g)
+    wg = wt.clone().requires_grad_(True)
+    F.conv2d(x, wg, None, padding=1).backward(dy)
+    dw = torch.empty(64, 3, 3, 3, device=DEV)
+    H.conv_wgrad(rows(dy).to(DEV), xr, None, dw, n, h, h, 3, 1)
+    assert rel(dw, wg.grad) < 2e-6
+
+
+@pytest.mark.parametrize("c", [16, 64, 512])
+def test_bn_relu_fwd_bwd(c):
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(c)
+    n, h = 3, 10
+    y = torch.randn(n, c, h, h, generator=g) * 2 + 0.5
+    gamma = torch.rand(c, generator=g) + 0.5
+    beta = torch.randn(c, generator=g) * 0.2
+    yv = y.clone().requires_grad_(True)
+    gv = gamma.clone().requires_grad_(True)
+    bv = beta.clone().requires_grad_(True)
+    rm, rv = torch.zeros(c), torch.ones(c)
+    a_ref = F.relu(F.batch_norm(yv, rm, rv, gv, bv, True, 0.1, 1e-5))
+    da = torch.randn(n, c, h, h, generator=g)
+    a_ref.backward(da)
+    # HIP: stats via a 1x1 identity? use the exact batch stats path through finalize from partials
+    yr = rows(y).to(DEV)
+    P = n * h * h
+    # build (mean, M2) partials of one block per 7 rows, exercising the Chan merge
+    blk = 7
+    nblk = (P + blk - 1) // blk
+    st = torch.empty(nblk, c, 2, dtype=torch.float32)
+    for k in range(nblk):
+        seg = rows(y)[k * blk:(k + 1) * blk].double()
+        st[k, :, 0] = seg.mean(0).float()
+        st[k, :, 1] = ((seg - seg.mean(0)) ** 2).sum(0).float()
+    rmd, rvd = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    mean, invstd = H.bn_train_finalize(st.to(DEV), nblk, blk, P, rmd, rvd, nbt, 0.1, 1e-5)
+    out = H.empty(P, c, device=DEV)
+    H.bn_relu_fwd(yr, mean, invstd, gamma.to(DEV), beta.to(DEV), out)
+    torch.cuda.synchronize()
+    assert rel(unrows(out, n, h, h), a_ref) < 2e-6
+    assert rel(rmd, rm) < 1e-6 and rel(rvd, rv) < 1e-6 and int(nbt) == 1
+    dy = H.empty(P, c, device=DEV)
+    dgam, dbet, dbias = (torch.empty(c, device=DEV) for _ in range(3))
+    H.bn_relu_bwd(yr, rows(da).to(DEV), mean, invstd, gamma.to(DEV), beta.to(DEV), dy, dgam, dbet, dbias)
+    torch.cuda.synchronize()
+    assert rel(unrows(dy, n, h, h), yv.grad) < 1e-5
+    assert rel(dgam, gv.grad) < 1e-5 and rel(dbet, bv.grad) < 1e-5
+    assert abs(float(dbias.abs().max())) < 1e-3 * float(yv.grad.abs().max()) * P
+
+
+def test_pool_upsample():
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(5)
+    n, c, h = 2, 64, 20
+    x = torch.randn(n, c, h, h, generator=g)
+    x[:, :, 0, 0] = x[:, :, 0, 1]  # ties: first max wins
+    xv = x.clone().requires_grad_(True)
+    p_ref = F.max_pool2d(xv, 2)
+    dp = torch.randn_like(p_ref)
+    p_ref.backward(dp)
+    xr = rows(x).to(DEV)
+    p = H.maxpool_fwd(xr, n, h, h)
+    dx = torch.full((n * h * h, c), 0.5, device=DEV)
+    H.maxpool_bwd(xr, rows(dp).to(DEV), dx, n, h, h, True)
+    torch.cuda.synchronize()
+    assert torch.equal(unrows(p, n, h // 2, h // 2).cpu(), p_ref.detach())
+    assert torch.allclose(unrows(dx, n, h, h).cpu(), xv.grad + 0.5)
+    uv = x.clone().requires_grad_(True)
+    u_ref = F.interpolate(uv, scale_factor=2, mode="bilinear", align_corners=True)
+    du = torch.randn_like(u_ref)
+    u_ref.backward(du)
+    u = H.upsample_fwd(xr, n, h, h, 2 * h, 2 * h)
+    dxu = H.empty(n * h * h, c, device=DEV)
+    H.upsample_bwd(rows(du).to(DEV), dxu, n, h, h, 2 * h, 2 * h, False)
+    torch.cuda.synchronize()
+    assert rel(unrows(u, n, 2 * h, 2 * h), u_ref) < 1e-6
+    assert rel(unrows(dxu, n, h, h), uv.grad) < 1e-6
+
+
+@pytest.mark.parametrize("c,gc,h", [(256, 512, 10), (64, 128, 40)])
+def test_attention(c, gc, h):
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(c)
+    n = 3
+    x = torch.randn(n, c, h, h, generator=g)
+    gt = torch.randn(n, gc, h, h, generator=g)
+    w1 = torch.randn(c // 8, c, generator=g) * 0.2
+    b1 = torch.randn(c // 8, generator=g) * 0.1
+    w2 = torch.randn(c, c // 8, generator=g) * 0.2
+    b2 = torch.randn(c, generator=g) * 0.1
+    wg = torch.randn(1, gc, generator=g) * 0.1
+    bg = torch.randn(1, generator=g) * 0.1
+    ts = [t.clone().requires_grad_(True) for t in (x, gt, w1, b1, w2, b2, wg, bg)]
+    xv, gv, w1v, b1v, w2v, b2v, wgv, bgv = ts
+    m = xv.mean(dim=(2, 3), keepdim=True)
+    hh = F.relu(F.conv2d(m, w1v[:, :, None, None], b1v))
+    ca = torch.sigmoid(F.conv2d(hh, w2v[:, :, None, None], b2v))
+    sa = torch.sigmoid(F.conv2d(gv, wgv[:, :, None, None], bgv))
+    ref = xv * ca * sa
+    dout = torch.randn_like(ref)
+    ref.backward(dout)
+    d = {k: v.to(DEV) for k, v in dict(w1=w1, b1=b1, w2=w2, b2=b2, wg=wg, bg=bg).items()}
+    xr, gr = rows(x).to(DEV), rows(gt).to(DEV)
+    out, saved = H.att_fwd(xr, gr, n, h * h, d["w1"], d["b1"], d["w2"], d["b2"], d["wg"], d["bg"])
+    assert rel(unrows(out, n, h, h), ref) < 2e-6
+    dx = H.empty(n * h * h, c, device=DEV)
+    dg = torch.ones(n * h * h, gc, device=DEV)
+    grads = [torch.empty_like(d[k]) for k in ("w1", "b1", "w2", "b2", "wg", "bg")]
+    H.att_bwd(rows(dout).to(DEV), xr, gr, n, h * h, d["w1"], d["w2"], d["wg"], saved, dx, False, dg, True, *grads)
+    torch.cuda.synchronize()
+    assert rel(unrows(dx, n, h, h), xv.grad) < 1e-5
+    assert rel(unrows(dg, n, h, h) - 1.0, gv.grad) < 1e-5
+    for got, want in zip(grads, (w1v, b1v, w2v, b2v, wgv, bgv)):
+        assert rel(got, want.grad) < 1e-5
+
+
+def test_head_and_mse():
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(9)
+    n, h = 3, 40
+    z = torch.relu(torch.randn(n, 16, h, h, generator=g))
+    xin = torch.randn(n, 3, h, h, generator=g)
+    wf = torch.randn(1, 16, 1, 1, generator=g) * 0.3
+    bf = torch.randn(1, generator=g)
+    tgt = torch.randn(n, 1, h, h, generator=g)
+    zv, wv, bv = (t.clone().requires_grad_(True) for t in (z, wf, bf))
+    out_ref = F.conv2d(zv, wv, bv) + xin[:, 0:1]
+    loss_ref = F.mse_loss(out_ref, tgt)
+    loss_ref.backward()
+    out = H.head_fwd(rows(z).to(DEV), wf.to(DEV), bf.to(DEV), xin.to(DEV), n, h * h)
+    assert rel(out.view(n, 1, h, h), out_ref) < 1e-6
+    loss = H.mse_fwd(out, tgt.to(DEV).view(-1))
+    assert abs(float(loss) - float(loss_ref)) < 1e-5 * float(loss_ref)
+    dy = H.mse_bwd(out, tgt.to(DEV).view(-1), None)
+    dz = H.empty(n * h * h, 16, device=DEV)
+    dwf, dbf = torch.empty(1, 16, 1, 1, device=DEV), torch.empty(1, device=DEV)
+    H.head_bwd(dy, rows(z).to(DEV), wf.to(DEV), n, h * h, dz, dwf, dbf)
+    torch.cuda.synchronize()
+    assert rel(unrows(dz, n, h, h), zv.grad) < 1e-5
+    assert rel(dwf, wv.grad) < 1e-5 and rel(dbf, bv.grad) < 1e-5
+
+
+def test_clip_adamw_matches_torch():
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(1)
+    ps = [torch.randn(1000, generator=g), torch.randn(37, generator=g)]
+    gs = [torch.randn(1000, generator=g) * 3, torch.randn(37, generator=g)]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    opt = torch.optim.AdamW(ref, lr=2e-4, weight_decay=1e-4)
+    flat_p = torch.cat(ps).to(DEV)
+    flat_g = torch.cat(gs).to(DEV)
+    m = torch.zeros_like(flat_p)
+    v = torch.zeros_like(flat_p)
+    coef = torch.empty(2, device=DEV)
+    for step in (1, 2, 3):
+        for r, gg in zip(ref, gs):
+            r.grad = gg.clone()
+        tot = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt.step()
+        H.clip_coef(flat_g, 1.0, 1.0, coef)
+        H.adamw_step(flat_p, flat_g, m, v, 2e-4, 0.9, 0.999, 1e-8, 1e-4, step, coef, 1.0)
+        torch.cuda.synchronize()
+        assert abs(float(coef[1]) - float(tot)) < 1e-5 * float(tot)
+        assert rel(flat_p, torch.cat([r.detach() for r in ref])) < 1e-7

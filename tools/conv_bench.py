@@ -1,0 +1,81 @@
+"""Micro-benchmark of the HIP conv kernels per U-Net layer at batch 1024 (fwd, dgrad, wgrad).
+
+    python tools/conv_bench.py [--batch 1024] [--iters 10] [--only fwd|dgrad|wgrad]
+Prints TFLOP/s per layer and the FLOP-weighted total for each pass.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from superresolution_for_pdes_amd import hipops as H  # noqa: E402
+
+# (name, c0, c1, cout, hw, dil)
+LAYERS = [("enc1.conv2", 64, 0, 64, 40, 1), ("enc2.conv1", 64, 0, 128, 20, 1), ("enc2.conv2", 128, 0, 128, 20, 1),
+          ("enc3.conv1", 128, 0, 256, 10, 1), ("enc3.conv2", 256, 0, 256, 10, 1), ("bridge.0", 256, 0, 512, 10, 2),
+          ("bridge.3", 512, 0, 512, 10, 2), ("dec3.conv1", 512, 256, 256, 10, 1), ("dec3.conv2", 256, 0, 256, 10, 1),
+          ("dec2.conv1", 256, 128, 128, 20, 1), ("dec2.conv2", 128, 0, 128, 20, 1), ("dec1.conv1", 128, 64, 64, 40, 1),
+          ("dec1.conv2", 64, 0, 64, 40, 1), ("out_conv1", 64, 0, 32, 40, 1), ("out_conv2", 32, 0, 16, 40, 1)]
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--layers", default="")
+    args = ap.parse_args()
+    dev = "cuda"
+    n = args.batch
+    tot = {}
+    for name, c0, c1, cout, hw, dil in LAYERS:
+        if args.layers and name not in args.layers.split(","):
+            continue
+        cin = c0 + c1
+        P = n * hw * hw
+        flops = 2.0 * cout * cin * 9 * P
+        x = torch.randn(P, cin, device=dev)
+        x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
+        w = torch.randn(cout, cin, 3, 3, device=dev) * 0.05
+        b = torch.randn(cout, device=dev)
+        wf, wd = H.pack_conv_weights(w, cin, True, True)
+        y = torch.empty(P, cout, device=dev)
+        stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, dev)
+        dy = torch.randn(P, cout, device=dev)
+        dx = torch.empty(P, cin, device=dev)
+        dw = torch.empty_like(w)
+        line = f"{name:11s}"
+        for kind in args.only.split(","):
+            if kind == "fwd":
+                ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats), args.iters)
+            elif kind == "dgrad":
+                ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
+                            args.iters)
+            else:
+                ms = timeit(lambda: H.conv_wgrad(dy, x0, x1, dw, n, hw, hw, 3, dil), args.iters)
+            tf = flops / ms / 1e9
+            t = tot.setdefault(kind, [0.0, 0.0])
+            t[0] += flops
+            t[1] += ms
+            line += f"  {kind} {ms:7.3f} ms {tf:6.1f} TF"
+        print(line, flush=True)
+    for k, (f, ms) in tot.items():
+        print(f"TOTAL {k}: {ms:.2f} ms  {f / ms / 1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
