@@ -121,6 +121,9 @@ int srpde_adamw_step(float* p, const float* g, float* m, float* v, long long n, 
 /* ---- Poisson: replaces scipy.sparse.linalg.spsolve(diag(theta) @ L, f)
  *      (src/data_generation.py:79-104, src/enhanced_data_generation.py:47-68) -------- */
 int srpde_poisson_lds_max_n(void);
+/* forcing f = sin(2 pi k1 X) sin(2 pi k2 Y) for B (k1, k2) pairs on linspace(0,1,n)^2
+ * (PoissonSolver.generate_forcing_term, src/data_generation.py:60-77) */
+int srpde_forcing_batched(const double* k12, int B, int n, double* out, hipStream_t stream);
 size_t srpde_poisson_workspace_size(int B, int n);
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream);

@@ -1,0 +1,102 @@
+"""Drop-in for reference ``src/enhanced_data_generation.py`` with batched on-device solves.
+
+``EnhancedPoissonSolver(n_coarse, n_fine, n_superfine)`` (enhanced_data_generation.py:11-244):
+subdomain samples solve on the super-fine grid (80^2), crop a random n_fine window
+(start in [0, n_superfine - n_fine)) and stride by 2 for the coarse grid.  The random draws
+(k1, k2, start_x, start_y per sample, global np.random) keep the reference's order, so a
+seeded run reproduces the reference's dataset; all super-fine solves run as one batch.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from . import poisson as P
+from .data_generation import PoissonSolver
+
+
+class EnhancedPoissonSolver(PoissonSolver):
+    def __init__(self, n_coarse: int = 20, n_fine: int = 40, n_superfine: int = 80, device: str = "cuda"):
+        super().__init__(n_coarse, n_fine, device)
+        self.n_superfine = n_superfine
+        self.x_superfine = np.linspace(0, 1, n_superfine)
+        self.y_superfine = np.linspace(0, 1, n_superfine)
+        self.X_superfine, self.Y_superfine = np.meshgrid(self.x_superfine, self.y_superfine)
+
+    @property
+    def L_superfine(self):
+        return self._create_laplacian(self.n_superfine)
+
+    def generate_forcing_term_superfine(self, k1: float, k2: float) -> np.ndarray:
+        return P.forcing_batched(np.array([[k1, k2]]), self.n_superfine, self.device)[0].cpu().numpy()
+
+    def solve_poisson_superfine(self, f: np.ndarray, theta: np.ndarray) -> np.ndarray:
+        n = self.n_superfine
+        return P.solve_batched(np.asarray(f, np.float64).reshape(n, n), np.asarray(theta, np.float64).reshape(n, n),
+                               device=self.device)[0].cpu().numpy()
+
+    def extract_subdomain(self, field, start_x: int, start_y: int, size: int):
+        return field[start_y:start_y + size, start_x:start_x + size]
+
+    def downsample(self, field, factor: int = 2):
+        return field[::factor, ::factor]
+
+    def generate_subdomain_dataset(self, n_samples: int, k_range: Tuple[float, float] = (0.5, 12.0)) -> dict:
+        """enhanced_data_generation.py:98-165 with one batched 80^2 solve."""
+        ns, nf, nsf = n_samples, self.n_fine, self.n_superfine
+        k = np.empty((ns, 2))
+        starts = np.empty((ns, 2), dtype=np.int64)
+        max_start = nsf - nf
+        for s in range(ns):  # reference draw order: k1, k2, start_x, start_y
+            k[s, 0] = np.random.uniform(*k_range)
+            k[s, 1] = np.random.uniform(*k_range)
+            starts[s, 0] = np.random.randint(0, max_start)
+            starts[s, 1] = np.random.randint(0, max_start)
+        f_sf = P.forcing_batched(k, nsf, self.device)
+        th_sf = torch.ones(ns, nsf, nsf, dtype=torch.float64, device=self.device)
+        u_sf = P.solve_batched(f_sf, th_sf, device=self.device)
+        # crop windows by one gather: rows start_y + i, cols start_x + j
+        ar = torch.arange(nf, device=self.device)
+        sx = torch.as_tensor(starts[:, 0], device=self.device)
+        sy = torch.as_tensor(starts[:, 1], device=self.device)
+        rows = (sy[:, None] + ar[None, :])[:, :, None].expand(ns, nf, nf)
+        cols = (sx[:, None] + ar[None, :])[:, None, :].expand(ns, nf, nf)
+        bidx = torch.arange(ns, device=self.device)[:, None, None].expand(ns, nf, nf)
+        crop = lambda a: a[bidx, rows, cols]  # noqa: E731
+        f_fine, u_fine, th_fine = crop(f_sf), crop(u_sf), crop(th_sf)
+        out = {
+            "u_coarse": u_fine[:, ::2, ::2],
+            "u_fine": u_fine,
+            "f_coarse": f_fine[:, ::2, ::2],
+            "f_fine": f_fine,
+            "theta_coarse": th_fine[:, ::2, ::2],
+            "theta_fine": th_fine,
+            "k1": k[:, 0].copy(),
+            "k2": k[:, 1].copy(),
+            "is_subdomain": np.ones(ns, dtype=bool),
+        }
+        return {kk: (v.contiguous().cpu().numpy() if isinstance(v, torch.Tensor) else v) for kk, v in out.items()}
+
+    def combine_datasets(self, dataset1: Dict, dataset2: Dict) -> Dict:
+        """enhanced_data_generation.py:167-191."""
+        if "is_subdomain" not in dataset1:
+            dataset1["is_subdomain"] = np.zeros(len(dataset1["u_fine"]), dtype=bool)
+        out = {}
+        for key in dataset1:
+            out[key] = np.concatenate([dataset1[key], dataset2[key]]) if key in dataset2 else dataset1[key]
+        return out
+
+
+if __name__ == "__main__":
+    from pathlib import Path
+    solver = EnhancedPoissonSolver(20, 40, 80)
+    path = Path("data") / "pde_dataset.npz"
+    if path.exists():
+        existing = dict(np.load(path))
+    else:
+        existing = solver.generate_dataset(n_samples=1000, k_range=(0.5, 5.0))
+    sub = solver.generate_subdomain_dataset(n_samples=1000, k_range=(0.5, 12.0))
+    solver.save_dataset(solver.combine_datasets(existing, sub))
+    print("Combined dataset saved successfully!")

@@ -1,0 +1,120 @@
+"""Poisson data-generation parity: HIP CG vs the reference's SuperLU spsolve (golden
+fixtures from tests/golden/make_golden.py) and vs the oracle restatement.
+
+Bar: relative L2 error vs spsolve <= 1e-10 (fp64).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.mark.parametrize("n", [20, 40, 80, 160])
+def test_cg_matches_spsolve_fixture(golden, n):
+    from superresolution_for_pdes_amd import poisson as P
+    z = golden["poisson"]
+    f = z[f"f{n}"]
+    k1, k2 = z[f"k{n}"]
+    fk = P.forcing_batched(np.array([[k1, k2]]), n)[0].cpu().numpy()
+    assert np.max(np.abs(fk - f)) < 1e-13
+    th = np.stack([np.ones((n, n)), z[f"thv{n}"]])
+    u, it = P.solve_batched(np.stack([f, f]), th, return_iters=True)
+    u = u.cpu().numpy()
+    assert rel(u[0], z[f"u1_{n}"]) < 1e-10
+    assert rel(u[1], z[f"uv_{n}"]) < 1e-10
+    assert int(it.max()) < 10 * n  # CG needs ~3.3 n iterations
+
+
+def test_cg_640_matches_spsolve_stats(golden):
+    from superresolution_for_pdes_amd import poisson as P
+    z = golden["poisson"]
+    n = 640
+    f = P.forcing_batched(np.array([[10.25, 10.75]]), n)
+    thv = np.random.default_rng(640).uniform(0.5, 2.0, (n, n))
+    u = P.solve_batched(f, thv)[0].cpu().numpy()
+    assert abs(np.linalg.norm(u) - float(z["u640_norm"])) < 1e-10 * float(z["u640_norm"])
+    assert rel(u[320], z["u640_row320"]) < 1e-9
+    assert rel(u[:, 100], z["u640_col100"]) < 1e-9
+
+
+def test_batched_large_against_oracle():
+    """B=1024 problems at n=40 (config #3 size): residual of every solution and spsolve on a sample."""
+    from superresolution_for_pdes_amd import poisson as P
+    from oracle import poisson_ref as R
+    rng = np.random.default_rng(3)
+    B, n = 1024, 40
+    k = rng.uniform(0.5, 12.0, (B, 2))
+    f = P.forcing_batched(k, n)
+    th = torch.from_numpy(rng.uniform(0.5, 2.0, (B, n, n))).cuda()
+    u = P.solve_batched(f, th)
+    fn, tn, un = f.cpu().numpy(), th.cpu().numpy(), u.cpu().numpy()
+    res = np.linalg.norm((R.apply_operator(un, tn) - fn).reshape(B, -1), axis=1) / np.linalg.norm(fn.reshape(B, -1),
+                                                                                                   axis=1)
+    assert res.max() < 1e-9
+    for b in (0, 517, 1023):
+        assert rel(un[b], R.solve(fn[b], tn[b])) < 1e-10
+
+
+def test_edge_cases():
+    from superresolution_for_pdes_amd import poisson as P
+    from oracle import poisson_ref as R
+    # zero forcing -> zero solution, no iterations
+    u, it = P.solve_batched(np.zeros((1, 20, 20)), np.ones((1, 20, 20)), return_iters=True)
+    assert float(u.abs().max()) == 0.0 and int(it[0]) == 0
+    # smallest grids and a non-power-of-two size
+    for n in (2, 3, 7, 33, 128, 129):
+        rng = np.random.default_rng(n)
+        f = rng.standard_normal((n, n))
+        th = rng.uniform(0.5, 2.0, (n, n))
+        assert rel(P.solve_batched(f, th)[0].cpu().numpy(), R.solve(f, th)) < 1e-10
+
+
+def test_generate_dataset_matches_reference(golden):
+    from superresolution_for_pdes_amd.enhanced_data_generation import EnhancedPoissonSolver
+    z = golden["datagen"]
+    s = EnhancedPoissonSolver(20, 40, 80)
+    np.random.seed(123)
+    d1 = s.generate_dataset(n_samples=3, k_range=(0.5, 5.0))
+    np.random.seed(7)
+    d2 = s.generate_subdomain_dataset(n_samples=3, k_range=(0.5, 12.0))
+    for key, v in d1.items():
+        ref = z[f"std:{key}"]
+        if key.startswith("u_"):
+            assert rel(v, ref) < 1e-10, key
+        else:
+            assert np.allclose(v, ref, rtol=0, atol=1e-13), key
+    for key, v in d2.items():
+        ref = z[f"sub:{key}"]
+        if key.startswith("u_"):
+            assert rel(v, ref) < 1e-10, key
+        else:
+            assert np.array_equal(v, ref) or np.allclose(v, ref, rtol=0, atol=1e-13), key
+    comb = s.combine_datasets(dict(d1), d2)
+    assert sorted(comb) == sorted(k[5:] for k in z.files if k.startswith("comb:"))
+    assert np.array_equal(comb["is_subdomain"], z["comb:is_subdomain"])
+
+
+def test_pdedataset_matches_reference(golden):
+    from superresolution_for_pdes_amd.models import PDEDataset
+    z = golden["datagen"]
+    comb = {k[5:]: z[k] for k in z.files if k.startswith("comb:")}
+    ds = PDEDataset(comb, device="cuda")
+    assert abs(float(ds.u_mean) - float(z["ds_u_mean"])) <= 1e-6 * abs(float(z["ds_u_mean"])) + 1e-12
+    assert abs(float(ds.u_std) - float(z["ds_u_std"])) <= 1e-6 * float(z["ds_u_std"])
+    assert bool(ds.theta_is_constant) == bool(z["ds_theta_const"])
+    x = torch.stack([ds[i][0] for i in range(len(ds))]).cpu().numpy()
+    y = torch.stack([ds[i][1] for i in range(len(ds))]).cpu().numpy()
+    assert np.max(np.abs(x - z["ds_x"])) < 1e-5
+    assert np.max(np.abs(y - z["ds_y"])) < 1e-5
+    varc = dict(comb)
+    varc["theta_fine"] = z["dsv_theta_fine"]
+    dsv = PDEDataset(varc, device="cuda")
+    xv = torch.stack([dsv[i][0] for i in range(len(dsv))]).cpu().numpy()
+    assert np.max(np.abs(xv - z["dsv_x"])) < 1e-5
