@@ -77,27 +77,31 @@ class FusedAdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm, grad_scale=1.0):
-        """clip_grad_norm_(all params, max_norm) computed on device; returns the total norm tensor."""
+        """clip_grad_norm_(all params, max_norm) on device.  Like torch's, the NEXT step()
+        uses the clipped gradients (the coefficient is applied inside the fused update
+        instead of rewriting the gradients).  Returns the total-norm tensor (device)."""
         grads = [p.grad for g in self.param_groups for p in g["params"]]
         flat = _flat_span(sorted(grads, key=lambda t: t.data_ptr())) if all(g is not None for g in grads) else None
         if flat is None:
-            flat = torch.cat([g.reshape(-1) for g in grads])
+            flat = torch.cat([g.reshape(-1) for g in grads if g is not None])
         if self._coef is None or self._coef.device != flat.device:
             self._coef = torch.empty(2, dtype=torch.float32, device=flat.device)
         H.clip_coef(flat, grad_scale, float(max_norm) if max_norm is not None else -1.0, self._coef)
+        self._pending = True
         self.last_total_norm = self._coef[1]
         return self._coef[1]
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale=1.0):
+    def step(self, closure=None, grad_scale=1.0, max_grad_norm=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        coef = None
-        if self.max_grad_norm is not None:
-            self.clip_grad_norm_(self.max_grad_norm, grad_scale)
-            coef = self._coef
+        mgn = max_grad_norm if max_grad_norm is not None else self.max_grad_norm
+        if mgn is not None:
+            self.clip_grad_norm_(mgn, grad_scale)
+        coef = self._coef if getattr(self, "_pending", False) else None
+        self._pending = False
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:

@@ -1,0 +1,135 @@
+"""Multi-level cascade inference + multi-resolution ground truth (config #5) on MI355X.
+
+Reference: src/resolution_comparison.py:13-229.  Semantics kept:
+  * ``solve_multi_resolution``: one (f, theta ~ U(0.5, 2)) field on the finest grid, strided
+    to every resolution, each solved with h = 1/(res-1) (the reference's quirk, :56-73) --
+    here by the batched HIP CG instead of SuperLU;
+  * ``ml_multi_level_upscale``: per level, GROUND-TRUTH statistics at the next resolution
+    normalise the inputs (:196-201, a label leak the reference has, reproduced for parity),
+    20^2 tiles -> normalise -> bilinear to 40^2 -> U-Net (eval) -> denormalise -> stitch.
+Difference: every level runs as ONE batched forward of all its tiles (1, 4, 16, 64, 256
+tiles for 20 -> 640) instead of the reference's batch-1 Python loop (:211-223), and the
+start resolution is a parameter (config #5 starts at 20).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+
+from . import poisson as P
+from .models import upsample_bilinear
+
+
+def solve_multi_resolution(n_coarse: int = 40, resolutions: List[int] = (80, 160, 320, 640), device="cuda",
+                           verbose: bool = False):
+    """resolution_comparison.py:13-78 with the GT solves on device (returns numpy fields)."""
+    resolutions = list(resolutions)
+    k1 = np.random.uniform(10.0, 11.0)
+    k2 = np.random.uniform(10.0, 11.0)
+    n_finest = max(resolutions)
+    x = np.linspace(0, 1, n_finest)
+    X, Y = np.meshgrid(x, x)
+    f_finest = np.sin(k1 * 2 * np.pi * X) * np.sin(k2 * 2 * np.pi * Y)   # host, as the reference (:36)
+    theta_finest = np.random.uniform(0.5, 2.0, size=(n_finest, n_finest))
+    data = {"k1": k1, "k2": k2, "f": {}, "theta": {}, "u": {}}
+    for res in [n_coarse] + resolutions:
+        step = n_finest // res
+        data["f"][res] = f_finest if res == n_finest else f_finest[::step, ::step]
+        data["theta"][res] = theta_finest if res == n_finest else theta_finest[::step, ::step]
+        data["u"][res] = P.solve_batched(data["f"][res], data["theta"][res], device=device)[0].cpu().numpy()
+        if verbose:
+            print(f"u_{res} - min: {data['u'][res].min():.6f}, max: {data['u'][res].max():.6f}")
+    return data
+
+
+class GlobalNormalization:
+    """resolution_comparison.py:160-181 (fp32 statistics, unbiased std)."""
+
+    def __init__(self, u_fine, u_coarse, f_fine, theta_fine, device="cuda"):
+        t = lambda a: torch.as_tensor(np.asarray(a)).to(device=device, dtype=torch.float32)  # noqa: E731
+        u_fine, f_fine, theta_fine = t(u_fine), t(f_fine), t(theta_fine)
+        self.u_mean, self.u_std = u_fine.mean(), u_fine.std()
+        self.f_mean, self.f_std = f_fine.mean(), f_fine.std()
+        self.theta_is_constant = bool(theta_fine.std() < 1e-6)
+        if self.theta_is_constant:
+            self.theta_mean, self.theta_std = 0, 1
+        else:
+            self.theta_mean, self.theta_std = theta_fine.mean(), theta_fine.std()
+
+
+def _tiles(a: torch.Tensor, s: int) -> torch.Tensor:
+    """[R, R] -> [(R/s)^2, s, s] row-major tile order (split_into_subdomains, :123-139)."""
+    m = a.shape[0] // s
+    return a.reshape(m, s, m, s).permute(0, 2, 1, 3).reshape(m * m, s, s)
+
+
+def _stitch(t: torch.Tensor) -> torch.Tensor:
+    """inverse of _tiles (stitch_subdomains, :141-158)."""
+    T, s, _ = t.shape
+    m = int(round(T ** 0.5))
+    return t.reshape(m, m, s, s).permute(0, 2, 1, 3).reshape(m * s, m * s)
+
+
+def split_into_subdomains(array: np.ndarray, subdomain_size: int) -> list:
+    m = array.shape[0] // subdomain_size
+    return [[array[i * subdomain_size:(i + 1) * subdomain_size, j * subdomain_size:(j + 1) * subdomain_size]
+             for j in range(m)] for i in range(m)]
+
+
+def stitch_subdomains(subdomains: list) -> np.ndarray:
+    s = subdomains[0][0].shape[0]
+    out = np.zeros((len(subdomains) * s, len(subdomains[0]) * s))
+    for i, row in enumerate(subdomains):
+        for j, t in enumerate(row):
+            out[i * s:(i + 1) * s, j * s:(j + 1) * s] = t
+    return out
+
+
+def _level_inputs(u_cur, f_next, th_next, norm, tile=20):
+    """Normalised model inputs for every tile of one level: [T, 3, 2*tile, 2*tile]."""
+    uc = _tiles(u_cur.float(), tile)
+    ft = _tiles(f_next.float(), 2 * tile)
+    tt = _tiles(th_next.float(), 2 * tile)
+    ucn = (uc - norm.u_mean) / norm.u_std
+    fn = (ft - norm.f_mean) / norm.f_std
+    tn = tt if norm.theta_is_constant else (tt - norm.theta_mean) / norm.theta_std
+    up = upsample_bilinear(ucn.unsqueeze(1).contiguous(), 2 * tile, 2 * tile)
+    return torch.cat([up, tn.unsqueeze(1), fn.unsqueeze(1)], dim=1).contiguous()
+
+
+def upscale_subdomain(model, u_coarse, f_fine, theta_fine, global_norm, device="cuda") -> np.ndarray:
+    """Single-tile API of the reference (:80-121)."""
+    dev = lambda a: torch.as_tensor(np.asarray(a)).to(device=device, dtype=torch.float64)  # noqa: E731
+    x = _level_inputs(dev(u_coarse), dev(f_fine), dev(theta_fine), global_norm, tile=u_coarse.shape[0])
+    with torch.no_grad():
+        y = model(x) * global_norm.u_std + global_norm.u_mean
+    return y.squeeze().double().cpu().numpy()
+
+
+@torch.no_grad()
+def ml_multi_level_upscale(model, data: dict, target_resolution: int, device: str = "cuda",
+                           start_resolution: int = 40, tile: int = 20, return_tensor: bool = False,
+                           max_batch: int = 4096):
+    """resolution_comparison.py:183-229 with one batched U-Net forward per level."""
+    model.eval()
+    cur_res = start_resolution
+    cur = torch.as_tensor(np.asarray(data["u"][cur_res])).to(device=device, dtype=torch.float64)
+    while cur_res < target_resolution:
+        nxt = cur_res * 2
+        norm = GlobalNormalization(data["u"][nxt], None, data["f"][nxt], data["theta"][nxt], device=device)
+        f_next = torch.as_tensor(np.asarray(data["f"][nxt])).to(device)
+        th_next = torch.as_tensor(np.asarray(data["theta"][nxt])).to(device)
+        x = _level_inputs(cur, f_next, th_next, norm, tile)
+        outs = [model(x[s:s + max_batch]) for s in range(0, x.shape[0], max_batch)]
+        y = torch.cat(outs) * norm.u_std + norm.u_mean
+        cur = _stitch(y[:, 0].double())
+        cur_res = nxt
+    return cur if return_tensor else cur.cpu().numpy()
+
+
+def cascade_metrics(pred: np.ndarray, gt: np.ndarray) -> dict:
+    d = np.asarray(pred, np.float64) - np.asarray(gt, np.float64)
+    return {"mae": float(np.mean(np.abs(d))), "rmse": float(np.sqrt(np.mean(d * d))),
+            "max_error": float(np.max(np.abs(d)))}
