@@ -45,7 +45,11 @@ int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout
                             int ksize, hipStream_t stream);
 int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const float* wpack,
                    const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
-                   int sign, int accumulate, float* stats, hipStream_t stream);
+                   int sign, int accumulate, float* stats, void* workspace, size_t ws_bytes,
+                   hipStream_t stream);
+/* optional scratch for splitting the last, partially filled round of tiles over K (pass
+ * NULL to disable); srpde_conv_fwd_workspace_size() bytes always suffice */
+size_t srpde_conv_fwd_workspace_size(int cout);
 size_t srpde_conv_stats_blocks(int n, int h, int w, int cout);
 int srpde_conv_stats_rows_per_block(int cout);
 size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, int ksize);

@@ -29,6 +29,10 @@ struct ConvParams {
   float2* stats;        // [mblocks][Cout] (mean, M2) or null
   int N, H, W, Cout, ksize, dil, sign, accumulate;
   int P, K, Cin;
+  // tail split (v2 only): the last `ntail` tiles are computed as `tsplit` K-pieces each,
+  // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
+  int ntail, tsplit;
+  float* part;
 };
 
 constexpr int BK = 16;      // k (tap*Cin + c) per stage
@@ -273,6 +277,28 @@ constexpr unsigned OOB = 0x80000000u;   // beyond num_records -> zero fill
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
+// One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds) as inline asm.  Issued through the
+// builtin, hipcc treats the DMA as an LDS store that may alias the following ds_reads and
+// emits s_waitcnt vmcnt(0) right after it, serialising the prefetch behind the compute;
+// as asm it is invisible to the waitcnt pass and we count vmcnt ourselves (vmcnt(0) before
+// the stage barrier).  M0 (the wave-uniform LDS destination) is saved/restored inside.
+__device__ __forceinline__ void dma16(int32x4 rsrc, unsigned voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr_of(const void* p) {
+  return (unsigned)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+
 template <int BM, int BN, int WM, int WN, int HP>
 __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -287,7 +313,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
   const int wmi = wave % WM, wni = wave / WM;
   const int nbn = (p.Cout + BN - 1) / BN;
   const int nbm = (p.P + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, nbm * nbn);
+  // tiles [0, nfull) whole (XCD-aware order); the last ntail tiles as tsplit K-pieces each,
+  // so the final partially-filled round of workgroups is spread over more CUs
+  const int nfull = nbm * nbn - p.ntail;
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
+  } else {
+    const int q = blockIdx.x - nfull;
+    wg = nfull + q / p.tsplit;
+    piece = q - (q / p.tsplit) * p.tsplit;
+  }
+  const bool tail = wg >= nfull;
   const int mt = wg / nbn, nt = wg - mt * nbn;
   const int m0 = mt * BM, n0 = nt * BN;
   const int HW = p.H * p.W;
@@ -297,22 +334,31 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const int32x4 rsw = make_rsrc(p.w, (unsigned)((size_t)p.Cout * p.K * 4));
 
-  // per-lane A rows and chunks (fixed over the K loop)
-  int a_nb[AI], a_yx[AI], a_c[AI];
+  // per-lane A rows, fixed over the K loop: byte offset of (pixel, swizzled chunk) in each
+  // source, and a bitmask of the taps whose shifted pixel lies inside the image (padding)
+  unsigned a_o0[AI], a_o1[AI], a_mask[AI];
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int q = (wave * AI + i) * 64 + lane;
     const int r = q >> 3;
-    a_c[i] = swz(r, q & 7) * 4;
+    const int c4 = swz(r, q & 7) * 4;
     const int m = m0 + r;
+    unsigned mask = 0;
+    int pix = 0;
     if (m < p.P) {
-      const int n = m / HW, rem = m - n * HW, yy = rem / p.W;
-      a_nb[i] = n * HW;
-      a_yx[i] = (yy << 16) | (rem - yy * p.W);
-    } else {
-      a_nb[i] = -1;
-      a_yx[i] = 0;
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+      pix = m;
+      for (int t = 0; t < p.ksize * p.ksize; ++t) {
+        const int ky = t / p.ksize, kx = t - ky * p.ksize;
+        const int iy = yy + (ky - kc) * p.dil * p.sign, ix = xx + (kx - kc) * p.dil * p.sign;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
+      }
+      (void)n;
     }
+    a_mask[i] = mask;
+    a_o0[i] = (unsigned)((pix * p.ldx0 + c4) * 4);
+    a_o1[i] = (unsigned)((pix * ld1 + c4) * 4);
   }
   int b_off[BI];
 #pragma unroll
@@ -323,30 +369,40 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
     b_off[j] = nn < p.Cout ? (nn * p.K + swz(r, q & 7) * 4) * 4 : -1;
   }
 
+  // this block's K range in BK2 stages (a tail piece covers a contiguous share)
+  const int nall = p.K / BK2;
+  const int s_beg = tail ? (piece * nall) / p.tsplit : 0;
+  const int s_end = tail ? ((piece + 1) * nall) / p.tsplit : nall;
+  // scalar K-walk state of the next stage to issue: (tap = ky*ksize + kx, channel offset)
+  int nx_tap = (s_beg * BK2) / p.Cin, nx_ch = s_beg * BK2 - nx_tap * p.Cin;
+  int nx_ky = nx_tap / p.ksize, nx_kx = nx_tap - nx_ky * p.ksize;
   auto issue = [&](int s, int buf) {
     const int k0 = s * BK2;
-    const int tap = k0 / p.Cin, ch0 = k0 - tap * p.Cin;
-    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
-    const int dy = (ky - kc) * p.dil * p.sign, dx = (kx - kc) * p.dil * p.sign;
+    const int tap = nx_tap, ch0 = nx_ch;
+    const int tsh = ((nx_ky - kc) * p.W + (nx_kx - kc)) * p.dil * p.sign;  // pixel shift of this tap
     const bool second = ch0 >= p.c0;
     const int32x4 rs = second ? rs1 : rs0;
-    const int ld = second ? p.ldx1 : p.ldx0;
+    const int ld = second ? ld1 : p.ldx0;
     const int cb = second ? ch0 - p.c0 : ch0;
+    const unsigned sadd = (unsigned)((tsh * ld + cb) * 4);
+    nx_ch += BK2;
+    if (nx_ch == p.Cin) {
+      nx_ch = 0;
+      ++nx_tap;
+      if (++nx_kx == p.ksize) { nx_kx = 0; ++nx_ky; }
+    }
     char* abase = lds + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int iy = (a_yx[i] >> 16) + dy, ix = (a_yx[i] & 0xffff) + dx;
-      const bool ok = a_nb[i] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-      const unsigned off = ok ? (unsigned)(((a_nb[i] + iy * p.W + ix) * ld + cb + a_c[i]) * 4) : OOB;
-      llvm_raw_buffer_load_lds(rs, (__attribute__((address_space(3))) unsigned*)(abase + (wave * AI + i) * 1024),
-                               16, (int)off, 0, 0, 0);
+      const unsigned base = second ? a_o1[i] : a_o0[i];
+      const unsigned off = ((a_mask[i] >> tap) & 1u) ? base + sadd : OOB;
+      dma16(rs, off, lds_addr_of(abase + (wave * AI + i) * 1024));
     }
     char* bbase = abase + BM * ROW2;
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
       const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 4) : OOB;
-      llvm_raw_buffer_load_lds(rsw, (__attribute__((address_space(3))) unsigned*)(bbase + (wave * BI + j) * 1024),
-                               16, (int)off, 0, 0, 0);
+      dma16(rsw, off, lds_addr_of(bbase + (wave * BI + j) * 1024));
     }
   };
 
@@ -358,21 +414,21 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nsteps = p.K / BK2;
   const int lr = lane & 31, lh = lane >> 5;
   const int wm0 = wmi * TM, wn0 = wni * TN;
-  issue(0, 0);
+  issue(s_beg, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // two-level accumulation: an MFMA chain of HP stages (32*HP products) starts from zero
   // and is then added into acc -- fp32 error ~sqrt(32 HP) + sqrt(K/(32 HP)) instead of
   // ~sqrt(K); HP*32 ~ sqrt(K) balances both (mkldnn-level accuracy).
   floatx16 part[TI][TJ];
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nsteps) issue(s + 1, buf ^ 1);
+  for (int s = s_beg; s < s_end; ++s) {
+    const int buf = (s - s_beg) & 1;
+    if (s + 1 < s_end) issue(s + 1, buf ^ 1);
     const char* a = lds + buf * STAGE;
     const char* b = a + BM * ROW2;
-    const bool fresh = (s % HP) == 0;
+    const bool fresh = ((s - s_beg) % HP) == 0;
 #pragma unroll
     for (int g = 0; g < BK2 / 8; ++g) {
       const int c = 2 * g + lh;
@@ -398,13 +454,30 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
           part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, part[i][j], 0, 0, 0);
         }
     }
-    if ((s + 1) % HP == 0 || s + 1 == nsteps) {
+    if ((s - s_beg + 1) % HP == 0 || s + 1 == s_end) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
     }
-    __syncthreads();  // hipcc emits vmcnt(0) here: the stage-(s+1) DMA has landed for every wave
+    // stage-(s+1) DMA of this wave has landed, then every wave's (and every wave is done
+    // reading stage s, whose buffer the next step's DMA overwrites)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (tail) {  // raw partial tile -> workspace [tail tile][piece][BM][BN]; conv_tail_fixup finishes
+    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
+        }
+    return;
   }
 
   // ---------------- epilogue: bias, store, BN partial statistics -----------------
@@ -480,6 +553,84 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
       for (int w = 0; w < WM; ++w) s += red[w * BN + cl];
       if (col < p.Cout) p.stats[(size_t)mt * p.Cout + col] = make_float2(mean[j], s);
     }
+  }
+}
+
+// Finish the split tail tiles: fixed-order sum of the K-pieces, bias, store (or accumulate),
+// and the same per-row-block BN partials (mean, M2) the main epilogue writes.
+template <int BM, int BN>
+__global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
+  constexpr int CQ = BN / 4;          // column quads
+  constexpr int G = 1024 / CQ;        // row groups
+  constexpr int RPT = BM / G;         // rows per thread
+  static_assert(RPT >= 1 && BM % G == 0, "fixup geometry");
+  __shared__ float4 red[G][CQ];
+  const int nbn = (p.Cout + BN - 1) / BN, nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  const int wg = nfull + blockIdx.x;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int cq = threadIdx.x % CQ, g = threadIdx.x / CQ;
+  const int col = n0 + cq * 4;
+  const bool cok = col < p.Cout;  // Cout % 4 == 0
+  const float* src = p.part + (size_t)blockIdx.x * p.tsplit * (BM * BN);
+  const float4 bias = (p.bias != nullptr && cok) ? *reinterpret_cast<const float4*>(p.bias + col)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v[RPT];
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = g + i * G;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < p.tsplit; ++k) {
+      const float4 q = *reinterpret_cast<const float4*>(src + (size_t)k * (BM * BN) + r * BN + cq * 4);
+      a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+    }
+    a.x += bias.x; a.y += bias.y; a.z += bias.z; a.w += bias.w;
+    v[i] = a;
+    const int row = m0 + r;
+    if (row < p.P && cok) {
+      float* dst = p.y + (size_t)row * p.ldy + col;
+      if (p.accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(dst);
+        *reinterpret_cast<float4*>(dst) = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
+      } else {
+        *reinterpret_cast<float4*>(dst) = a;
+      }
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  if (p.stats == nullptr) return;
+  red[g][cq] = s;
+  __syncthreads();
+  const int cnt = min(BM, p.P - m0);
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < G; ++k) {
+    const float4 q = red[k][cq];
+    t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+  }
+  const float inv = 1.f / (float)cnt;
+  const float4 mean = make_float4(t.x * inv, t.y * inv, t.z * inv, t.w * inv);
+  __syncthreads();
+  float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    if (m0 + g + i * G < p.P) {
+      const float dx = v[i].x - mean.x, dy = v[i].y - mean.y, dz = v[i].z - mean.z, dw = v[i].w - mean.w;
+      m2.x += dx * dx; m2.y += dy * dy; m2.z += dz * dz; m2.w += dw * dw;
+    }
+  }
+  red[g][cq] = m2;
+  __syncthreads();
+  if (g == 0 && cok) {
+    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < G; ++k) {
+      const float4 q = red[k][cq];
+      u.x += q.x; u.y += q.y; u.z += q.z; u.w += q.w;
+    }
+    float2* st = p.stats + (size_t)mt * p.Cout + col;
+    st[0] = make_float2(mean.x, u.x); st[1] = make_float2(mean.y, u.y);
+    st[2] = make_float2(mean.z, u.z); st[3] = make_float2(mean.w, u.w);
   }
 }
 
@@ -689,11 +840,39 @@ static int launch_fwd(const ConvParams& p, hipStream_t st) {
 }
 
 template <int BM, int BN, int WM, int WN, int HP>
-static int launch_fwd_v2(const ConvParams& p, hipStream_t st) {
+static int launch_fwd_v2(ConvParams p, hipStream_t st, void* ws, size_t ws_bytes) {
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const int T = nbm * nbn;
   const size_t lds = (size_t)2 * (BM + BN) * ROW2;
-  hipLaunchKernelGGL((conv_fwd_v2_kernel<BM, BN, WM, WN, HP>), dim3(nbm * nbn), dim3(256), lds, st, p);
+  // workgroups resident at once (occupancy x CUs), queried once per instantiation
+  static int slots = [&] {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_v2_kernel<BM, BN, WM, WN, HP>, 256, lds);
+    return std::max(1, per_cu) * std::max(1, cus);
+  }();
+  // tail split: when the last round of workgroups would be under half full, cut its tiles
+  // into F K-pieces so that round runs on ~F x more CUs for 1/F of the time
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  const int nall = p.K / BK2;
+  const int rem = T % slots;
+  static const bool tail_on = [] {
+    const char* e = getenv("SRPDE_CONV_TAIL");  // tuning/diagnostics: 0 disables the split
+    return !e || atoi(e) != 0;
+  }();
+  if (tail_on && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
+    int F = std::min(std::min(slots / rem, nall / 2), 8);
+    while (F >= 2 && (size_t)rem * F * BM * BN * sizeof(float) > ws_bytes) --F;
+    if (F >= 2) { p.ntail = rem; p.tsplit = F; p.part = static_cast<float*>(ws); }
+  }
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  hipLaunchKernelGGL((conv_fwd_v2_kernel<BM, BN, WM, WN, HP>), dim3(grid), dim3(256), lds, st, p);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd(v2)");
+  if (p.ntail > 0) {
+    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN>), dim3(p.ntail), dim3(1024), 0, st, p);
+    SRPDE_LAUNCH_CHECK("srpde_conv_fwd(tail fixup)");
+  }
   return 0;
 }
 
@@ -755,10 +934,17 @@ size_t srpde_conv_stats_blocks(int n, int h, int w, int cout) {
 
 int srpde_conv_stats_rows_per_block(int cout) { return fwd_bm(fwd_config(cout)); }
 
+// tail-split scratch: at most one round of workgroups worth of fp32 tiles (<= 1024 slots)
+size_t srpde_conv_fwd_workspace_size(int cout) {
+  const int bm = fwd_bm(fwd_config(cout));
+  const int bn = cout % 128 == 0 ? 128 : (cout % 64 == 0 ? 64 : 32);
+  return (size_t)1024 * bm * bn * sizeof(float);
+}
+
 int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1,
                    const float* wpack, const float* bias, float* y, int ldy,
                    int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
-                   float* stats, hipStream_t stream) {
+                   float* stats, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wpack && y, "srpde_conv_fwd: null pointer");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd: bad shape");
   SRPDE_CHECK_ARG(ksize == 1 || ksize == 3, "srpde_conv_fwd: ksize must be 1 or 3");
@@ -776,17 +962,18 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   if (v2_ok(p)) {
     switch (fwd_config(cout)) {
       case 0:
         switch (conv_hp()) {
-          case 1: return launch_fwd_v2<128, 128, 2, 2, 1>(p, stream);
-          case 2: return launch_fwd_v2<128, 128, 2, 2, 2>(p, stream);
-          case 1000: return launch_fwd_v2<128, 128, 2, 2, 1000000>(p, stream);
-          default: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream);
+          case 1: return launch_fwd_v2<128, 128, 2, 2, 1>(p, stream, workspace, ws_bytes);
+          case 2: return launch_fwd_v2<128, 128, 2, 2, 2>(p, stream, workspace, ws_bytes);
+          case 1000: return launch_fwd_v2<128, 128, 2, 2, 1000000>(p, stream, workspace, ws_bytes);
+          default: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream, workspace, ws_bytes);
         }
-      case 1: return launch_fwd_v2<256, 64, 4, 1, 4>(p, stream);
-      default: return launch_fwd_v2<256, 32, 4, 1, 4>(p, stream);
+      case 1: return launch_fwd_v2<256, 64, 4, 1, 4>(p, stream, workspace, ws_bytes);
+      default: return launch_fwd_v2<256, 32, 4, 1, 4>(p, stream, workspace, ws_bytes);
     }
   }
   switch (fwd_config(cout)) {

@@ -52,8 +52,22 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     else:
         p1, ld1, c1 = 0, 0, 0
     py, ldy = _pl(y)
+    ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
-         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), stream_ptr())
+         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+_SCRATCH = {}
+
+
+def _scratch(nbytes, device):
+    """Per-device scratch reused by stream-ordered kernels (tail-split partial tiles)."""
+    key = (device.type, device.index)
+    buf = _SCRATCH.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _SCRATCH[key] = buf
+    return buf
 
 
 def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
