@@ -373,23 +373,28 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
   const int nall = p.K / BK2;
   const int s_beg = tail ? (piece * nall) / p.tsplit : 0;
   const int s_end = tail ? ((piece + 1) * nall) / p.tsplit : nall;
-  // scalar K-walk state of the next stage to issue: (tap = ky*ksize + kx, channel offset)
-  int nx_tap = (s_beg * BK2) / p.Cin, nx_ch = s_beg * BK2 - nx_tap * p.Cin;
+  // scalar K-walk state of the next stage to issue.  Stages run channel-chunk-major, tap
+  // minor (stage s = chunk * taps + tap): the taps of one 32-channel chunk re-read the same
+  // ~(BM + halo) x 128 B of activations back to back, so they hit in L2 instead of being
+  // re-fetched once per tap after a whole-Cin sweep.
+  const int taps = p.ksize * p.ksize;
+  int nx_tap = s_beg % taps, nx_ch = (s_beg / taps) * BK2;
   int nx_ky = nx_tap / p.ksize, nx_kx = nx_tap - nx_ky * p.ksize;
   auto issue = [&](int s, int buf) {
-    const int k0 = s * BK2;
+    (void)s;
     const int tap = nx_tap, ch0 = nx_ch;
+    const int k0 = tap * p.Cin + ch0;
     const int tsh = ((nx_ky - kc) * p.W + (nx_kx - kc)) * p.dil * p.sign;  // pixel shift of this tap
     const bool second = ch0 >= p.c0;
     const int32x4 rs = second ? rs1 : rs0;
     const int ld = second ? ld1 : p.ldx0;
     const int cb = second ? ch0 - p.c0 : ch0;
     const unsigned sadd = (unsigned)((tsh * ld + cb) * 4);
-    nx_ch += BK2;
-    if (nx_ch == p.Cin) {
-      nx_ch = 0;
-      ++nx_tap;
-      if (++nx_kx == p.ksize) { nx_kx = 0; ++nx_ky; }
+    ++nx_tap;
+    if (++nx_kx == p.ksize) { nx_kx = 0; ++nx_ky; }
+    if (nx_tap == taps) {
+      nx_tap = 0; nx_ky = 0; nx_kx = 0;
+      nx_ch += BK2;
     }
     char* abase = lds + buf * STAGE;
 #pragma unroll
@@ -785,6 +790,177 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     }
 }
 
+// ------------------- weight gradient v2: LDS-DMA staged, BKW pixels -------------------
+// For c0 % 32 == 0 and c1 % 32 == 0.  Both GEMM operands are pixel-major in HBM (dY[p][m],
+// X[p + off(tap)][c]); a stage is BKW pixels of each.  LDS keeps every operand as 32-column
+// groups [group][pixel][32 floats] (128-B rows; group stride padded by 128 B so the two groups
+// a half-wave reads sit on different banks).  One DMA wave-instruction fills 8 pixels x 32
+// columns of ONE group, so its (tap, source tensor) is wave-uniform; padding taps and pixels
+// past the chunk use the out-of-range offset (hardware zero fill).  MFMA operands need no
+// transpose: lane (r, h) reads QA consecutive dY channels of pixel 2kp+h with one ds_read, and
+// channel q of that read feeds output tile q, whose rows are the interleaved channels
+// wm0 + QA*r + q (same for the QB X columns).
+constexpr int BKW = 32;                  // pixels per stage (= 4 waves x 8-pixel row blocks)
+constexpr int GSTR = BKW * 128 + 128;    // LDS bytes per 32-column group (+128 B bank pad)
+
+template <int Q>
+struct vecf;
+template <> struct vecf<1> { typedef float t; };
+template <> struct vecf<2> { typedef float2 t; };
+template <> struct vecf<4> { typedef float4 t; };
+__device__ __forceinline__ float vget(float v, int) { return v; }
+__device__ __forceinline__ float vget(float2 v, int q) { return q == 0 ? v.x : v.y; }
+__device__ __forceinline__ float vget(float4 v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
+
+template <int BM, int BN, int WM, int WN, int HP>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_v2_kernel(WgradParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN, QA = TM / 32, QB = TN / 32;
+  constexpr int GA = BM / 32, GB = BN / 32;  // column groups; wave w loads row block w of each
+  static_assert(BKW == 32, "4 waves x 8 rows");
+  static_assert(QA == 1 || QA == 2 || QA == 4, "QA");
+  static_assert(QB == 1 || QB == 2 || QB == 4, "QB");
+  constexpr int STAGE = (GA + GB) * GSTR;
+  typedef typename vecf<QA>::t va_t;
+  typedef typename vecf<QB>::t vb_t;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbm = (p.Cout + BM - 1) / BM, nbn = (p.K + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  // consecutive logical blocks = tiles of one pixel chunk -> same XCD (shared dY / X rows)
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / nbn, nt = tile - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int HW = p.H * p.W, kc = p.ksize >> 1;
+
+  const int32x4 rsy = make_rsrc(p.dy, (unsigned)((size_t)p.P * p.lddy * 4));
+  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * ld1 * 4));
+  const int sub = lane >> 3, c4 = (lane & 7) * 4;
+
+  // per-group constants (wave-uniform): dY column byte offset / validity, and for X the tap
+  // shift, the source tensor and the channel byte offset of the group's first column
+  int a_colb[GA];
+  bool a_ok[GA];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int m = m0 + 32 * g + c4;
+    a_ok[g] = m < p.Cout;
+    a_colb[g] = m * 4;
+  }
+  int b_dy[GB], b_dx[GB], b_sh[GB], b_chb[GB];
+  bool b_ok[GB], b_second[GB];
+#pragma unroll
+  for (int g = 0; g < GB; ++g) {
+    const int kg = n0 + 32 * g;
+    b_ok[g] = kg < p.K;
+    const int tap = b_ok[g] ? kg / p.Cin : 0;
+    const int ch = kg - tap * p.Cin;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    b_dy[g] = (ky - kc) * p.dil;
+    b_dx[g] = (kx - kc) * p.dil;
+    b_sh[g] = b_dy[g] * p.W + b_dx[g];
+    b_second[g] = ch >= p.c0;
+    b_chb[g] = ((b_second[g] ? ch - p.c0 : ch) + c4) * 4;
+  }
+
+  auto issue = [&](int pbase, int buf) {
+    const int pix = pbase + wave * 8 + sub;
+    const bool pok = pix < pend;
+    const int n = pix / HW, rem = pix - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+    char* abase = lds + buf * STAGE + wave * 1024;
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const unsigned off = (pok && a_ok[g]) ? (unsigned)(pix * p.lddy * 4 + a_colb[g]) : OOB;
+      dma16(rsy, off, lds_addr_of(abase + g * GSTR));
+    }
+    char* bbase = abase + GA * GSTR;
+#pragma unroll
+    for (int g = 0; g < GB; ++g) {
+      const int iy = yy + b_dy[g], ix = xx + b_dx[g];
+      const bool ok = pok && b_ok[g] && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      const int ld = b_second[g] ? ld1 : p.ldx0;
+      const unsigned off = ok ? (unsigned)((pix + b_sh[g]) * ld * 4 + b_chb[g]) : OOB;
+      dma16(b_second[g] ? rs1 : rs0, off, lds_addr_of(bbase + g * GSTR));
+    }
+  };
+
+  floatx16 acc[QA][QB], part[QA][QB];
+#pragma unroll
+  for (int i = 0; i < QA; ++i)
+#pragma unroll
+    for (int j = 0; j < QB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  // per-lane operand read offsets inside a stage (pixel row lh; + 256 B per k-pair)
+  const int ma = wm0 + QA * lr, nb = wn0 + QB * lr;
+  const int a_rd = (ma >> 5) * GSTR + (ma & 31) * 4 + lh * 128;
+  const int b_rd = GA * GSTR + (nb >> 5) * GSTR + (nb & 31) * 4 + lh * 128;
+
+  const int nsteps = (pend - pbeg + BKW - 1) / BKW;
+  if (nsteps > 0) issue(pbeg, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) issue(pbeg + (s + 1) * BKW, buf ^ 1);
+    const char* st = lds + buf * STAGE;
+    const bool fresh = (s % HP) == 0;
+#pragma unroll
+    for (int kp = 0; kp < BKW / 2; ++kp) {
+      const va_t av = *reinterpret_cast<const va_t*>(st + a_rd + kp * 256);
+      const vb_t bv = *reinterpret_cast<const vb_t*>(st + b_rd + kp * 256);
+#pragma unroll
+      for (int i = 0; i < QA; ++i)
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+          const floatx16 c0 = (kp == 0 && fresh) ? floatx16{} : part[i][j];
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av, i), vget(bv, j), c0, 0, 0, 0);
+        }
+    }
+    if ((s + 1) % HP == 0 || s + 1 == nsteps) {
+#pragma unroll
+      for (int i = 0; i < QA; ++i)
+#pragma unroll
+        for (int j = 0; j < QB; ++j) acc[i][j] += part[i][j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // slab [split][Cout][K]: tile (i, j) element (row rc, col lr) is dW[wm0+QA*rc+i][wn0+QB*lr+j]
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+  const int n = n0 + nb;
+  if (n < p.K) {
+#pragma unroll
+    for (int i = 0; i < QA; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rc = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int m = m0 + wm0 + QA * rc + i;
+        if (m < p.Cout) {
+          float* dst = out + (size_t)m * p.K + n;
+          if constexpr (QB == 1) {
+            dst[0] = acc[i][0][r];
+          } else if constexpr (QB == 2) {
+            *reinterpret_cast<float2*>(dst) = make_float2(acc[i][0][r], acc[i][1][r]);
+          } else {
+            *reinterpret_cast<float4*>(dst) = make_float4(acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]);
+          }
+        }
+      }
+  }
+}
+
 // sum the split-K slabs in fixed order, write dW in torch layout [Cout][Cin_real][k][k]
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, int splits,
                                     int cout, int cin, int cin_real, int taps, int accumulate) {
@@ -903,6 +1079,33 @@ static int launch_wgrad(const WgradParams& p, hipStream_t st) {
   return 0;
 }
 
+template <int BM, int BN, int WM, int WN>
+static int launch_wgrad_v2(const WgradParams& p, hipStream_t st) {
+  const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
+  const size_t lds = (size_t)2 * (BM / 32 + BN / 32) * GSTR;
+  hipLaunchKernelGGL((conv_wgrad_v2_kernel<BM, BN, WM, WN, 2>), dim3(nb), dim3(256), lds, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(v2)");
+  return 0;
+}
+
+// Cout = 64 tile: 64x256 (1 workgroup/CU by LDS) or 64x128 (2/CU); SRPDE_WGRAD64 tuning
+static bool wgrad64_wide() {
+  static const bool wide = [] {
+    const char* e = getenv("SRPDE_WGRAD64");
+    return e && atoi(e) != 0;
+  }();
+  return wide;
+}
+
+static bool wgrad_v2_ok(const WgradParams& p) {
+  static const bool on = [] {
+    const char* e = getenv("SRPDE_WGRAD_V2");  // tuning/diagnostics: 0 = register-staged kernel
+    return !e || atoi(e) != 0;
+  }();
+  const long long maxld = std::max(std::max(p.ldx0, p.c1 ? p.ldx1 : 0), p.lddy);
+  return on && p.c0 % 32 == 0 && p.c1 % 32 == 0 && (long long)p.P * maxld * 4 < (1LL << 31);
+}
+
 static void wgrad_tiles(int cout, int K, int* bm, int* bn) {
   if (cout >= 128) { *bm = 128; *bn = 128; }
   else if (cout >= 64) { *bm = 64; *bn = 256; }
@@ -914,9 +1117,11 @@ static void wgrad_split(int P, int cout, int K, int* chunk, int* splits) {
   int bm, bn;
   wgrad_tiles(cout, K, &bm, &bn);
   const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
-  long long want = (2048 + tiles - 1) / tiles;           // ~8 blocks per CU in flight
+  // at most 2048 workgroups (= whole rounds of 256 CUs x 1|2 resident): rounding the split
+  // count UP would leave a nearly empty last round (e.g. 36 tiles x 57 = 2052 = 4 rounds + 4)
+  long long want = std::max(1LL, 2048 / tiles);
   long long c = (P + want - 1) / want;
-  c = (c + BKP - 1) / BKP * BKP;
+  c = (c + BKW - 1) / BKW * BKW;  // multiple of both stage sizes (BKP | BKW)
   if (c < 256) c = 256;
   *chunk = (int)c;
   *splits = ceil_div(P, c);
@@ -1012,9 +1217,16 @@ int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx
   p.part = static_cast<float*>(workspace);
   int bm, bn, rc;
   wgrad_tiles(cout, p.K, &bm, &bn);
-  if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream);
-  else if (bm == 64) rc = launch_wgrad<64, 256, 1, 4>(p, stream);
-  else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
+  if (wgrad_v2_ok(p)) {
+    if (bm == 128) rc = launch_wgrad_v2<128, 128, 2, 2>(p, stream);
+    else if (bm == 64) rc = wgrad64_wide() ? launch_wgrad_v2<64, 256, 1, 4>(p, stream)
+                                           : launch_wgrad_v2<64, 128, 1, 4>(p, stream);
+    else rc = launch_wgrad_v2<32, 256, 1, 4>(p, stream);
+  } else {
+    if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream);
+    else if (bm == 64) rc = launch_wgrad<64, 256, 1, 4>(p, stream);
+    else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
+  }
   if (rc) return rc;
   const int taps = ksize * ksize;
   const long long total = (long long)cout * p.K;

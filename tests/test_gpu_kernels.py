@@ -30,7 +30,9 @@ def rel(a, b):
 @pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
     (2, 64, 0, 64, 40, 1), (3, 128, 0, 256, 10, 1), (2, 256, 0, 512, 10, 2), (2, 512, 256, 256, 10, 1),
     (2, 128, 64, 64, 40, 1), (2, 32, 0, 16, 40, 1), (2, 64, 0, 32, 40, 1), (1, 4, 0, 64, 40, 1),
-    (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1)])
+    (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1),
+    # ragged: P % 32 != 0, Cout not a tile multiple, K = 864 not a tile multiple, dil 2 on 7x7
+    (3, 64, 32, 96, 7, 2), (16, 128, 0, 128, 20, 1)])
 def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil):
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator().manual_seed(n * 1000 + cout + cin0)

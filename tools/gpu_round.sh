@@ -1,10 +1,21 @@
-# usage: bash tools/gpu_round.sh TAG  -- tests + bench + kernel-trace profile, each step time-limited
+# Round-end evidence on one MI355X: full GPU tests, smoke, bench line, kernel-trace stats of
+# the bench command, and HBM traffic PMC passes for the roofline kernel (bridge.3 fwd conv).
+# usage: bash tools/gpu_round.sh TAG     (outputs under gpurun_out/, copy what is judged to profiles/)
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+T=${1:-final}
+R=$GRAFT_REPO_ROOT
+cd $R
 export TMPDIR=/tmp
-TAG=${1:-x}
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_$TAG.log 2>&1; echo "pytest rc=$?"
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 10 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; exit 1; }
-echo "bench ok"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log 2>&1
-echo "prof rc=$?"
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_$T.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_$T.log; exit 1; }
+tail -1 gpurun_out/pytest_$T.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$T.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke_$T.log; exit 1; }
+timeout -k 10 400 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { echo "bench failed"; tail -20 gpurun_out/bench_$T.err; exit 1; }
+cat gpurun_out/bench_$T.json
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o bench -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$T.log 2>&1 || { echo "prof failed"; exit 1; }
+i=0
+for C in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_$T -o p$i -- python $R/tools/conv_bench.py --layers bridge.3 --only fwd --iters 3 > $R/gpurun_out/pmc_${T}_$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+done
+echo "round evidence done"
