@@ -53,6 +53,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--workload", choices=("train", "poisson", "cascade"), default="train",
+                    help="train = the BASELINE metric (default); poisson = config #3 CG data-gen solve; "
+                         "cascade = config #5 20->640 multi-level inference")
+    ap.add_argument("--poisson-sizes", default="40:1024,80:1024,160:64,320:16,640:4",
+                    help="n:B pairs for --workload poisson")
+    ap.add_argument("--checkpoint", default=None, help="--workload cascade: model_state_dict checkpoint")
     return ap.parse_args()
 
 
@@ -81,6 +87,182 @@ def cpu_baseline(seconds):
                       f"{dt:.1f}s, torch {torch.__version__} threads={threads}"}
 
 
+def cpu_baseline_poisson(seconds, sizes=(40, 80)):
+    """Oracle spsolve (the reference's SciPy SuperLU call) per problem on the host."""
+    import numpy as np
+    from oracle import poisson_ref as R
+    out, rng = {}, np.random.default_rng(7)
+    per = seconds / len(sizes)
+    for n in sizes:
+        k = rng.uniform(0.5, 12.0, 2)
+        f = R.forcing(k[0], k[1], n)
+        th = rng.uniform(0.5, 2.0, (n, n))
+        R.solve(f, th)
+        cnt, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < per or cnt < 2:
+            R.solve(f, th)
+            cnt += 1
+        out[n] = cnt / (time.perf_counter() - t0)
+    return out
+
+
+def run_poisson(args, world, rank, dev):
+    """Config #3: batched on-device CG (HIP) solves/s.  Each rank solves its own B problems
+    per size (independent units, weak scaling, no collective)."""
+    import numpy as np
+    from superresolution_for_pdes_amd import poisson as P
+    sizes = [tuple(int(v) for v in s.split(":")) for s in args.poisson_sizes.split(",")]
+    rng = np.random.default_rng(100 + rank)
+    levels = {}
+    for n, B in sizes:
+        k = rng.uniform(0.5, 12.0, (B, 2))
+        f = P.forcing_batched(k, n, device=dev)
+        th = torch.from_numpy(rng.uniform(0.5, 2.0, (B, n, n))).to(dev)
+        u, it = P.solve_batched(f, th, device=dev, return_iters=True)   # warm-up (+ iteration counts)
+        reps = max(1, min(args.steps, 5 if n >= 320 else args.steps))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            u, it = P.solve_batched(f, th, device=dev, return_iters=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt)
+        iters = float(it.double().mean())
+        t = el / reps
+        pts_it = B * n * n * iters
+        lv = {"B": B, "solves_per_s": round(world * B / t, 2), "ms_per_batch": round(1e3 * t, 3),
+              "mean_iters": round(iters, 1)}
+        if n <= 128:   # LDS-resident: fp64 VALU bound, 19 flop / point / iteration (SURVEY 8(d))
+            lv["fp64_tflops"] = round(19 * pts_it / t / 1e12, 3)
+            lv["fp64_frac"] = round(19 * pts_it / t / 78.6e12, 4)
+        else:          # grid CG: HBM bound, 88 B / point / iteration
+            lv["hbm_gbs"] = round(88 * pts_it / t / 1e9, 1)
+            lv["hbm_frac"] = round(88 * pts_it / t / 8.0e12, 4)
+        levels[n] = lv
+    if rank != 0:
+        return
+    head = levels.get(80) or next(iter(levels.values()))
+    big = max(levels)
+    rec = {"metric": "Poisson CG solves/s (batched fp64 5-point, rtol 1e-12)",
+           "value": head["solves_per_s"], "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+           "warmup": 1, "ms_per_step": head["ms_per_batch"], "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic: f = sin(2 pi k1 x) sin(2 pi k2 y), k ~ U(0.5,12), theta ~ U(0.5,2), in HBM",
+           "config": {"workload": "config #3 on-device data-gen solve, headline n=80 B=1024/GPU",
+                      "levels": {str(k): v for k, v in levels.items()}},
+           "roofline": {"bound": "hbm", "kernel": f"poisson_cg_grid[n={big}]",
+                        "achieved": levels[big].get("hbm_gbs"), "peak": 8000.0, "unit": "GB/s",
+                        "frac": levels[big].get("hbm_frac"), "traffic": None}}
+    if not args.no_cpu_baseline and world == 1:
+        cb = cpu_baseline_poisson(min(args.cpu_seconds, 10.0))
+        rec["cpu_baseline"] = {"value": round(cb[80], 2), "unit": "solves/s", "cores": 1, "kind": "port",
+                               "sample": "scipy spsolve(diag(theta) L, f) per problem (the reference's call), "
+                                         + ", ".join(f"n={n}: {v:.1f}/s" for n, v in cb.items())}
+    print(json.dumps(rec), flush=True)
+
+
+def cpu_baseline_cascade(st, data, seconds):
+    """The reference's cascade loop (batch-1 forwards, resolution_comparison.py:203-223) on
+    the oracle U-Net, host cores; one full 20->640 pass (bounded by its own length)."""
+    import numpy as np
+    from oracle import unet_ref as U, poisson_ref as R
+    import torch.nn.functional as F
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    cur, res, nf = np.asarray(data["u"][20]), 20, 0
+    with torch.no_grad():
+        while res < 640:
+            nxt = 2 * res
+            u32 = torch.tensor(np.asarray(data["u"][nxt]), dtype=torch.float32)
+            f32 = torch.tensor(np.asarray(data["f"][nxt]), dtype=torch.float32)
+            t32 = torch.tensor(np.asarray(data["theta"][nxt]), dtype=torch.float32)
+            um, us, fm, fs, tm, ts = u32.mean(), u32.std(), f32.mean(), f32.std(), t32.mean(), t32.std()
+            uc, ft, tt = R.split(cur, 20), R.split(np.asarray(data["f"][nxt]), 40), R.split(
+                np.asarray(data["theta"][nxt]), 40)
+            rows = []
+            for ra, rb, rc in zip(uc, ft, tt):
+                row = []
+                for a, b, c in zip(ra, rb, rc):
+                    x0 = F.interpolate(((torch.tensor(a, dtype=torch.float32) - um) / us)[None, None],
+                                       size=(40, 40), mode="bilinear", align_corners=True)
+                    x = torch.cat([x0, ((torch.tensor(c, dtype=torch.float32) - tm) / ts)[None, None],
+                                   ((torch.tensor(b, dtype=torch.float32) - fm) / fs)[None, None]], 1)
+                    row.append((U.unet_forward(st, x, training=False) * us + um)[0, 0].double().numpy())
+                    nf += 1
+                rows.append(row)
+            cur, res = R.stitch(rows), nxt
+            if time.perf_counter() - t0 > 4 * seconds:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": round(dt * 1e3, 1), "unit": "ms per 20->640 cascade", "cores": threads, "kind": "port",
+            "sample": f"{nf} batch-1 oracle U-Net forwards (the reference's loop) in {dt:.2f}s, "
+                      f"torch {torch.__version__} threads={threads}"}
+
+
+def run_cascade(args, world, rank, dev):
+    """Config #5: 20->640 multi-level cascade (5 levels; 256 tiles at the last), ground truth by
+    the HIP CG at every resolution; subtrees sharded over ranks for N>1."""
+    import numpy as np
+    from superresolution_for_pdes_amd.models import UNet, init_weights
+    from superresolution_for_pdes_amd import resolution_comparison as RC
+    torch.manual_seed(42)
+    model = UNet()
+    model.apply(init_weights)
+    if args.checkpoint:
+        ck = torch.load(args.checkpoint, map_location="cpu", weights_only=True)
+        model.load_state_dict(ck.get("model_state_dict", ck))
+    model = model.to(dev).eval()
+    np.random.seed(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    data = RC.solve_multi_resolution(n_coarse=20, resolutions=(40, 80, 160, 320, 640), device=dev)
+    torch.cuda.synchronize()
+    gt_s = time.perf_counter() - t0
+    dd = {k: {r: torch.as_tensor(v).to(dev) for r, v in data[k].items()} for k in ("u", "f", "theta")}
+    for _ in range(max(1, args.warmup)):
+        pred = RC.ml_multi_level_upscale(model, dd, 640, device=dev, start_resolution=20, return_tensor=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pred = RC.ml_multi_level_upscale(model, dd, 640, device=dev, start_resolution=20, return_tensor=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt)
+    if rank != 0:
+        return
+    m = RC.cascade_metrics(pred.cpu().numpy(), data["u"][640])
+    ms = 1e3 * el / args.steps
+    tiles = 1 + 4 + 16 + 64 + 256
+    rec = {"metric": "20->640 cascade latency (5 levels, 256 tiles at the last)", "value": round(ms, 3),
+           "unit": "ms", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+           "higher_is_better": False, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic: solve_multi_resolution seed 0 (k ~ U(10,11), theta ~ U(0.5,2)); "
+                   + ("checkpoint " + os.path.basename(args.checkpoint) if args.checkpoint else "random-init U-Net"),
+           "config": {"workload": "config #5 cascade 20->640, eval-mode U-Net, subtrees sharded over ranks",
+                      "tiles": tiles, "last_level_batch": 256 // world if world <= 16 else None,
+                      "gt_solve_s": round(gt_s, 3), "rmse_vs_gt640": m["rmse"], "mae_vs_gt640": m["mae"],
+                      "tiles_per_s": round(tiles / (ms * 1e-3), 1)}}
+    if not args.no_cpu_baseline and world == 1:
+        st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        rec["cpu_baseline"] = cpu_baseline_cascade(st, data, args.cpu_seconds)
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,6 +273,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.workload != "train":
+        (run_poisson if args.workload == "poisson" else run_cascade)(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from superresolution_for_pdes_amd.models import UNet, init_weights
     from superresolution_for_pdes_amd.functional import mse_loss

@@ -48,7 +48,7 @@ class GlobalNormalization:
     """resolution_comparison.py:160-181 (fp32 statistics, unbiased std)."""
 
     def __init__(self, u_fine, u_coarse, f_fine, theta_fine, device="cuda"):
-        t = lambda a: torch.as_tensor(np.asarray(a)).to(device=device, dtype=torch.float32)  # noqa: E731
+        t = lambda a: _field(a, device, torch.float32)  # noqa: E731
         u_fine, f_fine, theta_fine = t(u_fine), t(f_fine), t(theta_fine)
         self.u_mean, self.u_std = u_fine.mean(), u_fine.std()
         self.f_mean, self.f_std = f_fine.mean(), f_fine.std()
@@ -87,11 +87,29 @@ def stitch_subdomains(subdomains: list) -> np.ndarray:
     return out
 
 
+def _blocks_to_tiles(b: torch.Tensor, s: int) -> torch.Tensor:
+    """[nb, S, S] -> [nb * (S/s)^2, s, s]: block-major, row-major tiles inside each block."""
+    nb, S, _ = b.shape
+    m = S // s
+    return b.reshape(nb, m, s, m, s).permute(0, 1, 3, 2, 4).reshape(nb * m * m, s, s)
+
+
+def _tiles_to_blocks(t: torch.Tensor, nb: int) -> torch.Tensor:
+    """inverse of _blocks_to_tiles: [nb * m^2, s, s] -> [nb, m*s, m*s]."""
+    T, s, _ = t.shape
+    m = int(round((T // nb) ** 0.5))
+    return t.reshape(nb, m, m, s, s).permute(0, 1, 3, 2, 4).reshape(nb, m * s, m * s)
+
+
 def _level_inputs(u_cur, f_next, th_next, norm, tile=20):
-    """Normalised model inputs for every tile of one level: [T, 3, 2*tile, 2*tile]."""
-    uc = _tiles(u_cur.float(), tile)
-    ft = _tiles(f_next.float(), 2 * tile)
-    tt = _tiles(th_next.float(), 2 * tile)
+    """Normalised model inputs for every tile of one level: [T, 3, 2*tile, 2*tile].
+
+    Fields are [S, S] (whole domain) or [nb, S, S] blocks (a rank's subtrees)."""
+    if u_cur.dim() == 2:
+        u_cur, f_next, th_next = u_cur[None], f_next[None], th_next[None]
+    uc = _blocks_to_tiles(u_cur.float(), tile)
+    ft = _blocks_to_tiles(f_next.float(), 2 * tile)
+    tt = _blocks_to_tiles(th_next.float(), 2 * tile)
     ucn = (uc - norm.u_mean) / norm.u_std
     fn = (ft - norm.f_mean) / norm.f_std
     tn = tt if norm.theta_is_constant else (tt - norm.theta_mean) / norm.theta_std
@@ -108,25 +126,74 @@ def upscale_subdomain(model, u_coarse, f_fine, theta_fine, global_norm, device="
     return y.squeeze().double().cpu().numpy()
 
 
+def _field(a, device, dtype=None):
+    t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a))
+    return t.to(device=device, dtype=dtype or t.dtype)
+
+
+def _shard(shard):
+    if shard is not None:
+        return shard
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 @torch.no_grad()
 def ml_multi_level_upscale(model, data: dict, target_resolution: int, device: str = "cuda",
                            start_resolution: int = 40, tile: int = 20, return_tensor: bool = False,
-                           max_batch: int = 4096):
-    """resolution_comparison.py:183-229 with one batched U-Net forward per level."""
+                           max_batch: int = 4096, shard=None):
+    """resolution_comparison.py:183-229 with one batched U-Net forward per level.
+
+    Multi-GPU: a level-(L+1) tile depends on one quadrant of one level-L
+    tile only, so the cascade is a forest.  Levels with fewer tiles than ranks run on every
+    rank (1 and 4 tiles for 20 -> 640); at the first level with >= world tiles each rank
+    takes a contiguous share of them as subtree roots and carries only its own blocks down
+    to the target resolution; one all-gather assembles the field.  The per-level
+    normalisation statistics come from the (replicated) ground truth, so the subtrees need
+    no other exchange.  ``shard`` = (rank, world); default: the torch.distributed world."""
     model.eval()
+    rank, world = _shard(shard)
     cur_res = start_resolution
-    cur = torch.as_tensor(np.asarray(data["u"][cur_res])).to(device=device, dtype=torch.float64)
+    cur = _field(data["u"][cur_res], device, torch.float64)[None]   # [nb, S, S] blocks
+    roots, m_split = None, None     # owned root-tile indices, tiles per side at the split level
     while cur_res < target_resolution:
         nxt = cur_res * 2
+        if roots is None and world > 1 and (cur_res // tile) ** 2 >= world:
+            m_split = cur_res // tile
+            roots = np.array_split(np.arange(m_split * m_split), world)[rank]
+            cur = _blocks_to_tiles(cur, tile)[torch.as_tensor(roots, device=cur.device)]
         norm = GlobalNormalization(data["u"][nxt], None, data["f"][nxt], data["theta"][nxt], device=device)
-        f_next = torch.as_tensor(np.asarray(data["f"][nxt])).to(device)
-        th_next = torch.as_tensor(np.asarray(data["theta"][nxt])).to(device)
+        f_next = _field(data["f"][nxt], device)[None]
+        th_next = _field(data["theta"][nxt], device)[None]
+        if roots is not None:  # this rank's regions of the next-level forcing / coefficient
+            s2 = nxt // m_split
+            idx = torch.as_tensor(roots, device=f_next.device)
+            f_next = _blocks_to_tiles(f_next, s2)[idx]
+            th_next = _blocks_to_tiles(th_next, s2)[idx]
         x = _level_inputs(cur, f_next, th_next, norm, tile)
         outs = [model(x[s:s + max_batch]) for s in range(0, x.shape[0], max_batch)]
         y = torch.cat(outs) * norm.u_std + norm.u_mean
-        cur = _stitch(y[:, 0].double())
+        cur = _tiles_to_blocks(y[:, 0].double(), cur.shape[0])
         cur_res = nxt
-    return cur if return_tensor else cur.cpu().numpy()
+    if roots is not None:
+        cur = _gather_blocks(cur, m_split, world)
+    out = cur[0] if cur.shape[0] == 1 else _tiles_to_blocks(cur, 1)[0]
+    return out if return_tensor else out.cpu().numpy()
+
+
+def _gather_blocks(blocks: torch.Tensor, m_split: int, world: int) -> torch.Tensor:
+    """All ranks' subtree blocks -> [m_split^2, S, S] in root order (one all-gather)."""
+    import torch.distributed as dist
+    counts = [len(a) for a in np.array_split(np.arange(m_split * m_split), world)]
+    cmax = max(counts)
+    S = blocks.shape[-1]
+    pad = blocks.new_zeros(cmax, S, S)
+    pad[:blocks.shape[0]] = blocks
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([parts[r][:counts[r]] for r in range(world)])
 
 
 def cascade_metrics(pred: np.ndarray, gt: np.ndarray) -> dict:
