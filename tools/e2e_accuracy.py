@@ -3,7 +3,7 @@ device (config #3), train with the reference's config (train_enhanced.main), the
 reference's resolution comparison (src/resolution_comparison.py:371-430: 40 -> 80/160/320/640
 cascade vs the ground-truth solve, against direct bilinear) with the trained model.
 
-    python tools/e2e_accuracy.py [--epochs 100] [--out gpurun_out/e2e]
+    python tools/e2e_accuracy.py [--epochs 100] [--out /tmp/srpde_e2e]
 Prints one JSON line (timings + the MAE/RMSE table the reference's README reports).
 """
 import argparse
@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=100)
     ap.add_argument("--n", type=int, nargs=2, default=(1000, 1000))
-    ap.add_argument("--out", default="gpurun_out/e2e")
+    ap.add_argument("--out", default="/tmp/srpde_e2e")   # checkpoints stay out of gpurun_out/
     args = ap.parse_args()
     from superresolution_for_pdes_amd import train_enhanced as T
     from superresolution_for_pdes_amd import resolution_comparison as RC
