@@ -50,6 +50,17 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
 /* optional scratch for splitting the last, partially filled round of tiles over K (pass
  * NULL to disable); srpde_conv_fwd_workspace_size() bytes always suffice */
 size_t srpde_conv_fwd_workspace_size(int cout);
+/* The same convolution (same arguments, same output and statistics layout) computed as
+ * fp32 products from exact 3-way bf16 splits of both operands: six partial products per
+ * fp32 product on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32-accurate; see
+ * DESIGN.md).  `wsplit` = srpde_split_weights() of the packed weights.  Needs c0, c1 and
+ * cout multiples of 32 (srpde_conv_x6_supported). */
+int srpde_conv_x6_supported(int c0, int c1, int cout);
+int srpde_split_weights(const float* w, void* planes, long long n, hipStream_t stream);
+int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const void* wsplit,
+                      const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
+                      int sign, int accumulate, float* stats, void* workspace, size_t ws_bytes,
+                      hipStream_t stream);
 size_t srpde_conv_stats_blocks(int n, int h, int w, int cout);
 int srpde_conv_stats_rows_per_block(int cout);
 size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, int ksize);

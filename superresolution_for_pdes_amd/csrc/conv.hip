@@ -563,12 +563,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
 
 // Finish the split tail tiles: fixed-order sum of the K-pieces, bias, store (or accumulate),
 // and the same per-row-block BN partials (mean, M2) the main epilogue writes.
-template <int BM, int BN>
+// SRB = rows per BN-statistics block (srpde_conv_stats_rows_per_block); a tile of BM rows
+// writes BM / SRB statistics rows.
+template <int BM, int BN, int SRB = BM>
 __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
   constexpr int CQ = BN / 4;          // column quads
   constexpr int G = 1024 / CQ;        // row groups
   constexpr int RPT = BM / G;         // rows per thread
+  constexpr int NSB = BM / SRB;       // statistics sub-blocks per tile
   static_assert(RPT >= 1 && BM % G == 0, "fixup geometry");
+  static_assert(BM % SRB == 0 && SRB % G == 0, "fixup statistics geometry");
   __shared__ float4 red[G][CQ];
   const int nbn = (p.Cout + BN - 1) / BN, nbm = (p.P + BM - 1) / BM;
   const int nfull = nbm * nbn - p.ntail;
@@ -582,7 +586,6 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
   const float4 bias = (p.bias != nullptr && cok) ? *reinterpret_cast<const float4*>(p.bias + col)
                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 v[RPT];
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int r = g + i * G;
@@ -602,40 +605,360 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
       } else {
         *reinterpret_cast<float4*>(dst) = a;
       }
-      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
     }
   }
   if (p.stats == nullptr) return;
-  red[g][cq] = s;
-  __syncthreads();
-  const int cnt = min(BM, p.P - m0);
-  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int k = 0; k < G; ++k) {
-    const float4 q = red[k][cq];
-    t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
-  }
-  const float inv = 1.f / (float)cnt;
-  const float4 mean = make_float4(t.x * inv, t.y * inv, t.z * inv, t.w * inv);
-  __syncthreads();
-  float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    if (m0 + g + i * G < p.P) {
-      const float dx = v[i].x - mean.x, dy = v[i].y - mean.y, dz = v[i].z - mean.z, dw = v[i].w - mean.w;
-      m2.x += dx * dx; m2.y += dy * dy; m2.z += dz * dz; m2.w += dw * dw;
-    }
-  }
-  red[g][cq] = m2;
-  __syncthreads();
-  if (g == 0 && cok) {
-    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sb = 0; sb < NSB; ++sb) {
+    const int rb = m0 + sb * SRB;
+    const int cnt = min(SRB, p.P - rb);
+    if (cnt <= 0) break;              // uniform over the block
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = sb * IPS; i < (sb + 1) * IPS; ++i)
+      if (m0 + g + i * G < p.P) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
+    red[g][cq] = s;
+    __syncthreads();
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int k = 0; k < G; ++k) {
       const float4 q = red[k][cq];
-      u.x += q.x; u.y += q.y; u.z += q.z; u.w += q.w;
+      t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
     }
-    float2* st = p.stats + (size_t)mt * p.Cout + col;
-    st[0] = make_float2(mean.x, u.x); st[1] = make_float2(mean.y, u.y);
-    st[2] = make_float2(mean.z, u.z); st[3] = make_float2(mean.w, u.w);
+    const float inv = 1.f / (float)cnt;
+    const float4 mean = make_float4(t.x * inv, t.y * inv, t.z * inv, t.w * inv);
+    __syncthreads();
+    float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = sb * IPS; i < (sb + 1) * IPS; ++i) {
+      if (m0 + g + i * G < p.P) {
+        const float dx = v[i].x - mean.x, dy = v[i].y - mean.y, dz = v[i].z - mean.z, dw = v[i].w - mean.w;
+        m2.x += dx * dx; m2.y += dy * dy; m2.z += dz * dz; m2.w += dw * dw;
+      }
+    }
+    red[g][cq] = m2;
+    __syncthreads();
+    if (g == 0 && cok) {
+      float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < G; ++k) {
+        const float4 q = red[k][cq];
+        u.x += q.x; u.y += q.y; u.z += q.z; u.w += q.w;
+      }
+      float2* st = p.stats + (size_t)(rb / SRB) * p.Cout + col;
+      st[0] = make_float2(mean.x, u.x); st[1] = make_float2(mean.y, u.y);
+      st[2] = make_float2(mean.z, u.z); st[3] = make_float2(mean.w, u.w);
+    }
+    __syncthreads();
+  }
+}
+
+// --------------- forward x6: fp32 products from 3-way bf16 splits --------------------
+// gfx950 has no xf32 MFMA and its fp32 MFMA runs at 1/16 of the bf16 rate.  Every fp32
+// operand x is split exactly into x = hi + mid + lo (three RNE bf16 pieces: 24 significand
+// bits) and a*b is formed from the six partial products whose magnitude reaches 2^-16 of
+// the leading one:  ah*bh + ah*bm + am*bh + am*bm + ah*bl + al*bh  (dropped terms <= 2^-23
+// relative), each on v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- an fp32 GEMM to
+// within fp32 rounding (checked against fp64 in tests/test_gpu_kernels.py) at up to 16/6 x
+// the fp32-MFMA rate.  Weights are split once per step into three bf16 planes
+// (srpde_split_weights); activations arrive fp32 by LDS-DMA exactly as in v2 and are split
+// in registers right after their ds_read, so the A side needs no extra HBM or LDS bytes.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const float4 a, const float4 b, bf16x8& hi, bf16x8& mi, bf16x8& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    const float r = v[j] - (float)h;
+    const __bf16 m = (__bf16)r;
+    hi[j] = h;
+    mi[j] = m;
+    lo[j] = (__bf16)(r - (float)m);
+  }
+}
+
+// 32-bf16 (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ ((r >> 2) & 3)
+__device__ __forceinline__ int swzb(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+template <int BM, int BN, int WM, int WN, int SRB, int HP>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_x6_kernel(ConvParams p, const __bf16* __restrict__ wsp) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int AI = BM / (8 * NW);        // A DMA wave-instructions (8 rows x 128 B) per wave
+  constexpr int BTOT = 3 * BN / 16;        // B DMA instructions per stage (16 rows x 64 B)
+  constexpr int BPW = (BTOT + NW - 1) / NW;
+  constexpr int A_BYTES = BM * ROW2;
+  constexpr int BP_BYTES = BN * 64;        // one bf16 plane of the B tile
+  constexpr int STAGE = A_BYTES + 3 * BP_BYTES;
+  constexpr int NSB = BM / SRB, WPS = WM / NSB;
+  static_assert(AI >= 1 && BM % (8 * NW) == 0, "A DMA split");
+  static_assert(BM % SRB == 0 && WM % NSB == 0, "statistics sub-blocks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
+  } else {
+    const int q = blockIdx.x - nfull;
+    wg = nfull + q / p.tsplit;
+    piece = q - (q / p.tsplit) * p.tsplit;
+  }
+  const bool tail = wg >= nfull;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+  const int kc = p.ksize >> 1;
+
+  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
+  const size_t plane = (size_t)p.Cout * p.K;   // bf16 elements per weight plane
+  const int32x4 rsw = make_rsrc(wsp, (unsigned)(3 * plane * 2));
+
+  unsigned a_o0[AI], a_o1[AI], a_mask[AI];
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int q = (wave * AI + i) * 64 + lane;
+    const int r = q >> 3;
+    const int c4 = swz(r, q & 7) * 4;
+    const int m = m0 + r;
+    unsigned mask = 0;
+    int pix = 0;
+    if (m < p.P) {
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+      pix = m;
+      for (int t = 0; t < p.ksize * p.ksize; ++t) {
+        const int ky = t / p.ksize, kx = t - ky * p.ksize;
+        const int iy = yy + (ky - kc) * p.dil * p.sign, ix = xx + (kx - kc) * p.dil * p.sign;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
+      }
+      (void)n;
+    }
+    a_mask[i] = mask;
+    a_o0[i] = (unsigned)((pix * p.ldx0 + c4) * 4);
+    a_o1[i] = (unsigned)((pix * ld1 + c4) * 4);
+  }
+  // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzb^-1
+  int b_off[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int q = wave + j * NW;
+    const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzb(r, lane & 3);
+    const int nn = n0 + r;
+    b_off[j] = (q < BTOT && nn < p.Cout) ? (int)((pl * plane + (size_t)nn * p.K + c * 8) * 2) : -1;
+  }
+
+  const int nall = p.K / BK2;
+  const int s_beg = tail ? (piece * nall) / p.tsplit : 0;
+  const int s_end = tail ? ((piece + 1) * nall) / p.tsplit : nall;
+  const int taps = p.ksize * p.ksize;
+  int nx_tap = s_beg % taps, nx_ch = (s_beg / taps) * BK2;
+  int nx_ky = nx_tap / p.ksize, nx_kx = nx_tap - nx_ky * p.ksize;
+  auto issue = [&](int buf) {
+    const int tap = nx_tap, ch0 = nx_ch;
+    const int k0 = tap * p.Cin + ch0;
+    const int tsh = ((nx_ky - kc) * p.W + (nx_kx - kc)) * p.dil * p.sign;
+    const bool second = ch0 >= p.c0;
+    const int32x4 rs = second ? rs1 : rs0;
+    const int ld = second ? ld1 : p.ldx0;
+    const int cb = second ? ch0 - p.c0 : ch0;
+    const unsigned sadd = (unsigned)((tsh * ld + cb) * 4);
+    ++nx_tap;
+    if (++nx_kx == p.ksize) { nx_kx = 0; ++nx_ky; }
+    if (nx_tap == taps) {
+      nx_tap = 0; nx_ky = 0; nx_kx = 0;
+      nx_ch += BK2;
+    }
+    char* abase = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const unsigned base = second ? a_o1[i] : a_o0[i];
+      const unsigned off = ((a_mask[i] >> tap) & 1u) ? base + sadd : OOB;
+      dma16(rs, off, lds_addr_of(abase + (wave * AI + i) * 1024));
+    }
+    char* bbase = abase + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int q = wave + j * NW;
+      if (q < BTOT) {
+        const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+        dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+      }
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = s_beg; s < s_end; ++s) {
+    const int buf = (s - s_beg) & 1;
+    if (s + 1 < s_end) issue(buf ^ 1);
+    const char* a = lds + buf * STAGE;
+    const char* b = a + A_BYTES;
+    const bool fresh = ((s - s_beg) % HP) == 0;
+#pragma unroll
+    for (int g = 0; g < BK2 / 16; ++g) {
+      bf16x8 ah[TI], am[TI], al[TI], bh[TJ], bm[TJ], bl[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm0 + i * 32 + lr;
+        const int c = 4 * g + 2 * lh;
+        const float4 x0 = *reinterpret_cast<const float4*>(a + r * ROW2 + swz(r, c) * 16);
+        const float4 x1 = *reinterpret_cast<const float4*>(a + r * ROW2 + swz(r, c + 1) * 16);
+        split3(x0, x1, ah[i], am[i], al[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 32 + lr;
+        const int o = r * 64 + swzb(r, 2 * g + lh) * 16;
+        bh[j] = *reinterpret_cast<const bf16x8*>(b + o);
+        bm[j] = *reinterpret_cast<const bf16x8*>(b + BP_BYTES + o);
+        bl[j] = *reinterpret_cast<const bf16x8*>(b + 2 * BP_BYTES + o);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          floatx16 c0 = (g == 0 && fresh) ? floatx16{} : part[i][j];
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c0, 0, 0, 0);   // small terms first
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c0, 0, 0, 0);
+        }
+    }
+    if ((s - s_beg + 1) % HP == 0 || s + 1 == s_end) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (tail) {
+    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
+        }
+    return;
+  }
+
+  // ---------------- epilogue: bias, store, BN partial statistics per SRB rows --------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float v = acc[i][j][r] + bcol[j];
+        acc[i][j][r] = v;
+        if (row < p.P && col < p.Cout) {
+          float* dst = p.y + (size_t)row * p.ldy + col;
+          *dst = p.accumulate ? *dst + v : v;
+        }
+      }
+    }
+  if (p.stats == nullptr) return;
+  float* red = smem;                  // [WM][BN] per-wave-row column partials
+  const int sb = wmi / WPS;           // this wave's statistics sub-block
+  const int rb0 = m0 + sb * SRB;
+  const int cnt = min(SRB, p.P - rb0);
+  float mean[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        s += (row < p.P) ? acc[i][j][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + wn0 + j * 32 + lr];
+    mean[j] = cnt > 0 ? s / (float)cnt : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float d = acc[i][j][r] - mean[j];
+        s += (row < p.P) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+  if (wmi % WPS == 0 && lh == 0 && cnt > 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + cl];
+      if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
+    }
+  }
+}
+
+// fp32 -> three bf16 planes [3][n] (hi, mid, lo) for the x6 kernels' weight operand
+__global__ void split_weights_kernel(const float* __restrict__ w, __bf16* __restrict__ out, long long n) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const float v = w[e];
+    const __bf16 h = (__bf16)v;
+    const float r = v - (float)h;
+    const __bf16 m = (__bf16)r;
+    out[e] = h;
+    out[n + e] = m;
+    out[2 * n + e] = (__bf16)(r - (float)m);
   }
 }
 
@@ -1015,6 +1338,8 @@ static int launch_fwd(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
+static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes);
+
 template <int BM, int BN, int WM, int WN, int HP>
 static int launch_fwd_v2(ConvParams p, hipStream_t st, void* ws, size_t ws_bytes) {
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
@@ -1030,24 +1355,57 @@ static int launch_fwd_v2(ConvParams p, hipStream_t st, void* ws, size_t ws_bytes
   }();
   // tail split: when the last round of workgroups would be under half full, cut its tiles
   // into F K-pieces so that round runs on ~F x more CUs for 1/F of the time
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
-  const int nall = p.K / BK2;
-  const int rem = T % slots;
-  static const bool tail_on = [] {
-    const char* e = getenv("SRPDE_CONV_TAIL");  // tuning/diagnostics: 0 disables the split
-    return !e || atoi(e) != 0;
-  }();
-  if (tail_on && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
-    int F = std::min(std::min(slots / rem, nall / 2), 8);
-    while (F >= 2 && (size_t)rem * F * BM * BN * sizeof(float) > ws_bytes) --F;
-    if (F >= 2) { p.ntail = rem; p.tsplit = F; p.part = static_cast<float*>(ws); }
-  }
+  plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
   const int grid = T - p.ntail + p.ntail * p.tsplit;
   hipLaunchKernelGGL((conv_fwd_v2_kernel<BM, BN, WM, WN, HP>), dim3(grid), dim3(256), lds, st, p);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd(v2)");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN>), dim3(p.ntail), dim3(1024), 0, st, p);
     SRPDE_LAUNCH_CHECK("srpde_conv_fwd(tail fixup)");
+  }
+  return 0;
+}
+
+static bool tail_split_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRPDE_CONV_TAIL");  // tuning/diagnostics: 0 disables the split
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// tail split plan shared by the LDS-DMA forward kernels (see launch_fwd_v2)
+static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes) {
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  const int nall = p.K / BK2;
+  const int rem = T % slots;
+  if (tail_split_enabled() && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
+    int F = std::min(std::min(slots / rem, nall / 2), 8);
+    while (F >= 2 && (size_t)rem * F * BM * BN * sizeof(float) > ws_bytes) --F;
+    if (F >= 2) { p.ntail = rem; p.tsplit = F; p.part = static_cast<float*>(ws); }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int SRB>
+static int launch_fwd_x6(ConvParams p, const __bf16* wsp, hipStream_t st, void* ws, size_t ws_bytes) {
+  constexpr int NT = WM * WN * 64;
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const int T = nbm * nbn;
+  const size_t lds = (size_t)2 * (BM * ROW2 + 3 * BN * 64);
+  static int slots = [&] {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_x6_kernel<BM, BN, WM, WN, SRB, 2>, NT, lds);
+    return std::max(1, per_cu) * std::max(1, cus);
+  }();
+  plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, SRB, 2>), dim3(grid), dim3(NT), lds, st, p, wsp);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6");
+  if (p.ntail > 0) {
+    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
+    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6(tail fixup)");
   }
   return 0;
 }
@@ -1185,6 +1543,48 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
     case 0: return launch_fwd<128, 128, 2, 2>(p, stream);
     case 1: return launch_fwd<256, 64, 4, 1>(p, stream);
     default: return launch_fwd<256, 32, 4, 1>(p, stream);
+  }
+}
+
+int srpde_conv_x6_supported(int c0, int c1, int cout) {
+  return c0 % 32 == 0 && c1 % 32 == 0 && cout % 32 == 0 && c0 + c1 > 0 ? 1 : 0;
+}
+
+int srpde_split_weights(const float* w, void* planes, long long n, hipStream_t stream) {
+  SRPDE_CHECK_ARG(w && planes && n > 0, "srpde_split_weights: bad arguments");
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(split_weights_kernel, dim3(blocks), dim3(256), 0, stream, w, static_cast<__bf16*>(planes), n);
+  SRPDE_LAUNCH_CHECK("srpde_split_weights");
+  return 0;
+}
+
+int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const void* wsplit,
+                      const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
+                      int sign, int accumulate, float* stats, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x0 && wsplit && y, "srpde_conv_fwd_x6: null pointer");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_x6: bad shape");
+  SRPDE_CHECK_ARG(ksize == 1 || ksize == 3, "srpde_conv_fwd_x6: ksize must be 1 or 3");
+  SRPDE_CHECK_ARG(sign == 1 || sign == -1, "srpde_conv_fwd_x6: sign must be +-1");
+  SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout), "srpde_conv_fwd_x6: needs c0, c1, cout multiples of 32 "
+                  "(c0=%d c1=%d cout=%d)", c0, c1, cout);
+  SRPDE_CHECK_ARG(ldx0 % 4 == 0 && (c1 == 0 || ldx1 % 4 == 0), "srpde_conv_fwd_x6: strides must be multiples of 4");
+  SRPDE_CHECK_ARG(c1 == 0 || x1 != nullptr, "srpde_conv_fwd_x6: x1 null with c1>0");
+  SRPDE_CHECK_ARG(aligned16(x0) && aligned16(wsplit) && (c1 == 0 || aligned16(x1)),
+                  "srpde_conv_fwd_x6: inputs must be 16-byte aligned");
+  ConvParams p;
+  p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0;
+  p.x1 = x1; p.c1 = c1; p.ldx1 = ldx1 > 0 ? ldx1 : 4;
+  p.w = nullptr; p.bias = bias; p.y = y; p.ldy = ldy;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  SRPDE_CHECK_ARG(v2_ok(p) && 3LL * cout * p.K * 2 < (1LL << 31), "srpde_conv_fwd_x6: tensor too large");
+  const __bf16* wsp = static_cast<const __bf16*>(wsplit);
+  switch (fwd_config(cout)) {
+    case 0: return launch_fwd_x6<256, 128, 4, 2, 128>(p, wsp, stream, workspace, ws_bytes);
+    case 1: return launch_fwd_x6<256, 64, 4, 2, 256>(p, wsp, stream, workspace, ws_bytes);
+    default: return launch_fwd_x6<256, 32, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
   }
 }
 

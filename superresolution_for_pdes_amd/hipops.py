@@ -7,6 +7,8 @@ No function here computes anything on the host; all math runs in libsrpde_hip.so
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import call, query, stream_ptr
@@ -30,12 +32,42 @@ def empty(*shape, device):
 
 
 # ---------------------------------- convolution ------------------------------------
+_CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "x6")
+
+
+def set_conv_math(mode: str):
+    """'x6': fp32 convolutions as six bf16-split MFMA products (fp32-accurate, default);
+    'f32': the fp32 MFMA kernels.  Both are HIP; this only picks the kernel family."""
+    global _CONV_MATH
+    if mode not in ("x6", "f32"):
+        raise ValueError(mode)
+    _CONV_MATH = mode
+
+
+def conv_math() -> str:
+    return _CONV_MATH
+
+
+def split_weights(wpack):
+    """fp32 packed weights -> [3, numel] bf16 planes (hi, mid, lo) for the x6 kernels."""
+    planes = torch.empty(3, wpack.numel(), dtype=torch.bfloat16, device=wpack.device)
+    call("srpde_split_weights", wpack.data_ptr(), planes.data_ptr(), wpack.numel(), stream_ptr())
+    return planes
+
+
 def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
+    """Packed fp32 weights (fwd [Cout][tap][Cin], dgrad [Cin][tap][Cout]); in x6 mode each
+    packed tensor carries its bf16 split planes as ``.x6``."""
     cout, cin_real, kh, _ = w.shape
     taps = kh * kh
     wf = empty(cout * taps * cin_pad, device=w.device) if want_fwd else None
     wd = empty(cout * taps * cin_pad, device=w.device) if want_dgrad else None
     call("srpde_pack_conv_weights", w.data_ptr(), _p(wf), _p(wd), cout, cin_pad, cin_real, kh, stream_ptr())
+    if _CONV_MATH == "x6":
+        if wf is not None and query("srpde_conv_x6_supported", cin_pad, 0, cout):
+            wf.x6 = split_weights(wf)
+        if wd is not None and query("srpde_conv_x6_supported", cout, 0, cin_pad):
+            wd.x6 = split_weights(wd)
     return wf, wd
 
 
@@ -53,6 +85,13 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         p1, ld1, c1 = 0, 0, 0
     py, ldy = _pl(y)
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
+    if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
+        planes = getattr(wpack, "x6", None)
+        if planes is None:
+            planes = split_weights(wpack)
+        call("srpde_conv_fwd_x6", p0, x0.shape[1], ld0, p1, c1, ld1, planes.data_ptr(), _p(bias), py, ldy,
+             n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+        return
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
 

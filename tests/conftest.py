@@ -24,6 +24,15 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
+@pytest.fixture
+def conv_math():
+    """Restores the conv kernel family (x6 / f32) a test switched."""
+    from superresolution_for_pdes_amd import hipops as H
+    before = H.conv_math()
+    yield before
+    H.set_conv_math(before)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -33,8 +33,10 @@ def rel(a, b):
     (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1),
     # ragged: P % 32 != 0, Cout not a tile multiple, K = 864 not a tile multiple, dil 2 on 7x7
     (3, 64, 32, 96, 7, 2), (16, 128, 0, 128, 20, 1)])
-def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil):
+@pytest.mark.parametrize("math", ["x6", "f32"])
+def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
     from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math(math)
     g = torch.Generator().manual_seed(n * 1000 + cout + cin0)
     cin = cin0 + cin1
     x = torch.randn(n, cin, h, h, generator=g)
@@ -70,6 +72,36 @@ def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil):
     torch.cuda.synchronize()
     assert rel(unrows(dx, n, h, h), xg.grad) < 2e-6
     assert rel(dw, wg.grad) < 2e-6
+
+
+@pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(512, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 0, 32, 40, 1)])
+def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
+    """The bf16-split (x6) conv against fp64: its error must sit at the fp32 kernel's level
+    (both far below the 2^-16-relative error a 3-term bf16 split would show)."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(cin0 + cout)
+    n, cin = 4, cin0 + cin1
+    x = torch.randn(n, cin, h, h, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * (2.0 / (9 * cin)) ** 0.5
+    y64 = F.conv2d(x, wt, None, padding=dil, dilation=dil)
+    dy = torch.randn(n, cout, h, h, generator=g, dtype=torch.float64)
+    dx64 = torch.nn.grad.conv2d_input(x.shape, wt, dy, padding=dil, dilation=dil)
+    xr = rows(x.float()).to(DEV)
+    x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
+    dyr = rows(dy.float()).to(DEV)
+    errs = {}
+    for math in ("f32", "x6"):
+        H.set_conv_math(math)
+        wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
+        y = H.empty(n * h * h, cout, device=DEV)
+        H.conv_fwd(x0, x1, wf, None, y, n, h, h, cout, 3, dil, 1, False, None)
+        dx = H.empty(n * h * h, cin, device=DEV)
+        H.conv_fwd(dyr, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None)
+        torch.cuda.synchronize()
+        errs[math] = (rel(unrows(y, n, h, h), y64), rel(unrows(dx, n, h, h), dx64))
+    for k in range(2):
+        assert errs["x6"][k] < 1e-6, errs
+        assert errs["x6"][k] < 2.0 * errs["f32"][k] + 1e-7, errs
 
 
 def test_conv_cin_pad_and_accumulate():

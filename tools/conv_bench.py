@@ -38,7 +38,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
+    ap.add_argument("--math", default="x6", choices=("x6", "f32"))
     args = ap.parse_args()
+    H.set_conv_math(args.math)
     dev = "cuda"
     n = args.batch
     tot = {}
