@@ -340,7 +340,11 @@ def main():
         cin, cout, hw = next((c, o, h) for n, c, o, h in CONV3 if n == args.roofline_layer)
         flops_launch = conv_flops(cin, cout, hw) * B
         achieved = flops_launch / (kern_avg * 1e-3) / 1e12 if kern_avg > 0 else None
-        peak = 157.3
+        from superresolution_for_pdes_amd import hipops as H
+        x6 = H.conv_math() == "x6"
+        # dense MFMA peak of the instruction the kernel runs: fp32 MFMA 157.3 TF, or for the
+        # x6 kernels bf16 MFMA (16 x the fp32 rate = 2516.8 TF) / 6 partial products = 419.5 TF
+        peak = round(157.3 * 16 / 6, 1) if x6 else 157.3
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
@@ -359,12 +363,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (x6: fp32 products from 3-way bf16 splits on bf16 MFMA, fp32 accumulate)" if x6 else "f32",
             "data": "synthetic (x~N(0,1), theta channel=1, t~N(0,1)), resident in HBM",
             "config": {"workload": "UNet 20->40 train step, fp32, batch 1024/GPU, 40x40",
                        "global_batch": world * B, "per_gpu_batch": B, "hw": "40x40",
                        "parallelism": f"dp{world}", "final_loss": round(float(loss), 6)},
-            "roofline": {"bound": "mfma", "kernel": f"conv_igemm_fwd[{args.roofline_layer}]",
+            "roofline": {"bound": "mfma", "kernel": f"{'conv_fwd_x6' if x6 else 'conv_fwd_v2'}[{args.roofline_layer}]",
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(kern_avg, 4),

@@ -664,24 +664,42 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
 // in registers right after their ds_read, so the A side needs no extra HBM or LDS bytes.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// upper 16 bits of two floats packed as a bf16 pair (element 0 = lo_e, element 1 = hi_e)
+__device__ __forceinline__ unsigned pack_hi16(float lo_e, float hi_e) {
+  return __builtin_amdgcn_perm(__float_as_uint(hi_e), __float_as_uint(lo_e), 0x07060302u);
+}
+
+// Truncation split (exact): hi = top 8 significant bits, r = x - hi (exact), mid = top 8
+// bits of r, lo = r - mid (exact and itself a bf16).  x == hi + mid + lo bit-for-bit; two
+// AND/SUB pairs and three byte-permutes per element pair, no conversions.
 __device__ __forceinline__ void split3(const float4 a, const float4 b, bf16x8& hi, bf16x8& mi, bf16x8& lo) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  auto trunc2 = [](f2v x) {
+    return f2v{__uint_as_float(__float_as_uint(x.x) & 0xffff0000u), __uint_as_float(__float_as_uint(x.y) & 0xffff0000u)};
+  };
+  u32x4 H, M, L;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
-    const float r = v[j] - (float)h;
-    const __bf16 m = (__bf16)r;
-    hi[j] = h;
-    mi[j] = m;
-    lo[j] = (__bf16)(r - (float)m);
+  for (int k = 0; k < 4; ++k) {
+    const f2v x = {v[2 * k], v[2 * k + 1]};
+    const f2v r = x - trunc2(x);      // v_pk_add_f32
+    const f2v q = r - trunc2(r);
+    H[k] = pack_hi16(x.x, x.y);
+    M[k] = pack_hi16(r.x, r.y);
+    L[k] = pack_hi16(q.x, q.y);
   }
+  hi = __builtin_bit_cast(bf16x8, H);
+  mi = __builtin_bit_cast(bf16x8, M);
+  lo = __builtin_bit_cast(bf16x8, L);
 }
 
 // 32-bf16 (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ ((r >> 2) & 3)
 __device__ __forceinline__ int swzb(int r, int c) { return c ^ ((r >> 2) & 3); }
 
 template <int BM, int BN, int WM, int WN, int SRB, int HP>
-__global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_x6_kernel(ConvParams p, const __bf16* __restrict__ wsp) {
+__global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x6_kernel(ConvParams p, const __bf16* __restrict__ wsp) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int AI = BM / (8 * NW);        // A DMA wave-instructions (8 rows x 128 B) per wave
@@ -809,12 +827,13 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_x6_kernel(ConvParams
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int s = s_beg; s < s_end; ++s) {
+  // one stage; FRESH (compile time) starts the partial chain from a literal zero
+  auto stage = [&](int s, auto fresh_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
     const int buf = (s - s_beg) & 1;
     if (s + 1 < s_end) issue(buf ^ 1);
     const char* a = lds + buf * STAGE;
     const char* b = a + A_BYTES;
-    const bool fresh = ((s - s_beg) % HP) == 0;
 #pragma unroll
     for (int g = 0; g < BK2 / 16; ++g) {
       bf16x8 ah[TI], am[TI], al[TI], bh[TJ], bm[TJ], bl[TJ];
@@ -838,8 +857,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_x6_kernel(ConvParams
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          floatx16 c0 = (g == 0 && fresh) ? floatx16{} : part[i][j];
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c0, 0, 0, 0);   // small terms first
+          floatx16 c0;
+          if (FRESH && g == 0)
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], floatx16{}, 0, 0, 0);  // small terms first
+          else
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], part[i][j], 0, 0, 0);
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c0, 0, 0, 0);
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c0, 0, 0, 0);
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c0, 0, 0, 0);
@@ -847,14 +869,18 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_x6_kernel(ConvParams
           part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c0, 0, 0, 0);
         }
     }
-    if ((s - s_beg + 1) % HP == 0 || s + 1 == s_end) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+  for (int s = s_beg; s < s_end; s += HP) {
+    stage(s, std::true_type{});
+#pragma unroll
+    for (int h = 1; h < HP; ++h)
+      if (s + h < s_end) stage(s + h, std::false_type{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
   }
 
   if (tail) {
@@ -1581,9 +1607,19 @@ int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   SRPDE_CHECK_ARG(v2_ok(p) && 3LL * cout * p.K * 2 < (1LL << 31), "srpde_conv_fwd_x6: tensor too large");
   const __bf16* wsp = static_cast<const __bf16*>(wsplit);
+  // waves stacked along M (WN = 1) so each activation fragment is split by one wave only
+  static const int layout = [] {
+    const char* e = getenv("SRPDE_X6_LAYOUT");   // tuning/diagnostics: 1 = 2-D wave grid
+    return e ? atoi(e) : 0;
+  }();
   switch (fwd_config(cout)) {
-    case 0: return launch_fwd_x6<256, 128, 4, 2, 128>(p, wsp, stream, workspace, ws_bytes);
-    case 1: return launch_fwd_x6<256, 64, 4, 2, 256>(p, wsp, stream, workspace, ws_bytes);
+    case 0:
+      if (layout == 2) return launch_fwd_x6<128, 128, 4, 1, 128>(p, wsp, stream, workspace, ws_bytes);
+      return layout == 1 ? launch_fwd_x6<256, 128, 4, 2, 128>(p, wsp, stream, workspace, ws_bytes)
+                         : launch_fwd_x6<256, 128, 8, 1, 128>(p, wsp, stream, workspace, ws_bytes);
+    case 1:
+      return layout == 1 ? launch_fwd_x6<256, 64, 4, 2, 256>(p, wsp, stream, workspace, ws_bytes)
+                         : launch_fwd_x6<256, 64, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
     default: return launch_fwd_x6<256, 32, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
   }
 }

@@ -10,6 +10,6 @@ for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
          "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU" \
          "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${L}_${K} -o p$i -- python $R/tools/conv_bench.py --layers $L --only $K --iters 3 > $R/gpurun_out/pmc_${L}_${K}_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -k 10 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${L}_${K} -o p$i -- python $R/tools/conv_bench.py --layers $L --only $K --iters 3 ${3:+--math $3} > $R/gpurun_out/pmc_${L}_${K}_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 echo pmc done

@@ -1,0 +1,31 @@
+"""HBM bytes per launch of the roofline kernel from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/traffic_json.py gpurun_out/pmc_<tag> [layer] [out.json]
+FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of the bytes of wide
+streaming reads (MI355X_MICROARCH.md, HBM section) so it is doubled.  The launch is the
+conv kernel plus its tail-fixup kernel (both bracketed by bench.py's HIP events).
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+d = sys.argv[1]
+layer = sys.argv[2] if len(sys.argv) > 2 else "bridge.3"
+out = sys.argv[3] if len(sys.argv) > 3 else None
+vals = collections.defaultdict(list)
+for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        if "conv_fwd" in k or "conv_tail_fixup" in k:
+            kind = "fixup" if "fixup" in k else "main"
+            vals[(kind, r["Counter_Name"])].append(float(r["Counter_Value"]))
+mean = {k: sum(v) / len(v) for k, v in vals.items()}
+fetch = 2 * 1024 * (mean.get(("main", "FETCH_SIZE"), 0) + mean.get(("fixup", "FETCH_SIZE"), 0))
+write = 1024 * (mean.get(("main", "WRITE_SIZE"), 0) + mean.get(("fixup", "WRITE_SIZE"), 0))
+rec = {layer: round(fetch + write), f"{layer}_detail": {"read_bytes": round(fetch), "write_bytes": round(write),
+       "source": d, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->B, conv + tail fixup per launch"}}
+print(json.dumps(rec))
+if out:
+    json.dump(rec, open(out, "w"), indent=1)
