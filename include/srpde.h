@@ -67,6 +67,10 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                      int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
+int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                        int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
+                        int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
 
 /* ---- BatchNorm2d + ReLU -------------------------------------------------------------
  * replaces aten::native_batch_norm / native_batch_norm_backward and relu /

@@ -1310,6 +1310,224 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_v2_kernel(WgradParams p) {
   }
 }
 
+// ------------------- weight gradient x6: 3-way bf16 split, 6 MFMA products -------------------
+// dW tile [BM couts][BN k-columns] over a pixel chunk, 16 pixels per stage.  Both operands
+// are pixel-major in HBM and the MFMA wants 8 consecutive PIXELS per lane, so each stage is
+// register-staged (one pixel row x 8 columns per task), split into hi/mid/lo bf16 and
+// written as three [16 pixel][columns] bf16 images; the MFMA fragments come back through
+// ds_read_b64_tr_b16 (hardware transpose: a 16-lane group reads 4 pixel rows x 16 columns
+// and each lane receives its column's 4 pixels).  Chunk XOR swizzle s(row) keeps the four
+// rows of a transposed read on distinct banks.  One barrier per stage (double-buffered
+// images); partial MFMA chains of HP stages (two-level accumulation, as the forward).
+constexpr int BKX = 16;    // pixels per wgrad-x6 stage
+
+template <int RB>
+__device__ __forceinline__ int wx_off(int row, int ch) {   // byte offset of 16-B chunk ch of a row
+  constexpr int sh = RB >= 256 ? 0 : (RB == 128 ? 1 : -1);
+  const int s = sh < 0 ? 0 : (((row >> sh) & 3) << 2) & (RB / 16 - 1);
+  return row * RB + 16 * (ch ^ s);
+}
+
+template <int RB>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int col0, int lane) {
+  // 8 k-values (pixels 8h .. 8h+7) of column col0 + (lane & 31): two transposed 4-row reads
+  const int h = lane >> 5, q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = col0 + (lane & 16) + 4 * pp;   // this lane's 4-column address slot
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  const int o0 = wx_off<RB>(8 * h + q, col >> 3) + 2 * (col & 7);
+  const int o1 = wx_off<RB>(8 * h + 4 + q, col >> 3) + 2 * (col & 7);
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o0));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o1));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 c = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <int BM, int BN, int WM, int WN, int HP>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int RA = BM * 2, RBB = BN * 2;             // image row bytes (bf16)
+  constexpr int IMG_A = BKX * RA, IMG_B = BKX * RBB;    // one plane
+  constexpr int STAGE = 3 * (IMG_A + IMG_B);
+  constexpr int TA = (2 * BM + 255) / 256, TB = (2 * BN + 255) / 256;   // staging tasks per thread
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbm = (p.Cout + BM - 1) / BM, nbn = (p.K + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / nbn, nt = tile - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int HW = p.H * p.W, kc = p.ksize >> 1;
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+
+  // staging tasks: (pixel row, 8-column chunk); A = dY[pix][m0 + 8c ..], B = X[pix + off][k ..]
+  int a_row[TA], a_col[TA];
+  bool a_on[TA];
+#pragma unroll
+  for (int i = 0; i < TA; ++i) {
+    const int q = tid + 256 * i;
+    a_on[i] = q < 2 * BM;
+    a_row[i] = q / (BM / 8);
+    a_col[i] = (q % (BM / 8)) * 8;
+  }
+  int b_row[TB], b_col[TB], b_dy[TB], b_dx[TB], b_sh[TB], b_ch[TB];
+  bool b_on[TB], b_second[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) {
+    const int q = tid + 256 * i;
+    b_row[i] = q / (BN / 8);
+    b_col[i] = (q % (BN / 8)) * 8;
+    const int k = n0 + b_col[i];
+    b_on[i] = q < 2 * BN && k < p.K;
+    const int tap = b_on[i] ? k / p.Cin : 0;
+    const int ch = k - tap * p.Cin;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    b_dy[i] = (ky - kc) * p.dil;
+    b_dx[i] = (kx - kc) * p.dil;
+    b_sh[i] = b_dy[i] * p.W + b_dx[i];
+    b_second[i] = ch >= p.c0;
+    b_ch[i] = b_second[i] ? ch - p.c0 : ch;
+  }
+
+  float4 ra[TA][2], rb[TB][2];
+  auto load_stage = [&](int pbase) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+      const int pix = pbase + a_row[i], m = m0 + a_col[i];
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (a_on[i] && pix < pend && m < p.Cout) {
+        const float* src = p.dy + (size_t)pix * p.lddy + m;
+        v0 = *reinterpret_cast<const float4*>(src);
+        v1 = *reinterpret_cast<const float4*>(src + 4);   // Cout % 8 == 0
+      }
+      ra[i][0] = v0; ra[i][1] = v1;
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int pix = pbase + b_row[i];
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (b_on[i] && pix < pend) {
+        const int n = pix / HW, rem = pix - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+        const int iy = yy + b_dy[i], ix = xx + b_dx[i];
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) {
+          const float* src = b_second[i] ? p.x1 + (size_t)(pix + b_sh[i]) * ld1 + b_ch[i]
+                                         : p.x0 + (size_t)(pix + b_sh[i]) * p.ldx0 + b_ch[i];
+          v0 = *reinterpret_cast<const float4*>(src);
+          v1 = *reinterpret_cast<const float4*>(src + 4);
+        }
+      }
+      rb[i][0] = v0; rb[i][1] = v1;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* base = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+      if (!a_on[i]) continue;
+      bf16x8 h, m, l;
+      split3(ra[i][0], ra[i][1], h, m, l);
+      const int o = wx_off<RA>(a_row[i], a_col[i] >> 3);
+      *reinterpret_cast<bf16x8*>(base + o) = h;
+      *reinterpret_cast<bf16x8*>(base + IMG_A + o) = m;
+      *reinterpret_cast<bf16x8*>(base + 2 * IMG_A + o) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      if (tid + 256 * i >= 2 * BN) continue;
+      bf16x8 h, m, l;
+      split3(rb[i][0], rb[i][1], h, m, l);
+      const int o = 3 * IMG_A + wx_off<RBB>(b_row[i], b_col[i] >> 3);
+      *reinterpret_cast<bf16x8*>(base + o) = h;
+      *reinterpret_cast<bf16x8*>(base + IMG_B + o) = m;
+      *reinterpret_cast<bf16x8*>(base + 2 * IMG_B + o) = l;
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  const int nsteps = (pend - pbeg + BKX - 1) / BKX;
+
+  auto stage = [&](int s, auto fresh_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load_stage(pbeg + (s + 1) * BKX);
+    const char* img = lds + buf * STAGE;
+    bf16x8 ah[TI], am[TI], al[TI];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      ah[i] = tr_frag<RA>(img, wm0 + 32 * i, lane);
+      am[i] = tr_frag<RA>(img + IMG_A, wm0 + 32 * i, lane);
+      al[i] = tr_frag<RA>(img + 2 * IMG_A, wm0 + 32 * i, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const bf16x8 bh = tr_frag<RBB>(img + 3 * IMG_A, wn0 + 32 * j, lane);
+      const bf16x8 bm = tr_frag<RBB>(img + 3 * IMG_A + IMG_B, wn0 + 32 * j, lane);
+      const bf16x8 bl = tr_frag<RBB>(img + 3 * IMG_A + 2 * IMG_B, wn0 + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        floatx16 c0;
+        if (FRESH)
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, floatx16{}, 0, 0, 0);
+        else
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, part[i][j], 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh, c0, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm, c0, 0, 0, 0);
+        part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, c0, 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) store_stage(buf ^ 1);
+    __syncthreads();
+  };
+
+  if (nsteps > 0) {
+    load_stage(pbeg);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; s += HP) {
+    stage(s, std::true_type{});
+#pragma unroll
+    for (int h = 1; h < HP; ++h)
+      if (s + h < nsteps) stage(s + h, std::false_type{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+  }
+
+  // slab [split][Cout][K]
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = n0 + wn0 + 32 * j + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.Cout && n < p.K) out[(size_t)m * p.K + n] = acc[i][j][r];
+      }
+    }
+}
+
 // sum the split-K slabs in fixed order, write dW in torch layout [Cout][Cin_real][k][k]
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, int splits,
                                     int cout, int cin, int cin_real, int taps, int accumulate) {
@@ -1472,6 +1690,15 @@ static int launch_wgrad_v2(const WgradParams& p, hipStream_t st) {
   return 0;
 }
 
+template <int BM, int BN, int WM, int WN>
+static int launch_wgrad_x6(const WgradParams& p, hipStream_t st) {
+  const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
+  const size_t lds = (size_t)2 * 3 * BKX * 2 * (BM + BN);
+  hipLaunchKernelGGL((conv_wgrad_x6_kernel<BM, BN, WM, WN, 4>), dim3(nb), dim3(256), lds, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_x6");
+  return 0;
+}
+
 // Cout = 64 tile: 64x256 (1 workgroup/CU by LDS) or 64x128 (2/CU); SRPDE_WGRAD64 tuning
 static bool wgrad64_wide() {
   static const bool wide = [] {
@@ -1631,9 +1858,9 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
   return (size_t)splits * cout * K * sizeof(float);
 }
 
-int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
-                     int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
-                     int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                           int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout,
+                           int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream, bool x6) {
   SRPDE_CHECK_ARG(dy && x0 && dw && workspace, "srpde_conv_wgrad: null pointer");
   SRPDE_CHECK_ARG(c0 % 4 == 0 && c1 % 4 == 0 && lddy % 4 == 0 && ldx0 % 4 == 0 && cout % 4 == 0,
                   "srpde_conv_wgrad: channel counts / strides must be multiples of 4");
@@ -1653,7 +1880,13 @@ int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx
   p.part = static_cast<float*>(workspace);
   int bm, bn, rc;
   wgrad_tiles(cout, p.K, &bm, &bn);
-  if (wgrad_v2_ok(p)) {
+  if (x6) {
+    SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout) && wgrad_v2_ok(p),
+                    "srpde_conv_wgrad_x6: needs c0, c1, cout multiples of 32 (c0=%d c1=%d cout=%d)", c0, c1, cout);
+    if (bm == 128) rc = launch_wgrad_x6<128, 128, 2, 2>(p, stream);
+    else if (bm == 64) rc = launch_wgrad_x6<64, 256, 1, 4>(p, stream);
+    else rc = launch_wgrad_x6<32, 256, 1, 4>(p, stream);
+  } else if (wgrad_v2_ok(p)) {
     if (bm == 128) rc = launch_wgrad_v2<128, 128, 2, 2>(p, stream);
     else if (bm == 64) rc = wgrad64_wide() ? launch_wgrad_v2<64, 256, 1, 4>(p, stream)
                                            : launch_wgrad_v2<64, 128, 1, 4>(p, stream);
@@ -1671,6 +1904,20 @@ int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx
                      p.Cin, cin_real, taps, accumulate);
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce)");
   return 0;
+}
+
+int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                     int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
+                     int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
+                         workspace, ws_bytes, stream, false);
+}
+
+int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
+                        int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
+                        int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
+                         workspace, ws_bytes, stream, true);
 }
 
 int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout, int cin, int cin_real, int ksize,

@@ -122,7 +122,9 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cin_real = dw.shape[1]
     ws_bytes = int(query("srpde_conv_wgrad_workspace_size", n, h, w, cout, cin, ksize))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dy.device)
-    call("srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1, dw.data_ptr(), cin_real,
+    x6 = _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout)
+    call("srpde_conv_wgrad_x6" if x6 else "srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1,
+         dw.data_ptr(), cin_real,
          int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
 
 

@@ -86,6 +86,7 @@ def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
     y64 = F.conv2d(x, wt, None, padding=dil, dilation=dil)
     dy = torch.randn(n, cout, h, h, generator=g, dtype=torch.float64)
     dx64 = torch.nn.grad.conv2d_input(x.shape, wt, dy, padding=dil, dilation=dil)
+    dw64 = torch.nn.grad.conv2d_weight(x, wt.shape, dy, padding=dil, dilation=dil)
     xr = rows(x.float()).to(DEV)
     x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
     dyr = rows(dy.float()).to(DEV)
@@ -97,9 +98,11 @@ def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
         H.conv_fwd(x0, x1, wf, None, y, n, h, h, cout, 3, dil, 1, False, None)
         dx = H.empty(n * h * h, cin, device=DEV)
         H.conv_fwd(dyr, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None)
+        dw = torch.empty(cout, cin, 3, 3, device=DEV)
+        H.conv_wgrad(dyr, x0, x1, dw, n, h, h, 3, dil)
         torch.cuda.synchronize()
-        errs[math] = (rel(unrows(y, n, h, h), y64), rel(unrows(dx, n, h, h), dx64))
-    for k in range(2):
+        errs[math] = (rel(unrows(y, n, h, h), y64), rel(unrows(dx, n, h, h), dx64), rel(dw, dw64))
+    for k in range(3):
         assert errs["x6"][k] < 1e-6, errs
         assert errs["x6"][k] < 2.0 * errs["f32"][k] + 1e-7, errs
 
