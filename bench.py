@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--poisson-sizes", default="40:1024,80:1024,160:64,320:16,640:4",
                     help="n:B pairs for --workload poisson")
     ap.add_argument("--checkpoint", default=None, help="--workload cascade: model_state_dict checkpoint")
+    ap.add_argument("--ddp", action="store_true",
+                    help="use the process group + DataParallel path even at world size 1 (RCCL smoke check)")
     return ap.parse_args()
 
 
@@ -268,14 +270,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_pg = world > 1 or args.ddp
+    if use_pg:
+        # keep stdout to the one JSON line: RCCL's version banner is printed at the
+        # VERSION debug level, so default the level to WARN unless the caller chose one
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.workload != "train":
         (run_poisson if args.workload == "poisson" else run_cascade)(args, world, rank, dev)
-        if world > 1:
+        if use_pg:
             dist.destroy_process_group()
         return
 
@@ -290,7 +300,7 @@ def main():
     model = model.to(dev).train()
     model.flatten_parameters_()
     net = model
-    if world > 1:
+    if use_pg:
         from superresolution_for_pdes_amd.distributed import DataParallel
         net = DataParallel(model)
     opt = FusedAdamW(model.parameters(), lr=2e-4, weight_decay=1e-4, max_grad_norm=1.0)
@@ -367,7 +377,7 @@ def main():
             "data": "synthetic (x~N(0,1), theta channel=1, t~N(0,1)), resident in HBM",
             "config": {"workload": "UNet 20->40 train step, fp32, batch 1024/GPU, 40x40",
                        "global_batch": world * B, "per_gpu_batch": B, "hw": "40x40",
-                       "parallelism": f"dp{world}", "final_loss": round(float(loss), 6)},
+                       "parallelism": f"dp{world}", "final_loss": round(float(loss.detach()), 6)},
             "roofline": {"bound": "mfma", "kernel": f"{'conv_fwd_x6' if x6 else 'conv_fwd_v2'}[{args.roofline_layer}]",
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
@@ -377,7 +387,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

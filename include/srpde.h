@@ -67,6 +67,13 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                      int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* activations pre-split once into three bf16 planes [3][P][c] (truncation split, exact) ... */
+int srpde_split_planes(const float* x, int ldx, int c, long long P, void* planes, hipStream_t stream);
+/* ... and the x6 convolution reading them (no split inside the GEMM loop); x0p/x1p are
+ * srpde_split_planes outputs of the two input halves (c0 / c1 channels, compact) */
+int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const void* wsplit, const float* bias,
+                       float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
+                       float* stats, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
 int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                         int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,

@@ -32,6 +32,10 @@ struct ConvParams {
   // tail split (v2 only): the last `ntail` tiles are computed as `tsplit` K-pieces each,
   // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
   int ntail, tsplit;
+  int dbg;              // diagnostics (SRPDE_CONV_DBG): 1 = x6 kernel skips the per-stage DMA
+  // x6p: the inputs as pre-split bf16 planes [3][P][c0] / [3][P][c1] (srpde_split_planes)
+  const __bf16* x0p;
+  const __bf16* x1p;
   float* part;
 };
 
@@ -698,6 +702,108 @@ __device__ __forceinline__ void split3(const float4 a, const float4 b, bf16x8& h
 // 32-bf16 (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ ((r >> 2) & 3)
 __device__ __forceinline__ int swzb(int r, int c) { return c ^ ((r >> 2) & 3); }
 
+// epilogue shared by the x6 forward kernels: raw tail-piece tiles, or bias + store + BN
+// partial statistics per SRB rows
+template <int BM, int BN, int WM, int WN, int SRB>
+__device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32], bool tail,
+                                          int wg, int nfull, int piece, int m0, int n0, int wmi, int wni, int lane,
+                                          float* smem) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int NSB = BM / SRB, WPS = WM / NSB;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  if (tail) {
+    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
+        }
+    return;
+  }
+
+  // ---------------- epilogue: bias, store, BN partial statistics per SRB rows --------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float v = acc[i][j][r] + bcol[j];
+        acc[i][j][r] = v;
+        if (row < p.P && col < p.Cout) {
+          float* dst = p.y + (size_t)row * p.ldy + col;
+          *dst = p.accumulate ? *dst + v : v;
+        }
+      }
+    }
+  if (p.stats == nullptr) return;
+  float* red = smem;                  // [WM][BN] per-wave-row column partials
+  const int sb = wmi / WPS;           // this wave's statistics sub-block
+  const int rb0 = m0 + sb * SRB;
+  const int cnt = min(SRB, p.P - rb0);
+  float mean[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        s += (row < p.P) ? acc[i][j][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + wn0 + j * 32 + lr];
+    mean[j] = cnt > 0 ? s / (float)cnt : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float d = acc[i][j][r] - mean[j];
+        s += (row < p.P) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+  if (wmi % WPS == 0 && lh == 0 && cnt > 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + cl];
+      if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int SRB, int HP>
 __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x6_kernel(ConvParams p, const __bf16* __restrict__ wsp) {
   constexpr int NW = WM * WN;
@@ -831,7 +937,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x
   auto stage = [&](int s, auto fresh_tag) {
     constexpr bool FRESH = decltype(fresh_tag)::value;
     const int buf = (s - s_beg) & 1;
-    if (s + 1 < s_end) issue(buf ^ 1);
+    if (s + 1 < s_end && !(p.dbg & 1)) issue(buf ^ 1);
     const char* a = lds + buf * STAGE;
     const char* b = a + A_BYTES;
 #pragma unroll
@@ -869,6 +975,199 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x
           part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c0, 0, 0, 0);
         }
     }
+    if (!(p.dbg & 2)) {   // (dbg bit 2: diagnostics only, results wrong)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+  for (int s = s_beg; s < s_end; s += HP) {
+    stage(s, std::true_type{});
+#pragma unroll
+    for (int h = 1; h < HP; ++h)
+      if (s + h < s_end) stage(s + h, std::false_type{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+  }
+
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem);
+}
+
+// x6p: the same convolution with the activations arriving pre-split (three bf16 planes
+// [3][P][c], srpde_split_planes): both operands are DMA'd as bf16 and read as MFMA fragments
+// directly -- no VALU split in the loop.  A rows are 64 B per plane per stage (swzb swizzle,
+// source-side, like the weights).
+template <int BM, int BN, int WM, int WN, int SRB, int HP>
+__global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x6p_kernel(ConvParams p, const __bf16* __restrict__ wsp) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int ATOT = 3 * BM / 16, APW = (ATOT + NW - 1) / NW;   // A DMA instructions (16 rows x 64 B)
+  constexpr int BTOT = 3 * BN / 16, BPW = (BTOT + NW - 1) / NW;
+  constexpr int AP_BYTES = BM * 64, BP_BYTES = BN * 64;
+  constexpr int STAGE = 3 * (AP_BYTES + BP_BYTES);
+  constexpr int NSB = BM / SRB;
+  static_assert(BM % SRB == 0 && WM % NSB == 0, "statistics sub-blocks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
+  } else {
+    const int q = blockIdx.x - nfull;
+    wg = nfull + q / p.tsplit;
+    piece = q - (q / p.tsplit) * p.tsplit;
+  }
+  const bool tail = wg >= nfull;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+  const int kc = p.ksize >> 1;
+
+  const int32x4 rs0 = make_rsrc(p.x0p, (unsigned)((size_t)3 * p.P * p.c0 * 2));
+  const int c1s = p.c1 ? p.c1 : p.c0;
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1p : p.x0p, (unsigned)((size_t)3 * p.P * c1s * 2));
+  const size_t plane = (size_t)p.Cout * p.K;
+  const int32x4 rsw = make_rsrc(wsp, (unsigned)(3 * plane * 2));
+
+  // A instructions: q = plane * (BM/16) + 16-row block; lane -> (row, slot), fetches chunk swzb
+  unsigned a_o0[APW], a_o1[APW], a_mask[APW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    const int q = wave + i * NW;
+    const int pl = q / (BM / 16), rb = q - pl * (BM / 16);
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzb(r, lane & 3);
+    const int m = m0 + r;
+    unsigned mask = 0;
+    int pix = 0;
+    if (q < ATOT && m < p.P) {
+      const int rem = m % HW, yy = rem / p.W, xx = rem - yy * p.W;
+      pix = m;
+      for (int t = 0; t < p.ksize * p.ksize; ++t) {
+        const int ky = t / p.ksize, kx = t - ky * p.ksize;
+        const int iy = yy + (ky - kc) * p.dil * p.sign, ix = xx + (kx - kc) * p.dil * p.sign;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
+      }
+    }
+    a_mask[i] = mask;
+    a_o0[i] = (unsigned)(((size_t)pl * p.P * p.c0 + (size_t)pix * p.c0 + c * 8) * 2);
+    a_o1[i] = (unsigned)(((size_t)pl * p.P * c1s + (size_t)pix * c1s + c * 8) * 2);
+  }
+  int b_off[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int q = wave + j * NW;
+    const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzb(r, lane & 3);
+    const int nn = n0 + r;
+    b_off[j] = (q < BTOT && nn < p.Cout) ? (int)((pl * plane + (size_t)nn * p.K + c * 8) * 2) : -1;
+  }
+
+  const int nall = p.K / BK2;
+  const int s_beg = tail ? (piece * nall) / p.tsplit : 0;
+  const int s_end = tail ? ((piece + 1) * nall) / p.tsplit : nall;
+  const int taps = p.ksize * p.ksize;
+  int nx_tap = s_beg % taps, nx_ch = (s_beg / taps) * BK2;
+  int nx_ky = nx_tap / p.ksize, nx_kx = nx_tap - nx_ky * p.ksize;
+  auto issue = [&](int buf) {
+    const int tap = nx_tap, ch0 = nx_ch;
+    const int k0 = tap * p.Cin + ch0;
+    const int tsh = ((nx_ky - kc) * p.W + (nx_kx - kc)) * p.dil * p.sign;
+    const bool second = ch0 >= p.c0;
+    const int32x4 rs = second ? rs1 : rs0;
+    const int cs = second ? c1s : p.c0;
+    const int cb = second ? ch0 - p.c0 : ch0;
+    const unsigned sadd = (unsigned)((tsh * cs + cb) * 2);
+    ++nx_tap;
+    if (++nx_kx == p.ksize) { nx_kx = 0; ++nx_ky; }
+    if (nx_tap == taps) {
+      nx_tap = 0; nx_ky = 0; nx_kx = 0;
+      nx_ch += BK2;
+    }
+    char* abase = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) {
+      const int q = wave + i * NW;
+      if (q < ATOT) {
+        const unsigned base = second ? a_o1[i] : a_o0[i];
+        const unsigned off = ((a_mask[i] >> tap) & 1u) ? base + sadd : OOB;
+        dma16(rs, off, lds_addr_of(abase + q * 1024));
+      }
+    }
+    char* bbase = abase + 3 * AP_BYTES;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int q = wave + j * NW;
+      if (q < BTOT) {
+        const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+        dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+      }
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto stage = [&](int s, auto fresh_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    const int buf = (s - s_beg) & 1;
+    if (s + 1 < s_end) issue(buf ^ 1);
+    const char* a = lds + buf * STAGE;
+    const char* b = a + 3 * AP_BYTES;
+#pragma unroll
+    for (int g = 0; g < BK2 / 16; ++g) {
+      bf16x8 ah[TI], am[TI], al[TI], bh[TJ], bm[TJ], bl[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm0 + i * 32 + lr;
+        const int o = r * 64 + swzb(r, 2 * g + lh) * 16;
+        ah[i] = *reinterpret_cast<const bf16x8*>(a + o);
+        am[i] = *reinterpret_cast<const bf16x8*>(a + AP_BYTES + o);
+        al[i] = *reinterpret_cast<const bf16x8*>(a + 2 * AP_BYTES + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 32 + lr;
+        const int o = r * 64 + swzb(r, 2 * g + lh) * 16;
+        bh[j] = *reinterpret_cast<const bf16x8*>(b + o);
+        bm[j] = *reinterpret_cast<const bf16x8*>(b + BP_BYTES + o);
+        bl[j] = *reinterpret_cast<const bf16x8*>(b + 2 * BP_BYTES + o);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          floatx16 c0;
+          if (FRESH && g == 0)
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], floatx16{}, 0, 0, 0);
+          else
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], part[i][j], 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c0, 0, 0, 0);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
@@ -882,96 +1181,26 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
   }
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem);
+}
 
-  if (tail) {
-    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
-        }
-    return;
-  }
-
-  // ---------------- epilogue: bias, store, BN partial statistics per SRB rows --------
-  float bcol[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn0 + j * 32 + lr;
-    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + lr;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float v = acc[i][j][r] + bcol[j];
-        acc[i][j][r] = v;
-        if (row < p.P && col < p.Cout) {
-          float* dst = p.y + (size_t)row * p.ldy + col;
-          *dst = p.accumulate ? *dst + v : v;
-        }
-      }
-    }
-  if (p.stats == nullptr) return;
-  float* red = smem;                  // [WM][BN] per-wave-row column partials
-  const int sb = wmi / WPS;           // this wave's statistics sub-block
-  const int rb0 = m0 + sb * SRB;
-  const int cnt = min(SRB, p.P - rb0);
-  float mean[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        s += (row < p.P) ? acc[i][j][r] : 0.f;
-      }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + wn0 + j * 32 + lr];
-    mean[j] = cnt > 0 ? s / (float)cnt : 0.f;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float d = acc[i][j][r] - mean[j];
-        s += (row < p.P) ? d * d : 0.f;
-      }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
-  __syncthreads();
-  if (wmi % WPS == 0 && lh == 0 && cnt > 0) {
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + cl];
-      if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
-    }
+// [P][c] fp32 view -> three bf16 planes [3][P][c] (truncation split: hi, mid, lo exact)
+__global__ void split_planes_kernel(const float* __restrict__ x, int ldx, int c, long long P,
+                                    __bf16* __restrict__ out) {
+  const int cq = c / 8;
+  const long long total = P * cq;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long r = e / cq;
+    const int ch = (int)(e - r * cq) * 8;
+    const float* src = x + r * ldx + ch;
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 b = *reinterpret_cast<const float4*>(src + 4);
+    bf16x8 h, m, l;
+    split3(a, b, h, m, l);
+    const long long o = r * c + ch;
+    *reinterpret_cast<bf16x8*>(out + o) = h;
+    *reinterpret_cast<bf16x8*>(out + P * c + o) = m;
+    *reinterpret_cast<bf16x8*>(out + 2 * P * c + o) = l;
   }
 }
 
@@ -1397,8 +1626,29 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
     b_ch[i] = b_second[i] ? ch - p.c0 : ch;
   }
 
-  float4 ra[TA][2], rb[TB][2];
-  auto load_stage = [&](int pbase) {
+  // image coordinates of each B task's pixel, advanced by BKX pixels per stage (no divisions
+  // in the loop; BKX < 2 W for every layer here, W >= 10)
+  int b_y[TB], b_x[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) {
+    const int pix = pbeg + b_row[i];
+    const int rem = pix % HW;
+    b_y[i] = rem / p.W;
+    b_x[i] = rem - b_y[i] * p.W;
+  }
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      int x = b_x[i] + BKX, y = b_y[i];
+      while (x >= p.W) { x -= p.W; ++y; }
+      while (y >= p.H) y -= p.H;
+      b_x[i] = x; b_y[i] = y;
+    }
+  };
+  // two register sets: stage s+2 is loaded while stage s computes and stage s+1 is stored
+  float4 ra[2][TA][2], rb[2][TB][2];
+  auto load_stage = [&](int pbase, auto set_tag) {
+    constexpr int SET = decltype(set_tag)::value;
 #pragma unroll
     for (int i = 0; i < TA; ++i) {
       const int pix = pbase + a_row[i], m = m0 + a_col[i];
@@ -1408,15 +1658,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
         v0 = *reinterpret_cast<const float4*>(src);
         v1 = *reinterpret_cast<const float4*>(src + 4);   // Cout % 8 == 0
       }
-      ra[i][0] = v0; ra[i][1] = v1;
+      ra[SET][i][0] = v0; ra[SET][i][1] = v1;
     }
 #pragma unroll
     for (int i = 0; i < TB; ++i) {
       const int pix = pbase + b_row[i];
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
       if (b_on[i] && pix < pend) {
-        const int n = pix / HW, rem = pix - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
-        const int iy = yy + b_dy[i], ix = xx + b_dx[i];
+        const int iy = b_y[i] + b_dy[i], ix = b_x[i] + b_dx[i];
         if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) {
           const float* src = b_second[i] ? p.x1 + (size_t)(pix + b_sh[i]) * ld1 + b_ch[i]
                                          : p.x0 + (size_t)(pix + b_sh[i]) * p.ldx0 + b_ch[i];
@@ -1424,16 +1673,17 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
           v1 = *reinterpret_cast<const float4*>(src + 4);
         }
       }
-      rb[i][0] = v0; rb[i][1] = v1;
+      rb[SET][i][0] = v0; rb[SET][i][1] = v1;
     }
   };
-  auto store_stage = [&](int buf) {
-    char* base = lds + buf * STAGE;
+  auto store_stage = [&](auto set_tag) {   // set SET -> LDS buffer SET
+    constexpr int SET = decltype(set_tag)::value;
+    char* base = lds + SET * STAGE;
 #pragma unroll
     for (int i = 0; i < TA; ++i) {
       if (!a_on[i]) continue;
       bf16x8 h, m, l;
-      split3(ra[i][0], ra[i][1], h, m, l);
+      split3(ra[SET][i][0], ra[SET][i][1], h, m, l);
       const int o = wx_off<RA>(a_row[i], a_col[i] >> 3);
       *reinterpret_cast<bf16x8*>(base + o) = h;
       *reinterpret_cast<bf16x8*>(base + IMG_A + o) = m;
@@ -1443,7 +1693,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
     for (int i = 0; i < TB; ++i) {
       if (tid + 256 * i >= 2 * BN) continue;
       bf16x8 h, m, l;
-      split3(rb[i][0], rb[i][1], h, m, l);
+      split3(rb[SET][i][0], rb[SET][i][1], h, m, l);
       const int o = 3 * IMG_A + wx_off<RBB>(b_row[i], b_col[i] >> 3);
       *reinterpret_cast<bf16x8*>(base + o) = h;
       *reinterpret_cast<bf16x8*>(base + IMG_B + o) = m;
@@ -1462,11 +1712,15 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
   const int wm0 = wmi * TM, wn0 = wni * TN;
   const int nsteps = (pend - pbeg + BKX - 1) / BKX;
 
-  auto stage = [&](int s, auto fresh_tag) {
+  // stage s (parity PAR = s & 1 at compile time): LDS buffer PAR holds it
+  auto stage = [&](int s, auto fresh_tag, auto par_tag) {
     constexpr bool FRESH = decltype(fresh_tag)::value;
-    const int buf = s & 1;
-    if (s + 1 < nsteps) load_stage(pbeg + (s + 1) * BKX);
-    const char* img = lds + buf * STAGE;
+    constexpr int PAR = decltype(par_tag)::value;
+    if (s + 2 < nsteps) {
+      load_stage(pbeg + (s + 2) * BKX, par_tag);
+      advance();
+    }
+    const char* img = lds + PAR * STAGE;
     bf16x8 ah[TI], am[TI], al[TI];
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -1493,20 +1747,28 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
         part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, c0, 0, 0, 0);
       }
     }
-    if (s + 1 < nsteps) store_stage(buf ^ 1);
+    if (s + 1 < nsteps) store_stage(std::integral_constant<int, 1 - PAR>{});
     __syncthreads();
   };
 
+  typedef std::integral_constant<int, 0> P0;
+  typedef std::integral_constant<int, 1> P1;
   if (nsteps > 0) {
-    load_stage(pbeg);
-    store_stage(0);
+    load_stage(pbeg, P0{});
+    advance();
+    store_stage(P0{});
+  }
+  if (nsteps > 1) {
+    load_stage(pbeg + BKX, P1{});
+    advance();
   }
   __syncthreads();
+  static_assert(HP == 4, "stage parities are unrolled for HP = 4");
   for (int s = 0; s < nsteps; s += HP) {
-    stage(s, std::true_type{});
-#pragma unroll
-    for (int h = 1; h < HP; ++h)
-      if (s + h < nsteps) stage(s + h, std::false_type{});
+    stage(s, std::true_type{}, P0{});
+    if (s + 1 < nsteps) stage(s + 1, std::false_type{}, P1{});
+    if (s + 2 < nsteps) stage(s + 2, std::false_type{}, P0{});
+    if (s + 3 < nsteps) stage(s + 3, std::false_type{}, P1{});
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -1620,7 +1882,7 @@ static bool tail_split_enabled() {
 
 // tail split plan shared by the LDS-DMA forward kernels (see launch_fwd_v2)
 static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes) {
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
   const int nall = p.K / BK2;
   const int rem = T % slots;
   if (tail_split_enabled() && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
@@ -1641,15 +1903,43 @@ static int launch_fwd_x6(ConvParams p, const __bf16* wsp, hipStream_t st, void* 
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_x6_kernel<BM, BN, WM, WN, SRB, 2>, NT, lds);
+    if (getenv("SRPDE_CONV_VERBOSE"))
+      fprintf(stderr, "conv_fwd_x6<%d,%d,%d,%d>: %d workgroups/CU (LDS %zu B)\n", BM, BN, WM, WN, per_cu, lds);
     return std::max(1, per_cu) * std::max(1, cus);
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
+  p.dbg = dbg;
   const int grid = T - p.ntail + p.ntail * p.tsplit;
   hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, SRB, 2>), dim3(grid), dim3(NT), lds, st, p, wsp);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
     SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6(tail fixup)");
+  }
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN, int SRB>
+static int launch_fwd_x6p(ConvParams p, const __bf16* wsp, hipStream_t st, void* ws, size_t ws_bytes) {
+  constexpr int NT = WM * WN * 64;
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const int T = nbm * nbn;
+  const size_t lds = (size_t)2 * 3 * (BM + BN) * 64;
+  static int slots = [&] {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_x6p_kernel<BM, BN, WM, WN, SRB, 2>, NT, lds);
+    return std::max(1, per_cu) * std::max(1, cus);
+  }();
+  plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  hipLaunchKernelGGL((conv_fwd_x6p_kernel<BM, BN, WM, WN, SRB, 2>), dim3(grid), dim3(NT), lds, st, p, wsp);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6p");
+  if (p.ntail > 0) {
+    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
+    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_x6p(tail fixup)");
   }
   return 0;
 }
@@ -1778,7 +2068,7 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
   if (v2_ok(p)) {
     switch (fwd_config(cout)) {
       case 0:
@@ -1831,7 +2121,7 @@ int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
   SRPDE_CHECK_ARG(v2_ok(p) && 3LL * cout * p.K * 2 < (1LL << 31), "srpde_conv_fwd_x6: tensor too large");
   const __bf16* wsp = static_cast<const __bf16*>(wsplit);
   // waves stacked along M (WN = 1) so each activation fragment is split by one wave only
@@ -1848,6 +2138,49 @@ int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1
       return layout == 1 ? launch_fwd_x6<256, 64, 4, 2, 256>(p, wsp, stream, workspace, ws_bytes)
                          : launch_fwd_x6<256, 64, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
     default: return launch_fwd_x6<256, 32, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
+  }
+}
+
+int srpde_split_planes(const float* x, int ldx, int c, long long P, void* planes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && planes && P > 0 && c > 0, "srpde_split_planes: bad arguments");
+  SRPDE_CHECK_ARG(c % 8 == 0 && ldx % 4 == 0 && aligned16(x) && aligned16(planes),
+                  "srpde_split_planes: c %% 8, ldx %% 4 and 16-byte alignment required (c=%d ldx=%d)", c, ldx);
+  const long long total = P * (c / 8);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, stream, x, ldx, c, P,
+                     static_cast<__bf16*>(planes));
+  SRPDE_LAUNCH_CHECK("srpde_split_planes");
+  return 0;
+}
+
+int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const void* wsplit, const float* bias,
+                       float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
+                       float* stats, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x0p && wsplit && y, "srpde_conv_fwd_x6p: null pointer");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_x6p: bad shape");
+  SRPDE_CHECK_ARG(ksize == 1 || ksize == 3, "srpde_conv_fwd_x6p: ksize must be 1 or 3");
+  SRPDE_CHECK_ARG(sign == 1 || sign == -1, "srpde_conv_fwd_x6p: sign must be +-1");
+  SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout), "srpde_conv_fwd_x6p: needs c0, c1, cout multiples of 32 "
+                  "(c0=%d c1=%d cout=%d)", c0, c1, cout);
+  SRPDE_CHECK_ARG(c1 == 0 || x1p != nullptr, "srpde_conv_fwd_x6p: x1p null with c1>0");
+  SRPDE_CHECK_ARG(aligned16(x0p) && aligned16(wsplit) && (c1 == 0 || aligned16(x1p)),
+                  "srpde_conv_fwd_x6p: inputs must be 16-byte aligned");
+  ConvParams p;
+  p.x0 = nullptr; p.c0 = c0; p.ldx0 = c0;
+  p.x1 = nullptr; p.c1 = c1; p.ldx1 = c1 > 0 ? c1 : 4;
+  p.x0p = static_cast<const __bf16*>(x0p); p.x1p = static_cast<const __bf16*>(x1p);
+  p.w = nullptr; p.bias = bias; p.y = y; p.ldy = ldy;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  SRPDE_CHECK_ARG(3LL * p.P * std::max(c0, c1) * 2 < (1LL << 31) && 3LL * cout * p.K * 2 < (1LL << 31),
+                  "srpde_conv_fwd_x6p: tensor too large");
+  const __bf16* wsp = static_cast<const __bf16*>(wsplit);
+  switch (fwd_config(cout)) {
+    case 0: return launch_fwd_x6p<256, 128, 8, 1, 128>(p, wsp, stream, workspace, ws_bytes);
+    case 1: return launch_fwd_x6p<256, 64, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
+    default: return launch_fwd_x6p<256, 32, 8, 1, 256>(p, wsp, stream, workspace, ws_bytes);
   }
 }
 

@@ -109,6 +109,28 @@ def _scratch(nbytes, device):
     return buf
 
 
+def split_planes(x):
+    """[P, c] fp32 view -> [3, P, c] bf16 planes (hi, mid, lo; exact truncation split)."""
+    P, c = x.shape
+    px, ld = _pl(x)
+    planes = torch.empty(3, P, c, dtype=torch.bfloat16, device=x.device)
+    call("srpde_split_planes", px, ld, c, P, planes.data_ptr(), stream_ptr())
+    return planes
+
+
+def conv_fwd_x6p(x0p, x1p, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None):
+    """x6 convolution on pre-split inputs (split_planes of each input half)."""
+    c0 = x0p.shape[2]
+    c1 = x1p.shape[2] if x1p is not None else 0
+    py, ldy = _pl(y)
+    ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
+    planes = getattr(wpack, "x6", None)
+    if planes is None:
+        planes = split_weights(wpack)
+    call("srpde_conv_fwd_x6p", x0p.data_ptr(), c0, _p(x1p), c1, planes.data_ptr(), _p(bias), py, ldy,
+         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
 def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cout = dy.shape[1]
     pdy, lddy = _pl(dy)

@@ -107,6 +107,33 @@ def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
         assert errs["x6"][k] < 2.0 * errs["f32"][k] + 1e-7, errs
 
 
+@pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(256, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 32, 96, 7, 1)])
+def test_conv_x6p_equals_x6(cin0, cin1, cout, h, dil, conv_math):
+    """Pre-split planes (split_planes + conv_fwd_x6p) reproduce the in-register split
+    bit for bit: same split, same products, same accumulation order."""
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("x6")
+    g = torch.Generator().manual_seed(cin0 + 7 * cout)
+    n, cin = 3, cin0 + cin1
+    x = rows(torch.randn(n, cin, h, h, generator=g)).to(DEV)
+    x0, x1 = (x[:, :cin0], x[:, cin0:]) if cin1 else (x, None)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(DEV)
+    b = torch.randn(cout, generator=g).to(DEV)
+    wf, wd = H.pack_conv_weights(wt, cin, want_dgrad=True)
+    st1, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV)
+    st2 = torch.empty_like(st1)
+    y1, y2 = H.empty(n * h * h, cout, device=DEV), H.empty(n * h * h, cout, device=DEV)
+    H.conv_fwd(x0, x1, wf, b, y1, n, h, h, cout, 3, dil, 1, False, st1)
+    H.conv_fwd_x6p(H.split_planes(x0), H.split_planes(x1) if x1 is not None else None, wf, b, y2, n, h, h, cout, 3,
+                   dil, 1, False, st2)
+    dy = rows(torch.randn(n, cout, h, h, generator=g)).to(DEV)
+    d1, d2 = H.empty(n * h * h, cin, device=DEV), H.empty(n * h * h, cin, device=DEV)
+    H.conv_fwd(dy, None, wd, None, d1, n, h, h, cin, 3, dil, -1, False, None)
+    H.conv_fwd_x6p(H.split_planes(dy), None, wd, None, d2, n, h, h, cin, 3, dil, -1, False, None)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2) and torch.equal(st1, st2) and torch.equal(d1, d2)
+
+
 def test_conv_cin_pad_and_accumulate():
     """enc1.conv1: 3 real input channels padded to 4; accumulate flag adds into the output."""
     from superresolution_for_pdes_amd import hipops as H

