@@ -74,6 +74,19 @@ int srpde_split_planes(const float* x, int ldx, int c, long long P, void* planes
 int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const void* wsplit, const float* bias,
                        float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
                        float* stats, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* h3: the same convolution (forward / dgrad, same output and statistics layout) from
+ * two-piece fp16 splits with power-of-two operand scales: three partial products per fp32
+ * product on v_mfma_f32_32x32x16_f16, halo-staged activation tiles (conv_h3.hip).
+ * amax0/amax1: device words holding max|x0| / max|x1| as float bits (any upper bound within a
+ * few orders of magnitude works; srpde_absmax or the amax output of srpde_bn_relu_fwd/_bwd).
+ * wsplit/wexp: srpde_split_weights_h3 of the packed weights ([2][rows][K] fp16, [rows] int). */
+int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize);
+int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
+int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
+int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
+                      const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
+                      int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
+                      void* workspace, size_t ws_bytes, hipStream_t stream);
 /* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
 int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                         int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
@@ -88,13 +101,16 @@ int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long
                             float momentum, float eps, float* mean_out, float* invstd_out, hipStream_t stream);
 int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, int C, float eps, float* mean_out,
                           float* invstd_out, hipStream_t stream);
+/* amax (nullable): *amax = max(*amax, max|out|) as float bits -- the operand-scale word of the
+ * h3 convolutions; the caller zeroes it before the producing call */
 int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
-                      const float* beta, float* out, int ldo, long long P, int C, int relu, hipStream_t stream);
+                      const float* beta, float* out, int ldo, long long P, int C, int relu, unsigned* amax,
+                      hipStream_t stream);
 size_t srpde_bn_relu_bwd_workspace_size(long long P, int C);
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
-                      float* dbias, long long P, int C, int relu, void* workspace, size_t ws_bytes,
-                      hipStream_t stream);
+                      float* dbias, long long P, int C, int relu, unsigned* amax, void* workspace,
+                      size_t ws_bytes, hipStream_t stream);
 
 /* ---- input staging: NCHW model input -> NHWC (channel-padded) ----------------------- */
 int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w, int cpad, hipStream_t stream);

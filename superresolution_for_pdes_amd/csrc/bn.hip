@@ -74,15 +74,32 @@ __global__ void bn_eval_prepare_kernel(const float* rm, const float* rv, int C, 
 
 __global__ void increment_i64_kernel(long long* p) { *p += 1; }
 
+// *amax = max(*amax, block max of v) as float bits (v >= 0): the max|x| word the h3
+// convolutions (conv_h3.hip) derive their power-of-two operand scale from
+__device__ __forceinline__ void block_amax(float v, unsigned* amax) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  __shared__ float wmax[16];
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) wmax[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.f;
+    for (int k = 0; k < nw; ++k) m = fmaxf(m, wmax[k]);
+    atomicMax(amax, __float_as_uint(m));
+  }
+}
+
 // out = relu((y - mean) * invstd * gamma + beta)
 __global__ __launch_bounds__(256) void bn_relu_fwd_kernel(const float* __restrict__ y, int ldy,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ out,
-                                                          int ldo, long long P, int C, int relu) {
+                                                          int ldo, long long P, int C, int relu, unsigned* amax) {
   const int C4 = C >> 2;
   const long long total = P * C4;
+  float mx = 0.f;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
     const long long p = e / C4;
@@ -101,7 +118,9 @@ __global__ __launch_bounds__(256) void bn_relu_fwd_kernel(const float* __restric
       o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
     }
     *reinterpret_cast<float4*>(out + p * ldo + c) = o;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
   }
+  if (amax) block_amax(mx, amax);
 }
 
 // Generic per-channel column reduction layout used by the backward passes:
@@ -198,8 +217,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            const double* __restrict__ sdz,
                                                            const double* __restrict__ sdzx, long long P, int C,
                                                            int rows_per_blk, int relu, float* __restrict__ dy,
-                                                           int lddy, float2* __restrict__ bias_part) {
+                                                           int lddy, float2* __restrict__ bias_part, unsigned* amax) {
   extern __shared__ float4 red4[];
+  float mx = 0.f;
   int c4, r0, rs;
   thread_rc(C, &c4, &r0, &rs);
   const int active = (C >> 2) * rs;
@@ -232,8 +252,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       BN_APPLY(x) BN_APPLY(y) BN_APPLY(z) BN_APPLY(w)
 #undef BN_APPLY
       *reinterpret_cast<float4*>(dy + p * lddy + c) = o;
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
     }
   }
+  if (amax) block_amax(mx, amax);
   if (bias_part == nullptr) return;
   red4[threadIdx.x] = sb;
   __syncthreads();
@@ -290,13 +312,14 @@ int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, i
 }
 
 int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
-                      const float* beta, float* out, int ldo, long long P, int C, int relu, hipStream_t stream) {
+                      const float* beta, float* out, int ldo, long long P, int C, int relu, unsigned* amax,
+                      hipStream_t stream) {
   SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out, "srpde_bn_relu_fwd: null");
   SRPDE_CHECK_ARG(C % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0, "srpde_bn_relu_fwd: C/ld must be multiples of 4");
   const long long total = P * (C / 4);
   const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
-                     out, ldo, P, C, relu);
+                     out, ldo, P, C, relu, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_fwd");
   return 0;
 }
@@ -309,8 +332,8 @@ size_t srpde_bn_relu_bwd_workspace_size(long long P, int C) {
 
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
-                      float* dbias, long long P, int C, int relu, void* workspace, size_t ws_bytes,
-                      hipStream_t stream) {
+                      float* dbias, long long P, int C, int relu, unsigned* amax, void* workspace,
+                      size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && dy && workspace, "srpde_bn_relu_bwd: null");
   SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0 && lddy % 4 == 0,
                   "srpde_bn_relu_bwd: C/ld must be multiples of 4 (C<=1024)");
@@ -332,7 +355,7 @@ int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const 
   hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, part, nblk, C, dbeta, dgamma, sdz, sdzx);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(colsum)");
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd,
-                     gamma, beta, sdz, sdzx, P, C, rpb, relu, dy, lddy, dbias ? bpart : nullptr);
+                     gamma, beta, sdz, sdzx, P, C, rpb, relu, dy, lddy, dbias ? bpart : nullptr, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd(apply)");
   if (dbias) {
     hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, bpart, nblk, C, dbias, (float*)nullptr,

@@ -1,0 +1,297 @@
+// srpde-mi355x: pieces shared by the implicit-GEMM convolution kernels (conv.hip, conv_h3.hip):
+// the parameter block, LDS-DMA helpers, XCD-aware tile order, the K-split tail fixup and the
+// bias/store/BN-statistics epilogue of the 32x32 MFMA accumulator tiles.
+#pragma once
+#include <algorithm>
+#include <cstdlib>
+#include "common.h"
+
+namespace srpde {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct ConvParams {
+  const float* x0; int c0; int ldx0;
+  const float* x1; int c1; int ldx1;
+  const float* w;       // [Cout][taps][Cin] packed, Cin = c0 + c1
+  const float* bias;    // [Cout] or null
+  float* y; int ldy;    // output view
+  float2* stats;        // [mblocks][Cout] (mean, M2) or null
+  int N, H, W, Cout, ksize, dil, sign, accumulate;
+  int P, K, Cin;
+  // tail split (v2 only): the last `ntail` tiles are computed as `tsplit` K-pieces each,
+  // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
+  int ntail, tsplit;
+  int dbg;              // diagnostics (SRPDE_CONV_DBG): 1 = x6 kernel skips the per-stage DMA
+  // x6p: the inputs as pre-split bf16 planes [3][P][c0] / [3][P][c1] (srpde_split_planes)
+  const __bf16* x0p;
+  const __bf16* x1p;
+  float* part;
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  // bijective: blocks that share an A row-panel land on one XCD (MI355X L2 per XCD)
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+typedef int int32x4 __attribute__((ext_vector_type(4)));
+
+__device__ void llvm_raw_buffer_load_lds(int32x4 rsrc, __attribute__((address_space(3))) unsigned* lds, int size,
+                                         int voffset, int soffset, int offset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ int32x4 make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  int32x4 r;
+  r.x = (int)(unsigned)(a & 0xffffffffu);
+  r.y = (int)(unsigned)((a >> 32) & 0xffffu);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+
+constexpr int BK2 = 32;                 // k per stage (one tap, 32 channels)
+constexpr int ROW2 = BK2 * 4;           // 128-byte LDS rows
+constexpr unsigned OOB = 0x80000000u;   // beyond num_records -> zero fill
+
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds) as inline asm.  Issued through the
+// builtin, hipcc treats the DMA as an LDS store that may alias the following ds_reads and
+// emits s_waitcnt vmcnt(0) right after it, serialising the prefetch behind the compute;
+// as asm it is invisible to the waitcnt pass and we count vmcnt ourselves (vmcnt(0) before
+// the stage barrier).  M0 (the wave-uniform LDS destination) is saved/restored inside.
+__device__ __forceinline__ void dma16(int32x4 rsrc, unsigned voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr_of(const void* p) {
+  return (unsigned)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+
+// Finish the split tail tiles: fixed-order sum of the K-pieces, bias, store (or accumulate),
+// and the same per-row-block BN partials (mean, M2) the main epilogue writes.
+// SRB = rows per BN-statistics block (srpde_conv_stats_rows_per_block); a tile of BM rows
+// writes BM / SRB statistics rows.
+template <int BM, int BN, int SRB = BM>
+__global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
+  constexpr int CQ = BN / 4;          // column quads
+  constexpr int G = 1024 / CQ;        // row groups
+  constexpr int RPT = BM / G;         // rows per thread
+  constexpr int NSB = BM / SRB;       // statistics sub-blocks per tile
+  static_assert(RPT >= 1 && BM % G == 0, "fixup geometry");
+  static_assert(BM % SRB == 0 && SRB % G == 0, "fixup statistics geometry");
+  __shared__ float4 red[G][CQ];
+  const int nbn = (p.Cout + BN - 1) / BN, nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  const int wg = nfull + blockIdx.x;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int cq = threadIdx.x % CQ, g = threadIdx.x / CQ;
+  const int col = n0 + cq * 4;
+  const bool cok = col < p.Cout;  // Cout % 4 == 0
+  const float* src = p.part + (size_t)blockIdx.x * p.tsplit * (BM * BN);
+  const float4 bias = (p.bias != nullptr && cok) ? *reinterpret_cast<const float4*>(p.bias + col)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = g + i * G;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < p.tsplit; ++k) {
+      const float4 q = *reinterpret_cast<const float4*>(src + (size_t)k * (BM * BN) + r * BN + cq * 4);
+      a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+    }
+    a.x += bias.x; a.y += bias.y; a.z += bias.z; a.w += bias.w;
+    v[i] = a;
+    const int row = m0 + r;
+    if (row < p.P && cok) {
+      float* dst = p.y + (size_t)row * p.ldy + col;
+      if (p.accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(dst);
+        *reinterpret_cast<float4*>(dst) = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
+      } else {
+        *reinterpret_cast<float4*>(dst) = a;
+      }
+    }
+  }
+  if (p.stats == nullptr) return;
+  constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
+#pragma unroll
+  for (int sb = 0; sb < NSB; ++sb) {
+    const int rb = m0 + sb * SRB;
+    const int cnt = min(SRB, p.P - rb);
+    if (cnt <= 0) break;              // uniform over the block
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = sb * IPS; i < (sb + 1) * IPS; ++i)
+      if (m0 + g + i * G < p.P) { s.x += v[i].x; s.y += v[i].y; s.z += v[i].z; s.w += v[i].w; }
+    red[g][cq] = s;
+    __syncthreads();
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < G; ++k) {
+      const float4 q = red[k][cq];
+      t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+    }
+    const float inv = 1.f / (float)cnt;
+    const float4 mean = make_float4(t.x * inv, t.y * inv, t.z * inv, t.w * inv);
+    __syncthreads();
+    float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = sb * IPS; i < (sb + 1) * IPS; ++i) {
+      if (m0 + g + i * G < p.P) {
+        const float dx = v[i].x - mean.x, dy = v[i].y - mean.y, dz = v[i].z - mean.z, dw = v[i].w - mean.w;
+        m2.x += dx * dx; m2.y += dy * dy; m2.z += dz * dz; m2.w += dw * dw;
+      }
+    }
+    red[g][cq] = m2;
+    __syncthreads();
+    if (g == 0 && cok) {
+      float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < G; ++k) {
+        const float4 q = red[k][cq];
+        u.x += q.x; u.y += q.y; u.z += q.z; u.w += q.w;
+      }
+      float2* st = p.stats + (size_t)(rb / SRB) * p.Cout + col;
+      st[0] = make_float2(mean.x, u.x); st[1] = make_float2(mean.y, u.y);
+      st[2] = make_float2(mean.z, u.z); st[3] = make_float2(mean.w, u.w);
+    }
+    __syncthreads();
+  }
+}
+
+// epilogue shared by the x6 forward kernels: raw tail-piece tiles, or bias + store + BN
+// partial statistics per SRB rows
+template <int BM, int BN, int WM, int WN, int SRB>
+__device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32], bool tail,
+                                          int wg, int nfull, int piece, int m0, int n0, int wmi, int wni, int lane,
+                                          float* smem) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int NSB = BM / SRB, WPS = WM / NSB;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  if (tail) {
+    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
+        }
+    return;
+  }
+
+  // ---------------- epilogue: bias, store, BN partial statistics per SRB rows --------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float v = acc[i][j][r] + bcol[j];
+        acc[i][j][r] = v;
+        if (row < p.P && col < p.Cout) {
+          float* dst = p.y + (size_t)row * p.ldy + col;
+          *dst = p.accumulate ? *dst + v : v;
+        }
+      }
+    }
+  if (p.stats == nullptr) return;
+  float* red = smem;                  // [WM][BN] per-wave-row column partials
+  const int sb = wmi / WPS;           // this wave's statistics sub-block
+  const int rb0 = m0 + sb * SRB;
+  const int cnt = min(SRB, p.P - rb0);
+  float mean[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        s += (row < p.P) ? acc[i][j][r] : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + wn0 + j * 32 + lr];
+    mean[j] = cnt > 0 ? s / (float)cnt : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float d = acc[i][j][r] - mean[j];
+        s += (row < p.P) ? d * d : 0.f;
+      }
+    s += __shfl_xor(s, 32, 64);
+    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
+  }
+  __syncthreads();
+  if (wmi % WPS == 0 && lh == 0 && cnt > 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + cl];
+      if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
+    }
+  }
+}
+
+// ---------------- host: K-split of the last, under-filled round of tiles ----------------
+static bool tail_split_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRPDE_CONV_TAIL");  // tuning/diagnostics: 0 disables the split
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// tail split plan shared by the LDS-DMA forward kernels (see launch_fwd_v2)
+static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes) {
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  const int nall = p.K / BK2;
+  const int rem = T % slots;
+  if (tail_split_enabled() && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
+    int F = std::min(std::min(slots / rem, nall / 2), 8);
+    while (F >= 2 && (size_t)rem * F * BM * BN * sizeof(float) > ws_bytes) --F;
+    if (F >= 2) { p.ntail = rem; p.tsplit = F; p.part = static_cast<float*>(ws); }
+  }
+}
+
+}  // namespace srpde

@@ -1,0 +1,412 @@
+// "h3" convolution family for gfx950: fp32-accurate 3x3 convolution from two-piece fp16
+// splits on the fp16 MFMA (v_mfma_f32_32x32x16_f16), three partial products per fp32 product.
+//
+// Same contract as srpde_conv_fwd (conv.hip header comment; reference nn.Conv2d calls at
+// src/models.py:16,18,43,46,57,59): forward (sign +1) and dgrad (sign -1, dgrad-packed
+// weights), virtual concat of two NHWC inputs, fused bias + BatchNorm partial statistics.
+//
+// Arithmetic.  Every operand is scaled by a power of two so that the tensor's max|x| lands
+// just under 2^15, then split x*s = hi + lo with hi = fp16_rne(x*s) and lo = fp16_rne(x*s - hi):
+// 22 significant bits, representation error <= 2^-23 relative (fp32 itself keeps 24).  The
+// product a*b is  al*bh + ah*bl + ah*bh  (the dropped al*bl is <= 2^-22 relative and of random
+// sign); each partial product is exact in fp32 and accumulated in fp32 by the MFMA.  The
+// scales are exact powers of two and are undone in the epilogue.  Activation scales come from
+// a max|x| word the producing kernel wrote with atomicMax (bn_relu_fwd / bn_relu_bwd, or
+// srpde_absmax); weight scales are per packed row (srpde_split_weights_h3).  fp16 has 11
+// significant bits against bf16's 8, so two pieces and three products replace the x6
+// kernels' three pieces and six products: half the MFMA work at the same accuracy class.
+//
+// Data movement.  A 3x3 tap only shifts the pixel rows an output tile reads, so the A
+// operand of one 32-channel chunk is staged ONCE as a halo tile -- the tile's BM pixel rows
+// plus (W+1)*dil rows either side -- and the nine taps read it at nine row offsets (7x fewer
+// A bytes than per-tap staging).  Taps that fall outside the image (padding, row and image
+// wrap) read a zeroed LDS row instead.  The next chunk's halo tile is DMA'd in slices during
+// the current chunk's nine tap stages; the weight tile of each tap stage is double-buffered.
+// Both operands go HBM/L2 -> LDS with buffer_load ... lds (no VGPR staging).
+#include "conv_common.h"
+
+namespace srpde {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+// power-of-two scale exponent that brings max|x| (float bits) just under 2^15
+__device__ __forceinline__ int h3_exp(unsigned bits) {
+  const int e = (int)((bits >> 23) & 0xffu);
+  if (e == 0) return bits ? 100 : 0;            // zero / denormal maximum
+  if (e == 0xff) return 0;                      // inf / nan: propagate
+  return min(max(15 - (e - 126), -100), 100);   // max < 2^(e-126)
+}
+__device__ __forceinline__ float exp2i(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
+
+__device__ __forceinline__ void split2h(const float4 a, const float4 b, float s, half8& hi, half8& lo) {
+  const float v[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const _Float16 h = (_Float16)v[k];
+    hi[k] = h;
+    lo[k] = (_Float16)(v[k] - (float)h);
+  }
+}
+
+// 32-half (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ ((r >> 2) & 3)
+__device__ __forceinline__ int swzh(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+struct H3Args {
+  const _Float16* wsp;     // [2][Cout][K] hi / lo planes
+  const int* wexp;         // [Cout] weight scale exponents
+  const unsigned* amax0;   // max|x0| (float bits), or null
+  const unsigned* amax1;   // max|x1|, or null
+  int halo;                // (W + 1) * dil
+  int arows;               // BM + 2 * halo, rounded up to 8
+};
+
+template <int BM, int BN, int WM, int SRB, int HP>
+__global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
+  constexpr int NW = WM;
+  constexpr int TM = BM / WM, TI = TM / 32, TJ = BN / 32;
+  constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per stage (16 rows x 64 B)
+  constexpr int BPW = (BTOT + NW - 1) / NW;
+  constexpr int BP_BYTES = BN * 64;        // one fp16 plane of the B tile
+  constexpr int B_STAGE = 2 * BP_BYTES;
+  static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int a_bytes = h.arows * ROW2;
+  char* const abuf0 = lds;
+  char* const bbuf0 = lds + 2 * a_bytes;
+  char* const zrow = bbuf0 + 2 * B_STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
+  } else {
+    const int q = blockIdx.x - nfull;
+    wg = nfull + q / p.tsplit;
+    piece = q - (q / p.tsplit) * p.tsplit;
+  }
+  const bool tail = wg >= nfull;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+
+  if (tid < 32) reinterpret_cast<float*>(zrow)[tid] = 0.f;
+
+  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
+  const size_t plane = (size_t)p.Cout * p.K;   // fp16 elements per weight plane
+  const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+
+  // activation scale (shared by both inputs of a virtual concat)
+  unsigned ab = h.amax0 ? *h.amax0 : 0u;
+  if (p.c1 && h.amax1) ab = max(ab, *h.amax1);
+  const int ea = h3_exp(ab);
+  const float sa = exp2i(ea);
+
+  // per-lane tap masks of this wave's output rows
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wave * TM;
+  unsigned tmask[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int m = m0 + wm0 + i * 32 + lr;
+    unsigned mask = 0;
+    if (m < p.P) {
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+      (void)n;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
+      }
+    }
+    tmask[i] = mask;
+  }
+  // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1
+  int b_off[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int q = wave + j * NW;
+    const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzh(r, lane & 3);
+    const int nn = n0 + r;
+    b_off[j] = (q < BTOT && nn < p.Cout) ? (int)((pl * plane + (size_t)nn * p.K + c * 8) * 2) : -1;
+  }
+
+  const int nch = p.Cin / BK2;
+  const int c_beg = tail ? (piece * nch) / p.tsplit : 0;
+  const int c_end = tail ? ((piece + 1) * nch) / p.tsplit : nch;
+  const int na = h.arows / 8;                 // A DMA instructions per chunk (8 rows x 128 B)
+  const int pix0 = m0 - h.halo;
+
+  // A slice `q` of chunk `ch` (8 halo rows) into buffer `buf`
+  auto issue_a = [&](int ch, int q, int buf) {
+    const int ch0 = ch * BK2;
+    const bool second = ch0 >= p.c0;
+    const int32x4 rs = second ? rs1 : rs0;
+    const int ld = second ? ld1 : p.ldx0;
+    const int cb = second ? ch0 - p.c0 : ch0;
+    const int r = q * 8 + (lane >> 3);
+    const int pix = pix0 + r;
+    const unsigned off = (pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
+    dma16(rs, off, lds_addr_of(abuf0 + buf * a_bytes + q * 1024));
+  };
+  auto issue_b = [&](int ch, int tap, int buf) {
+    const int k0 = tap * p.Cin + ch * BK2;
+    char* bbase = bbuf0 + buf * B_STAGE;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int q = wave + j * NW;
+      if (q < BTOT) {
+        const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+        dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+      }
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f, part[i][j][r] = 0.f;
+
+  // prologue: whole halo tile of the first chunk + first weight stage
+  for (int q = wave; q < na; q += NW) issue_a(c_beg, q, c_beg & 1);
+  issue_b(c_beg, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  int sidx = 0;      // stage counter (B buffer parity)
+  int hp = 0;        // stages in the current partial chain
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    const char* a = abuf0 + (ch & 1) * a_bytes;
+    for (int tap = 0; tap < 9; ++tap, ++sidx) {
+      // prefetch: next weight stage, one slice of the next chunk's halo tile
+      if (tap < 8) issue_b(ch, tap + 1, (sidx + 1) & 1);
+      else if (ch + 1 < c_end) issue_b(ch + 1, 0, (sidx + 1) & 1);
+      if (ch + 1 < c_end) {
+        const int q = wave + tap * NW;
+        if (q < na) issue_a(ch + 1, q, (ch + 1) & 1);
+        if (tap == 8)
+          for (int q2 = wave + 9 * NW; q2 < na; q2 += NW) issue_a(ch + 1, q2, (ch + 1) & 1);
+      }
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int toff = p.sign > 0 ? (ky * p.W + kx) * p.dil : ((2 - ky) * p.W + (2 - kx)) * p.dil;
+      const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+#pragma unroll
+      for (int g = 0; g < BK2 / 16; ++g) {
+        half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int r = wm0 + i * 32 + lr + toff;
+          const int c = 4 * g + 2 * lh;
+          const bool ok = (tmask[i] >> tap) & 1u;
+          const char* a0 = ok ? a + r * ROW2 + swz(r, c) * 16 : zrow;
+          const char* a1 = ok ? a + r * ROW2 + swz(r, c + 1) * 16 : zrow;
+          const float4 x0 = *reinterpret_cast<const float4*>(a0);
+          const float4 x1 = *reinterpret_cast<const float4*>(a1);
+          split2h(x0, x1, sa, ah[i], al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int r = j * 32 + lr;
+          const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
+          bh[j] = *reinterpret_cast<const half8*>(b + o);
+          bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            floatx16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], part[i][j], 0, 0, 0);  // small first
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
+            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
+          }
+      }
+      if (++hp == HP) {   // two-level accumulation: fold the partial chain
+        hp = 0;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[i][j] += part[i][j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) part[i][j][r] = 0.f;
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact), then fold the last partial chain
+  const float ia = exp2i(-ea);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + j * 32 + lr;
+    const float iw = col < p.Cout ? exp2i(-h.wexp[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = ((acc[i][j][r] + part[i][j][r]) * ia) * iw;
+  }
+  x6_finish<BM, BN, WM, 1, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wave, 0, lane, smem);
+}
+
+// fp32 packed weights [rows][K] -> fp16 hi / lo planes [2][rows][K] with a power-of-two scale
+// per row (one wave per row)
+__global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
+                                                               int* __restrict__ wexp, int rows, int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* src = w + (size_t)row * K;
+  float m = 0.f;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(src[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int e = h3_exp(__float_as_uint(m));
+  const float s = exp2i(e);
+  _Float16* hi = out + (size_t)row * K;
+  _Float16* lo = out + (size_t)rows * K + (size_t)row * K;
+  for (int k = lane; k < K; k += 64) {
+    const float v = src[k] * s;
+    const _Float16 hv = (_Float16)v;
+    hi[k] = hv;
+    lo[k] = (_Float16)(v - (float)hv);
+  }
+  if (lane == 0) wexp[row] = e;
+}
+
+// *amax = max(*amax, max|x|) over a [P][c] view (float bits; caller zeroes *amax)
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int ldx, int c, long long P,
+                                                     unsigned* amax) {
+  const int c4 = c >> 2;
+  const long long total = P * c4;
+  float m = 0.f;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long r = e / c4;
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ldx + (e - r * c4) * 4);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+
+// ---------------------------------- host side ---------------------------------------
+static int h3_cfg(int cout) { return cout % 128 == 0 ? 0 : (cout % 64 == 0 ? 1 : 2); }
+constexpr int H3_BM = 256;
+
+static int h3_arows(int w, int dil) { return (H3_BM + 2 * (w + 1) * dil + 7) / 8 * 8; }
+
+static size_t h3_lds(int bn, int arows) { return (size_t)2 * arows * ROW2 + (size_t)2 * 2 * bn * 64 + 128; }
+
+template <int BM, int BN, int WM, int SRB>
+static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
+  constexpr int NT = WM * 64;
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const int T = nbm * nbn;
+  const size_t lds = h3_lds(BN, h.arows);
+  static int slots = [&] {
+    int dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, cus);      // one workgroup per CU (LDS)
+  }();
+  plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  const int nch = p.Cin / BK2;
+  if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
+  if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, SRB, 2>), dim3(grid), dim3(NT), lds, st, p, h);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
+  if (p.ntail > 0) {
+    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
+    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
+  }
+  return 0;
+}
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
+  if (!(ksize == 3 && c0 % 32 == 0 && c1 % 32 == 0 && cout % 32 == 0 && c0 + c1 > 0 && w > 0 && dil >= 1)) return 0;
+  const int bn = h3_cfg(cout) == 0 ? 128 : (h3_cfg(cout) == 1 ? 64 : 32);
+  const int arows = h3_arows(w, dil);
+  return (arows / 8 <= 9 * 8 && h3_lds(bn, arows) <= 160 * 1024) ? 1 : 0;
+}
+
+int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream) {
+  SRPDE_CHECK_ARG(w && planes && wexp && rows > 0 && K > 0, "srpde_split_weights_h3: bad arguments");
+  hipLaunchKernelGGL(split_weights_h3_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, stream, w,
+                     static_cast<_Float16*>(planes), wexp, rows, K);
+  SRPDE_LAUNCH_CHECK("srpde_split_weights_h3");
+  return 0;
+}
+
+int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && amax && c % 4 == 0 && ldx % 4 == 0 && aligned16(x), "srpde_absmax: bad arguments");
+  if (P <= 0) return 0;
+  const long long total = P * (c / 4);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(absmax_kernel, dim3(blocks), dim3(256), 0, stream, x, ldx, c, P, amax);
+  SRPDE_LAUNCH_CHECK("srpde_absmax");
+  return 0;
+}
+
+int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
+                      const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
+                      int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
+                      void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
+  SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
+  SRPDE_CHECK_ARG(sign == 1 || sign == -1, "srpde_conv_fwd_h3: sign must be +-1");
+  SRPDE_CHECK_ARG(srpde_conv_h3_supported(c0, c1, cout, w, dil, ksize),
+                  "srpde_conv_fwd_h3: unsupported shape (c0=%d c1=%d cout=%d w=%d dil=%d ksize=%d)", c0, c1, cout, w,
+                  dil, ksize);
+  SRPDE_CHECK_ARG(ldx0 % 4 == 0 && (c1 == 0 || ldx1 % 4 == 0), "srpde_conv_fwd_h3: strides must be multiples of 4");
+  SRPDE_CHECK_ARG(aligned16(x0) && aligned16(wsplit) && (c1 == 0 || aligned16(x1)),
+                  "srpde_conv_fwd_h3: inputs must be 16-byte aligned");
+  ConvParams p;
+  p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0;
+  p.x1 = x1; p.c1 = c1; p.ldx1 = ldx1 > 0 ? ldx1 : 4;
+  p.x0p = nullptr; p.x1p = nullptr;
+  p.w = nullptr; p.bias = bias; p.y = y; p.ldy = ldy;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  const long long maxld = std::max(ldx0, c1 ? ldx1 : 0);
+  SRPDE_CHECK_ARG((long long)p.P * maxld * 4 < (1LL << 31) && 2LL * cout * p.K * 2 < (1LL << 31),
+                  "srpde_conv_fwd_h3: tensor too large");
+  H3Args a;
+  a.wsp = static_cast<const _Float16*>(wsplit);
+  a.wexp = wexp;
+  a.amax0 = amax0;
+  a.amax1 = c1 ? amax1 : nullptr;
+  a.halo = (w + 1) * dil;
+  a.arows = h3_arows(w, dil);
+  switch (h3_cfg(cout)) {
+    case 0: return launch_fwd_h3<256, 128, 8, 128>(p, a, stream, workspace, ws_bytes);
+    case 1: return launch_fwd_h3<256, 64, 8, 256>(p, a, stream, workspace, ws_bytes);
+    default: return launch_fwd_h3<256, 32, 8, 256>(p, a, stream, workspace, ws_bytes);
+  }
+}
+
+}  // extern "C"

@@ -36,10 +36,11 @@ _CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "x6")
 
 
 def set_conv_math(mode: str):
-    """'x6': fp32 convolutions as six bf16-split MFMA products (fp32-accurate, default);
-    'f32': the fp32 MFMA kernels.  Both are HIP; this only picks the kernel family."""
+    """Pick the conv kernel family (all HIP, all fp32-accurate):
+    'h3': three fp16-split MFMA products with power-of-two operand scales, halo-staged tiles;
+    'x6': six bf16-split MFMA products; 'f32': the fp32 MFMA kernels."""
     global _CONV_MATH
-    if mode not in ("x6", "f32"):
+    if mode not in ("h3", "x6", "f32"):
         raise ValueError(mode)
     _CONV_MATH = mode
 
@@ -55,14 +56,30 @@ def split_weights(wpack):
     return planes
 
 
+def split_weights_h3(wpack, rows):
+    """fp32 packed weights [rows][K] -> ([2, rows*K] fp16 hi/lo planes, [rows] int32 scale
+    exponents) for the h3 kernels."""
+    K = wpack.numel() // rows
+    planes = torch.empty(2, wpack.numel(), dtype=torch.float16, device=wpack.device)
+    wexp = torch.empty(rows, dtype=torch.int32, device=wpack.device)
+    call("srpde_split_weights_h3", wpack.data_ptr(), planes.data_ptr(), wexp.data_ptr(), rows, K, stream_ptr())
+    return planes, wexp
+
+
 def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
     """Packed fp32 weights (fwd [Cout][tap][Cin], dgrad [Cin][tap][Cout]); in x6 mode each
-    packed tensor carries its bf16 split planes as ``.x6``."""
+    packed tensor carries its bf16 split planes as ``.x6``, in h3 mode its fp16 planes and
+    row scales as ``.h3``."""
     cout, cin_real, kh, _ = w.shape
     taps = kh * kh
     wf = empty(cout * taps * cin_pad, device=w.device) if want_fwd else None
     wd = empty(cout * taps * cin_pad, device=w.device) if want_dgrad else None
     call("srpde_pack_conv_weights", w.data_ptr(), _p(wf), _p(wd), cout, cin_pad, cin_real, kh, stream_ptr())
+    if _CONV_MATH == "h3" and kh == 3:
+        if wf is not None and cin_pad % 32 == 0 and cout % 32 == 0:
+            wf.h3 = split_weights_h3(wf, cout)
+        if wd is not None and cin_pad % 32 == 0 and cout % 32 == 0:
+            wd.h3 = split_weights_h3(wd, cin_pad)
     if _CONV_MATH == "x6":
         if wf is not None and query("srpde_conv_x6_supported", cin_pad, 0, cout):
             wf.x6 = split_weights(wf)
@@ -85,6 +102,14 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         p1, ld1, c1 = 0, 0, 0
     py, ldy = _pl(y)
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
+    if _CONV_MATH == "h3" and query("srpde_conv_h3_supported", x0.shape[1], c1, cout, w, dil, ksize):
+        planes, wexp = getattr(wpack, "h3", None) or split_weights_h3(wpack, cout)
+        a0 = amax_of(x0)
+        a1 = amax_of(x1) if x1 is not None else None
+        call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
+             wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
+             ws.data_ptr(), ws.numel(), stream_ptr())
+        return
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
         planes = getattr(wpack, "x6", None)
         if planes is None:
@@ -94,6 +119,41 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         return
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+# ---------------------- operand-scale words of the h3 convolutions ----------------------
+# A tensor that feeds an h3 convolution carries ``._srpde_amax``: a 1-element int32 device
+# tensor holding max|x| as float bits (an upper bound suffices).  Producers fill it on the
+# fly (bn_relu_fwd / bn_relu_bwd); ops whose output is bounded by their input (max-pool,
+# bilinear upsample, attention gating) pass the input's word on (tag_amax).
+class AmaxSlots:
+    """A zeroed block of max|x| words, handed out one per produced activation."""
+
+    def __init__(self, n, device):
+        self.buf = torch.zeros(n, dtype=torch.int32, device=device)
+        self.next = 0
+
+    def take(self):
+        if self.next >= self.buf.numel():
+            raise RuntimeError("AmaxSlots exhausted")
+        self.next += 1
+        return self.buf[self.next - 1:self.next]
+
+
+def tag_amax(t, slot):
+    if slot is not None:
+        t._srpde_amax = slot
+    return t
+
+
+def amax_of(x):
+    """The max|x| word of ``x``: its tag, else computed now (one HIP reduction)."""
+    a = getattr(x, "_srpde_amax", None)
+    if a is None:
+        a = torch.zeros(1, dtype=torch.int32, device=x.device)
+        px, ld = _pl(x)
+        call("srpde_absmax", px, ld, x.shape[1], x.shape[0], a.data_ptr(), stream_ptr())
+    return a
 
 
 _SCRATCH = {}
@@ -169,14 +229,15 @@ def bn_eval_prepare(running_mean, running_var, eps):
     return mean, invstd
 
 
-def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True):
+def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True, amax=None):
     py, ldy = _pl(y)
     po, ldo = _pl(out)
     call("srpde_bn_relu_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-         po, ldo, y.shape[0], y.shape[1], int(relu), stream_ptr())
+         po, ldo, y.shape[0], y.shape[1], int(relu), _p(amax), stream_ptr())
+    tag_amax(out, amax)
 
 
-def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True):
+def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True, amax=None):
     P, C = y.shape
     py, ldy = _pl(y)
     pda, ldda = _pl(da)
@@ -184,8 +245,9 @@ def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu
     ws_bytes = int(query("srpde_bn_relu_bwd_workspace_size", P, C))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
     call("srpde_bn_relu_bwd", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
-         beta.data_ptr(), pdy, lddy, _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), ws.data_ptr(), ws_bytes,
-         stream_ptr())
+         beta.data_ptr(), pdy, lddy, _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), _p(amax), ws.data_ptr(),
+         ws_bytes, stream_ptr())
+    tag_amax(dy, amax)
 
 
 # ------------------------------ pool / upsample / misc -----------------------------
@@ -201,7 +263,7 @@ def maxpool_fwd(x, n, h, w):
     out = empty(n * (h // 2) * (w // 2), c, device=x.device)
     px, ldx = _pl(x)
     call("srpde_maxpool2x2_fwd", px, ldx, out.data_ptr(), c, n, h, w, c, stream_ptr())
-    return out
+    return tag_amax(out, getattr(x, "_srpde_amax", None))
 
 
 def maxpool_bwd(x, dout, dx, n, h, w, accumulate):
@@ -218,7 +280,7 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     px, ldx = _pl(x)
     po, ldo = _pl(out)
     call("srpde_upsample_bilinear_fwd", px, ldx, po, ldo, n, h, w, ho, wo, c, stream_ptr())
-    return out
+    return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
 
 
 def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate):
@@ -244,6 +306,7 @@ def att_fwd(x, g, n, hw, w1, b1, w2, b2, wg, bg, out=None):
     call("srpde_att_fwd", px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
          b2.data_ptr(), wg.data_ptr(), bg.data_ptr(), m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(),
          po, ldo, stream_ptr())
+    tag_amax(out, getattr(x, "_srpde_amax", None))   # x * sigmoid * sigmoid: |out| <= |x|
     return out, (m, hb, ca, sa)
 
 

@@ -64,7 +64,7 @@ class ConvBlock(nn.Module):
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
             return _ConvBlockFn.apply(x, self, *params)
         n, _, h, w = x.shape
-        a, _ = X._block_fwd(self, _to_rows(x), None, n, h, w, self.training)
+        a, _ = X._block_fwd(self, _to_rows(x), None, n, h, w, self.training, H.AmaxSlots(2, x.device))
         return _from_rows(a, n, self.conv2.out_channels, h, w)
 
 
@@ -73,7 +73,7 @@ class _ConvBlockFn(torch.autograd.Function):
     def forward(ctx, x, blk, *params):
         n, c, h, w = x.shape
         xr = _to_rows(x)
-        a, saved = X._block_fwd(blk, xr, None, n, h, w, blk.training)
+        a, saved = X._block_fwd(blk, xr, None, n, h, w, blk.training, H.AmaxSlots(2, x.device))
         ctx.blk, ctx.saved, ctx.shape, ctx.cin, ctx.cpad = blk, saved, (n, h, w), c, xr.shape[1]
         return _from_rows(a, n, blk.conv2.out_channels, h, w)
 
@@ -88,7 +88,7 @@ class _ConvBlockFn(torch.autograd.Function):
                   blk.conv2.weight, blk.conv2.bias, blk.bn2.weight, blk.bn2.bias]
         grads = {p: torch.empty_like(p) for p in params}
         dx = H.empty(n * h * w, ctx.cpad, device=dout.device) if ctx.needs_input_grad[0] else None
-        X._block_bwd(blk, ctx.saved, da, n, h, w, grads, dx)
+        X._block_bwd(blk, ctx.saved, da, n, h, w, grads, H.AmaxSlots(2, dout.device), dx)
         gx = _from_rows(dx, n, ctx.cin, h, w) if dx is not None else None
         return (gx, None, *[grads[p] for p in params])
 

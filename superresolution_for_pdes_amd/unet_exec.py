@@ -70,7 +70,7 @@ def _conv_launch(conv, *args):
     sink.append((a, b))
 
 
-def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, cin_pad=None):
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots):
     """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48)."""
     dev = x0.device
     cout = conv.out_channels
@@ -88,15 +88,16 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, cin_pad=None):
         H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
         mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
     a = H.empty(P, cout, device=dev)
-    H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a)
+    H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
     return a, (x0, x1, y, mean, invstd)
 
 
-def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, dx=None, dx_accumulate=False):
+def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False):
     x0, x1, y, mean, invstd = saved
     P, cout = y.shape
     dy = H.empty(P, cout, device=y.device)
-    H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias])
+    H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
+                  amax=slots.take())
     H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
     if dx is not None:
         cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
@@ -104,18 +105,18 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, dx=None, dx_accumulate=Fa
         H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None)
 
 
-def _block_fwd(blk, x0, x1, n, h, w, training):
-    a1, s1 = _cbr_fwd(blk.conv1, blk.bn1, x0, x1, n, h, w, training, 1)
-    a2, s2 = _cbr_fwd(blk.conv2, blk.bn2, a1, None, n, h, w, training, 1)
+def _block_fwd(blk, x0, x1, n, h, w, training, slots):
+    a1, s1 = _cbr_fwd(blk.conv1, blk.bn1, x0, x1, n, h, w, training, 1, slots)
+    a2, s2 = _cbr_fwd(blk.conv2, blk.bn2, a1, None, n, h, w, training, 1, slots)
     return a2, (s1, s2)
 
 
-def _block_bwd(blk, saved, da, n, h, w, grads, dx, dx_accumulate=False):
+def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False):
     s1, s2 = saved
     P = n * h * w
     da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
-    _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, da1)
-    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, dx, dx_accumulate)
+    _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1)
+    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate)
 
 
 def _att_params(att):
@@ -156,27 +157,28 @@ def unet_forward(m, x, training, save=False):
     S.x = x
     x4 = H.nchw_to_nhwc(x, 4)
     S.x4 = x4
+    slots = H.AmaxSlots(16, x.device)   # max|x| words of the 16 BN+ReLU outputs (h3 operand scales)
     # encoder
-    e1, S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training)
+    e1, S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots)
     p1 = H.maxpool_fwd(e1, n, h, w)
-    e2, S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training)
+    e2, S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots)
     p2 = H.maxpool_fwd(e2, n, h2, w2)
-    e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training)
+    e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots)
     # bridge (dilated)
-    ab1, S.br1 = _cbr_fwd(m.bridge[0], m.bridge[1], e3, None, n, h3, w3, training, 2)
-    b, S.br2 = _cbr_fwd(m.bridge[3], m.bridge[4], ab1, None, n, h3, w3, training, 2)
+    ab1, S.br1 = _cbr_fwd(m.bridge[0], m.bridge[1], e3, None, n, h3, w3, training, 2, slots)
+    b, S.br2 = _cbr_fwd(m.bridge[3], m.bridge[4], ab1, None, n, h3, w3, training, 2, slots)
     # decoder with attention, virtual concat
     e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3)
-    d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training)
+    d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
     u3 = H.upsample_fwd(d3, n, h3, w3, h2, w2)
     e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2)
-    d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training)
+    d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
     u2 = H.upsample_fwd(d2, n, h2, w2, h, w)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1)
-    d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training)
+    d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots)
     # multi-scale head + residual
-    o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1)
-    o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1)
+    o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots)
+    o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots)
     out = H.head_fwd(o2, m.final.weight, m.final.bias, x, n, hw1)
     if not save:
         return out.view(n, 1, h, w), None
@@ -193,20 +195,21 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     dev = dout.device
     P1, P2, P3 = n * hw1, n * hw2, n * hw3
     ready = grad_ready or (lambda g: None)
+    slots = H.AmaxSlots(16, dev)   # max|dy| words of the 16 BN backward outputs
     dout = dout.contiguous().view(-1)
     # head
     do2 = H.empty(P1, 16, device=dev)
     H.head_bwd(dout, S.o2, m.final.weight, n, hw1, do2, grads[m.final.weight], grads[m.final.bias])
     ready("final")
     do1 = H.empty(P1, m.out_conv1.out_channels, device=dev)
-    _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, do1)
+    _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1)
     ready("out_bn2"); ready("out_conv2")
     dd1 = H.empty(P1, 64, device=dev)
-    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, dd1)
+    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1)
     ready("out_bn1"); ready("out_conv1")
     # dec1: grad of cat[u2 (128), e1a (64)]
     dcat1 = H.empty(P1, 192, device=dev)
-    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, dcat1)
+    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1)
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
     _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, dcat1[:, :128], True)
@@ -215,7 +218,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False)
     # dec2: grad of cat[u3 (256), e2a (128)]
     dcat2 = H.empty(P2, 384, device=dev)
-    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, dcat2)
+    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2)
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
     _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, dcat2[:, :256], True)
@@ -224,26 +227,26 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False)
     # dec3: grad of cat[b (512), e3a (256)]
     dcat3 = H.empty(P3, 768, device=dev)
-    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, dcat3)
+    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3)
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)
     _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True)
     ready("att3")
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
-    _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, dab1)
-    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, de3, True)
+    _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1)
+    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True)
     ready("bridge")
     # encoder
     dp2 = H.empty(P3, 128, device=dev)
-    _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, dp2)
+    _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, slots, dp2)
     ready("enc3")
     H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
     dp1 = H.empty(P2, 64, device=dev)
-    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, dp1)
+    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1)
     ready("enc2")
     H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
-    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, None)
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, None)
     ready("enc1")
 
 

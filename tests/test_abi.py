@@ -59,7 +59,7 @@ def test_argument_errors_are_reported(lib):
     assert rc < 0
     assert "null" in lib.last_error()
     with pytest.raises(RuntimeError, match="srpde_bn_relu_fwd"):
-        lib.call("srpde_bn_relu_fwd", 0, 4, 0, 0, 0, 0, 0, 4, 16, 4, 1, 0)
+        lib.call("srpde_bn_relu_fwd", 0, 4, 0, 0, 0, 0, 0, 4, 16, 4, 1, 0, 0)
 
 
 def test_product_path_never_imports_oracle():

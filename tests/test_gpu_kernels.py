@@ -33,7 +33,7 @@ def rel(a, b):
     (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1),
     # ragged: P % 32 != 0, Cout not a tile multiple, K = 864 not a tile multiple, dil 2 on 7x7
     (3, 64, 32, 96, 7, 2), (16, 128, 0, 128, 20, 1)])
-@pytest.mark.parametrize("math", ["x6", "f32"])
+@pytest.mark.parametrize("math", ["h3", "x6", "f32"])
 def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
     from superresolution_for_pdes_amd import hipops as H
     H.set_conv_math(math)
@@ -75,9 +75,11 @@ def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
 
 
 @pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(512, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 0, 32, 40, 1)])
-def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
-    """The bf16-split (x6) conv against fp64: its error must sit at the fp32 kernel's level
-    (both far below the 2^-16-relative error a 3-term bf16 split would show)."""
+def test_conv_split_kernels_are_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
+    """The split-operand convs against fp64: the bf16 three-piece (x6) and the scaled fp16
+    two-piece (h3) kernels must sit at the fp32 kernel's error level (all far below the
+    2^-16-relative error of a 2-piece bf16 split).  Bars: < 1e-6 relative L2, and x6 within
+    2x / h3 within 3x of the fp32-MFMA kernel's own error (+1e-7)."""
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator().manual_seed(cin0 + cout)
     n, cin = 4, cin0 + cin1
@@ -91,7 +93,7 @@ def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
     x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
     dyr = rows(dy.float()).to(DEV)
     errs = {}
-    for math in ("f32", "x6"):
+    for math in ("f32", "x6", "h3"):
         H.set_conv_math(math)
         wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
         y = H.empty(n * h * h, cout, device=DEV)
@@ -102,9 +104,12 @@ def test_conv_x6_is_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
         H.conv_wgrad(dyr, x0, x1, dw, n, h, h, 3, dil)
         torch.cuda.synchronize()
         errs[math] = (rel(unrows(y, n, h, h), y64), rel(unrows(dx, n, h, h), dx64), rel(dw, dw64))
+    print(f"conv fp64 errors (fwd, dgrad, wgrad): {errs}")
     for k in range(3):
         assert errs["x6"][k] < 1e-6, errs
         assert errs["x6"][k] < 2.0 * errs["f32"][k] + 1e-7, errs
+        assert errs["h3"][k] < 1e-6, errs
+        assert errs["h3"][k] < 3.0 * errs["f32"][k] + 1e-7, errs
 
 
 @pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(256, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 32, 96, 7, 1)])
@@ -313,3 +318,49 @@ def test_clip_adamw_matches_torch():
         torch.cuda.synchronize()
         assert abs(float(coef[1]) - float(tot)) < 1e-5 * float(tot)
         assert rel(flat_p, torch.cat([r.detach() for r in ref])) < 1e-7
+
+
+@pytest.mark.parametrize("scale", [1e-12, 1.0, 3e4])
+def test_conv_h3_scale_invariance(scale, conv_math):
+    """The h3 operand scales are powers of two picked from max|x|: scaling the input by any
+    factor (tiny gradients, large activations) scales the output by the same factor with the
+    same relative accuracy, and a loose max|x| upper bound (tag 1000x too big) changes nothing
+    beyond rounding."""
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("h3")
+    g = torch.Generator().manual_seed(11)
+    n, cin, cout, h = 3, 128, 128, 20
+    x = torch.randn(n, cin, h, h, generator=g, dtype=torch.float64) * scale
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.03
+    y64 = F.conv2d(x, wt, None, padding=1)
+    xr = rows(x.float()).to(DEV)
+    wf, _ = H.pack_conv_weights(wt.float().to(DEV), cin)
+    y = H.empty(n * h * h, cout, device=DEV)
+    H.conv_fwd(xr, None, wf, None, y, n, h, h, cout, 3, 1, 1, False, None)
+    e_exact = rel(unrows(y, n, h, h), y64)
+    loose = torch.tensor([int(np.float32(float(xr.abs().max()) * 1000).view(np.int32))], dtype=torch.int32, device=DEV)
+    xr._srpde_amax = loose
+    y2 = H.empty(n * h * h, cout, device=DEV)
+    H.conv_fwd(xr, None, wf, None, y2, n, h, h, cout, 3, 1, 1, False, None)
+    torch.cuda.synchronize()
+    assert e_exact < 1e-6 and rel(unrows(y2, n, h, h), y64) < 1e-6, (e_exact, scale)
+
+
+def test_amax_words_match_outputs():
+    """bn_relu_fwd / bn_relu_bwd write max|out| (float bits) into the word they are given."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(5)
+    P, C = 5000, 64
+    y = rows(torch.randn(1, C, 50, 100, generator=g)).to(DEV)
+    mean, invstd = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    gam, bet = torch.rand(C, generator=g).to(DEV) + 0.5, torch.randn(C, generator=g).to(DEV)
+    slots = H.AmaxSlots(2, DEV)
+    out = H.empty(P, C, device=DEV)
+    H.bn_relu_fwd(y, mean, invstd, gam, bet, out, amax=slots.take())
+    dy = H.empty(P, C, device=DEV)
+    da = rows(torch.randn(1, C, 50, 100, generator=g)).to(DEV)
+    H.bn_relu_bwd(y, da, mean, invstd, gam, bet, dy, None, None, None, amax=slots.take())
+    torch.cuda.synchronize()
+    got = slots.buf.cpu().numpy().view(np.float32)
+    assert got[0] == float(out.abs().max()) and got[1] == float(dy.abs().max())
+    assert out._srpde_amax.data_ptr() == slots.buf.data_ptr()

@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--math", default="x6", choices=("x6", "f32", "x6p"))
+    ap.add_argument("--math", default="x6", choices=("h3", "x6", "f32", "x6p"))
     args = ap.parse_args()
     H.set_conv_math("x6" if args.math == "x6p" else args.math)
     dev = "cuda"
@@ -58,6 +58,9 @@ def main():
         y = torch.empty(P, cout, device=dev)
         stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, dev)
         dy = torch.randn(P, cout, device=dev)
+        for t in (x0, x1, dy):   # h3: max|x| words computed once, as the producers would
+            if t is not None:
+                t._srpde_amax = H.amax_of(t)
         dx = torch.empty(P, cin, device=dev)
         dw = torch.empty_like(w)
         line = f"{name:11s}"
