@@ -87,6 +87,12 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
                       void* workspace, size_t ws_bytes, hipStream_t stream);
+/* weight gradient with the h3 arithmetic (same workspace as srpde_conv_wgrad; c0, c1, cout % 32 == 0);
+ * amax_dy / amax0 / amax1: the max|.| words of dy, x0, x1 as for srpde_conv_fwd_h3 */
+int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,
+                        const unsigned* amax0, const float* x1, int c1, int ldx1, const unsigned* amax1, float* dw,
+                        int cin_real, int accumulate, int n, int h, int w, int cout, int ksize, int dil,
+                        void* workspace, size_t ws_bytes, hipStream_t stream);
 /* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
 int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                         int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,

@@ -317,7 +317,8 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
   SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out, "srpde_bn_relu_fwd: null");
   SRPDE_CHECK_ARG(C % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0, "srpde_bn_relu_fwd: C/ld must be multiples of 4");
   const long long total = P * (C / 4);
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  // with an amax word: fewer, longer blocks (one same-address atomic per block)
+  const int blocks = (int)std::min<long long>((total + 255) / 256, amax ? 1024 : 8192);
   hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
                      out, ldo, P, C, relu, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_fwd");

@@ -959,14 +959,7 @@ __global__ void split_weights_kernel(const float* __restrict__ w, __bf16* __rest
 }
 
 // ------------------------------ weight gradient --------------------------------
-struct WgradParams {
-  const float* dy; int lddy;          // [P][Cout] view
-  const float* x0; int c0; int ldx0;  // forward input (virtual concat)
-  const float* x1; int c1; int ldx1;
-  float* part;                        // [splits][Cout][K]
-  int N, H, W, Cout, ksize, dil;
-  int P, K, Cin, chunk, splits;
-};
+
 
 constexpr int BKP = 16;  // pixels per stage
 
@@ -1291,30 +1284,6 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_v2_kernel(WgradParams p) {
 // images); partial MFMA chains of HP stages (two-level accumulation, as the forward).
 constexpr int BKX = 16;    // pixels per wgrad-x6 stage
 
-template <int RB>
-__device__ __forceinline__ int wx_off(int row, int ch) {   // byte offset of 16-B chunk ch of a row
-  constexpr int sh = RB >= 256 ? 0 : (RB == 128 ? 1 : -1);
-  const int s = sh < 0 ? 0 : (((row >> sh) & 3) << 2) & (RB / 16 - 1);
-  return row * RB + 16 * (ch ^ s);
-}
-
-template <int RB>
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int col0, int lane) {
-  // 8 k-values (pixels 8h .. 8h+7) of column col0 + (lane & 31): two transposed 4-row reads
-  const int h = lane >> 5, q = (lane & 15) >> 2, pp = lane & 3;
-  const int col = col0 + (lane & 16) + 4 * pp;   // this lane's 4-column address slot
-  typedef short v4i16 __attribute__((ext_vector_type(4)));
-  const int o0 = wx_off<RB>(8 * h + q, col >> 3) + 2 * (col & 7);
-  const int o1 = wx_off<RB>(8 * h + 4 + q, col >> 3) + 2 * (col & 7);
-  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o0));
-  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o1));
-  typedef short v8i16 __attribute__((ext_vector_type(8)));
-  const v8i16 c = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  return __builtin_bit_cast(bf16x8, c);
-}
-
 template <int BM, int BN, int WM, int WN, int HP>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -1465,15 +1434,15 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
     bf16x8 ah[TI], am[TI], al[TI];
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
-      ah[i] = tr_frag<RA>(img, wm0 + 32 * i, lane);
-      am[i] = tr_frag<RA>(img + IMG_A, wm0 + 32 * i, lane);
-      al[i] = tr_frag<RA>(img + 2 * IMG_A, wm0 + 32 * i, lane);
+      ah[i] = tr_frag<bf16x8, RA>(img, wm0 + 32 * i, lane);
+      am[i] = tr_frag<bf16x8, RA>(img + IMG_A, wm0 + 32 * i, lane);
+      al[i] = tr_frag<bf16x8, RA>(img + 2 * IMG_A, wm0 + 32 * i, lane);
     }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const bf16x8 bh = tr_frag<RBB>(img + 3 * IMG_A, wn0 + 32 * j, lane);
-      const bf16x8 bm = tr_frag<RBB>(img + 3 * IMG_A + IMG_B, wn0 + 32 * j, lane);
-      const bf16x8 bl = tr_frag<RBB>(img + 3 * IMG_A + 2 * IMG_B, wn0 + 32 * j, lane);
+      const bf16x8 bh = tr_frag<bf16x8, RBB>(img + 3 * IMG_A, wn0 + 32 * j, lane);
+      const bf16x8 bm = tr_frag<bf16x8, RBB>(img + 3 * IMG_A + IMG_B, wn0 + 32 * j, lane);
+      const bf16x8 bl = tr_frag<bf16x8, RBB>(img + 3 * IMG_A + 2 * IMG_B, wn0 + 32 * j, lane);
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         floatx16 c0;
@@ -1914,7 +1883,9 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
 
 static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                            int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout,
-                           int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream, bool x6) {
+                           int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream, bool x6,
+                           const unsigned* amax_dy = nullptr, const unsigned* amax0 = nullptr,
+                           const unsigned* amax1 = nullptr) {
   SRPDE_CHECK_ARG(dy && x0 && dw && workspace, "srpde_conv_wgrad: null pointer");
   SRPDE_CHECK_ARG(c0 % 4 == 0 && c1 % 4 == 0 && lddy % 4 == 0 && ldx0 % 4 == 0 && cout % 4 == 0,
                   "srpde_conv_wgrad: channel counts / strides must be multiples of 4");
@@ -1934,7 +1905,12 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
   p.part = static_cast<float*>(workspace);
   int bm, bn, rc;
   wgrad_tiles(cout, p.K, &bm, &bn);
-  if (x6) {
+  if (amax_dy) {
+    SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout) && wgrad_v2_ok(p) && amax0 && (c1 == 0 || amax1),
+                    "srpde_conv_wgrad_h3: needs c0, c1, cout multiples of 32 and the amax words (c0=%d c1=%d cout=%d)",
+                    c0, c1, cout);
+    rc = launch_wgrad_h3(p, amax_dy, amax0, amax1, stream);
+  } else if (x6) {
     SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout) && wgrad_v2_ok(p),
                     "srpde_conv_wgrad_x6: needs c0, c1, cout multiples of 32 (c0=%d c1=%d cout=%d)", c0, c1, cout);
     if (bm == 128) rc = launch_wgrad_x6<128, 128, 2, 2>(p, stream);
@@ -1972,6 +1948,15 @@ int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int 
                         int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
   return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
                          workspace, ws_bytes, stream, true);
+}
+
+int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,
+                        const unsigned* amax0, const float* x1, int c1, int ldx1, const unsigned* amax1, float* dw,
+                        int cin_real, int accumulate, int n, int h, int w, int cout, int ksize, int dil,
+                        void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(amax_dy, "srpde_conv_wgrad_h3: null amax_dy");
+  return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
+                         workspace, ws_bytes, stream, false, amax_dy, amax0, amax1);
 }
 
 int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout, int cin, int cin_real, int ksize,

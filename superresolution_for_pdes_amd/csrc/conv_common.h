@@ -273,6 +273,46 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
   }
 }
 
+// ------------------------------ weight gradient --------------------------------
+struct WgradParams {
+  const float* dy; int lddy;          // [P][Cout] view
+  const float* x0; int c0; int ldx0;  // forward input (virtual concat)
+  const float* x1; int c1; int ldx1;
+  float* part;                        // [splits][Cout][K]
+  int N, H, W, Cout, ksize, dil;
+  int P, K, Cin, chunk, splits;
+};
+
+// 16-bit MFMA operand images for the weight-gradient kernels: [pixel][column] rows of RB
+// bytes, read back transposed (8 consecutive pixels of one column per lane)
+template <int RB>
+__device__ __forceinline__ int wx_off(int row, int ch) {   // byte offset of 16-B chunk ch of a row
+  constexpr int sh = RB >= 256 ? 0 : (RB == 128 ? 1 : -1);
+  const int s = sh < 0 ? 0 : (((row >> sh) & 3) << 2) & (RB / 16 - 1);
+  return row * RB + 16 * (ch ^ s);
+}
+
+template <typename V, int RB>
+__device__ __forceinline__ V tr_frag(const char* img, int col0, int lane) {
+  // 8 k-values (pixels 8h .. 8h+7) of column col0 + (lane & 31): two transposed 4-row reads
+  const int h = lane >> 5, q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = col0 + (lane & 16) + 4 * pp;   // this lane's 4-column address slot
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  const int o0 = wx_off<RB>(8 * h + q, col >> 3) + 2 * (col & 7);
+  const int o1 = wx_off<RB>(8 * h + 4 + q, col >> 3) + 2 * (col & 7);
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o0));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(uintptr_t)lds_addr_of(img + o1));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 c = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(V, c);
+}
+
+// h3 weight-gradient launcher (conv_h3.hip): raw scaled-back slabs into p.part
+int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigned* amax0, const unsigned* amax1,
+                    hipStream_t st);
+
 // ---------------- host: K-split of the last, under-filled round of tiles ----------------
 static bool tail_split_enabled() {
   static const bool on = [] {

@@ -260,6 +260,234 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
   x6_finish<BM, BN, WM, 1, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wave, 0, lane, smem);
 }
 
+// ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
+// Same tiling and staging as conv_wgrad_x6 (conv.hip): dW tile [BM couts][BN k-columns] over a
+// pixel chunk (split-K), 16 pixels per stage, register-staged pixel rows split into hi / lo
+// fp16 images and read back as transposed MFMA fragments (ds_read_b64_tr_b16).
+constexpr int BKH = 16;    // pixels per stage
+
+struct H3W {
+  const unsigned* ady;   // max|dY| word
+  const unsigned* ax0;   // max|x0| word
+  const unsigned* ax1;   // max|x1| word (c1 > 0)
+};
+
+template <int BM, int BN, int WM, int WN, int HP>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_h3_kernel(WgradParams p, H3W sc) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int RA = BM * 2, RBB = BN * 2;             // image row bytes (fp16)
+  constexpr int IMG_A = BKH * RA, IMG_B = BKH * RBB;    // one plane
+  constexpr int STAGE = 2 * (IMG_A + IMG_B);
+  constexpr int TA = (2 * BM + 255) / 256, TB = (2 * BN + 255) / 256;   // staging tasks per thread
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbm = (p.Cout + BM - 1) / BM, nbn = (p.K + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / nbn, nt = tile - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int HW = p.H * p.W, kc = p.ksize >> 1;
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+  // operand scales: dY (A) and the forward input (B, both halves of a virtual concat)
+  const int ea = h3_exp(*sc.ady);
+  unsigned bb = *sc.ax0;
+  if (p.c1) bb = max(bb, *sc.ax1);
+  const int eb = h3_exp(bb);
+  const float sa = exp2i(ea), sb = exp2i(eb);
+
+  // staging tasks: (pixel row, 8-column chunk); A = dY[pix][m0 + 8c ..], B = X[pix + off][k ..]
+  int a_row[TA], a_col[TA];
+  bool a_on[TA];
+#pragma unroll
+  for (int i = 0; i < TA; ++i) {
+    const int q = tid + 256 * i;
+    a_on[i] = q < 2 * BM;
+    a_row[i] = q / (BM / 8);
+    a_col[i] = (q % (BM / 8)) * 8;
+  }
+  int b_row[TB], b_col[TB], b_dy[TB], b_dx[TB], b_sh[TB], b_ch[TB];
+  bool b_on[TB], b_second[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) {
+    const int q = tid + 256 * i;
+    b_row[i] = q / (BN / 8);
+    b_col[i] = (q % (BN / 8)) * 8;
+    const int k = n0 + b_col[i];
+    b_on[i] = q < 2 * BN && k < p.K;
+    const int tap = b_on[i] ? k / p.Cin : 0;
+    const int ch = k - tap * p.Cin;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    b_dy[i] = (ky - kc) * p.dil;
+    b_dx[i] = (kx - kc) * p.dil;
+    b_sh[i] = b_dy[i] * p.W + b_dx[i];
+    b_second[i] = ch >= p.c0;
+    b_ch[i] = b_second[i] ? ch - p.c0 : ch;
+  }
+
+  // image coordinates of each B task's pixel, advanced by BKH pixels per stage (no divisions
+  // in the loop; BKH < 2 W for every layer here, W >= 10)
+  int b_y[TB], b_x[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) {
+    const int pix = pbeg + b_row[i];
+    const int rem = pix % HW;
+    b_y[i] = rem / p.W;
+    b_x[i] = rem - b_y[i] * p.W;
+  }
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      int x = b_x[i] + BKH, y = b_y[i];
+      while (x >= p.W) { x -= p.W; ++y; }
+      while (y >= p.H) y -= p.H;
+      b_x[i] = x; b_y[i] = y;
+    }
+  };
+  // two register sets: stage s+2 is loaded while stage s computes and stage s+1 is stored
+  float4 ra[2][TA][2], rb[2][TB][2];
+  auto load_stage = [&](int pbase, auto set_tag) {
+    constexpr int SET = decltype(set_tag)::value;
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+      const int pix = pbase + a_row[i], m = m0 + a_col[i];
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (a_on[i] && pix < pend && m < p.Cout) {
+        const float* src = p.dy + (size_t)pix * p.lddy + m;
+        v0 = *reinterpret_cast<const float4*>(src);
+        v1 = *reinterpret_cast<const float4*>(src + 4);   // Cout % 8 == 0
+      }
+      ra[SET][i][0] = v0; ra[SET][i][1] = v1;
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int pix = pbase + b_row[i];
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (b_on[i] && pix < pend) {
+        const int iy = b_y[i] + b_dy[i], ix = b_x[i] + b_dx[i];
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) {
+          const float* src = b_second[i] ? p.x1 + (size_t)(pix + b_sh[i]) * ld1 + b_ch[i]
+                                         : p.x0 + (size_t)(pix + b_sh[i]) * p.ldx0 + b_ch[i];
+          v0 = *reinterpret_cast<const float4*>(src);
+          v1 = *reinterpret_cast<const float4*>(src + 4);
+        }
+      }
+      rb[SET][i][0] = v0; rb[SET][i][1] = v1;
+    }
+  };
+  auto store_stage = [&](auto set_tag) {   // set SET -> LDS buffer SET
+    constexpr int SET = decltype(set_tag)::value;
+    char* base = lds + SET * STAGE;
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+      if (!a_on[i]) continue;
+      half8 h, l;
+      split2h(ra[SET][i][0], ra[SET][i][1], sa, h, l);
+      const int o = wx_off<RA>(a_row[i], a_col[i] >> 3);
+      *reinterpret_cast<half8*>(base + o) = h;
+      *reinterpret_cast<half8*>(base + IMG_A + o) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      if (tid + 256 * i >= 2 * BN) continue;
+      half8 h, l;
+      split2h(rb[SET][i][0], rb[SET][i][1], sb, h, l);
+      const int o = 2 * IMG_A + wx_off<RBB>(b_row[i], b_col[i] >> 3);
+      *reinterpret_cast<half8*>(base + o) = h;
+      *reinterpret_cast<half8*>(base + IMG_B + o) = l;
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  const int nsteps = (pend - pbeg + BKH - 1) / BKH;
+
+  // stage s (parity PAR = s & 1 at compile time): LDS buffer PAR holds it
+  auto stage = [&](int s, auto fresh_tag, auto par_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    constexpr int PAR = decltype(par_tag)::value;
+    if (s + 2 < nsteps) {
+      load_stage(pbeg + (s + 2) * BKH, par_tag);
+      advance();
+    }
+    const char* img = lds + PAR * STAGE;
+    half8 ah[TI], al[TI];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      ah[i] = tr_frag<half8, RA>(img, wm0 + 32 * i, lane);
+      al[i] = tr_frag<half8, RA>(img + IMG_A, wm0 + 32 * i, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const half8 bh = tr_frag<half8, RBB>(img + 2 * IMG_A, wn0 + 32 * j, lane);
+      const half8 bl = tr_frag<half8, RBB>(img + 2 * IMG_A + IMG_B, wn0 + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        floatx16 c0;
+        if (FRESH)
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, floatx16{}, 0, 0, 0);   // small terms first
+        else
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, part[i][j], 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, c0, 0, 0, 0);
+        part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, c0, 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) store_stage(std::integral_constant<int, 1 - PAR>{});
+    __syncthreads();
+  };
+
+  typedef std::integral_constant<int, 0> P0;
+  typedef std::integral_constant<int, 1> P1;
+  if (nsteps > 0) {
+    load_stage(pbeg, P0{});
+    advance();
+    store_stage(P0{});
+  }
+  if (nsteps > 1) {
+    load_stage(pbeg + BKH, P1{});
+    advance();
+  }
+  __syncthreads();
+  static_assert(HP == 4, "stage parities are unrolled for HP = 4");
+  for (int s = 0; s < nsteps; s += HP) {
+    stage(s, std::true_type{}, P0{});
+    if (s + 1 < nsteps) stage(s + 1, std::false_type{}, P1{});
+    if (s + 2 < nsteps) stage(s + 2, std::false_type{}, P0{});
+    if (s + 3 < nsteps) stage(s + 3, std::false_type{}, P1{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+  }
+
+  // slab [split][Cout][K], scales undone (exact powers of two)
+  const float unscale_a = exp2i(-ea), unscale_b = exp2i(-eb);
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = n0 + wn0 + 32 * j + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.Cout && n < p.K) out[(size_t)m * p.K + n] = (acc[i][j][r] * unscale_a) * unscale_b;
+      }
+    }
+}
+
 // fp32 packed weights [rows][K] -> fp16 hi / lo planes [2][rows][K] with a power-of-two scale
 // per row (one wave per row)
 __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
@@ -335,6 +563,22 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
     SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
   }
+  return 0;
+}
+
+int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigned* amax0, const unsigned* amax1,
+                    hipStream_t st) {
+  const H3W sc{amax_dy, amax0, p.c1 ? amax1 : amax0};
+  const int nb = ceil_div(p.Cout, p.Cout >= 128 ? 128 : (p.Cout >= 64 ? 64 : 32)) *
+                 ceil_div(p.K, p.Cout >= 128 ? 128 : 256) * p.splits;
+  if (p.Cout >= 128) {
+    hipLaunchKernelGGL((conv_wgrad_h3_kernel<128, 128, 2, 2, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (128 + 128), st, p, sc);
+  } else if (p.Cout >= 64) {
+    hipLaunchKernelGGL((conv_wgrad_h3_kernel<64, 256, 1, 4, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (64 + 256), st, p, sc);
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_h3_kernel<32, 256, 1, 4, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (32 + 256), st, p, sc);
+  }
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3");
   return 0;
 }
 

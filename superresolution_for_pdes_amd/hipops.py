@@ -204,6 +204,12 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cin_real = dw.shape[1]
     ws_bytes = int(query("srpde_conv_wgrad_workspace_size", n, h, w, cout, cin, ksize))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dy.device)
+    if _CONV_MATH == "h3" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
+        a1 = amax_of(x1) if x1 is not None else None
+        call("srpde_conv_wgrad_h3", pdy, lddy, amax_of(dy).data_ptr(), p0, x0.shape[1], ld0, amax_of(x0).data_ptr(),
+             p1, c1, ld1, _p(a1), dw.data_ptr(), cin_real, int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(),
+             ws_bytes, stream_ptr())
+        return
     x6 = _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout)
     call("srpde_conv_wgrad_x6" if x6 else "srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1,
          dw.data_ptr(), cin_real,
