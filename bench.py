@@ -351,14 +351,16 @@ def main():
         flops_launch = conv_flops(cin, cout, hw) * B
         achieved = flops_launch / (kern_avg * 1e-3) / 1e12 if kern_avg > 0 else None
         from superresolution_for_pdes_amd import hipops as H
-        x6 = H.conv_math() == "x6"
-        # dense MFMA peak of the instruction the kernel runs: fp32 MFMA 157.3 TF, or for the
-        # x6 kernels bf16 MFMA (16 x the fp32 rate = 2516.8 TF) / 6 partial products = 419.5 TF
-        peak = round(157.3 * 16 / 6, 1) if x6 else 157.3
+        math = H.conv_math()
+        # dense MFMA peak of the instruction the kernel runs, in fp32-product units: fp32 MFMA
+        # 157.3 TF; bf16 / fp16 MFMA run at 16x that (2516.8 TF), divided by the partial
+        # products per fp32 product: 6 for x6 (419.5 TF), 3 for h3 (838.9 TF)
+        peak = {"h3": round(157.3 * 16 / 3, 1), "x6": round(157.3 * 16 / 6, 1)}.get(math, 157.3)
+        kname = {"h3": "conv_fwd_h3", "x6": "conv_fwd_x6"}.get(math, "conv_fwd_v2")
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
-                traffic = json.load(open(args.traffic_json)).get(args.roofline_layer)
+                traffic = json.load(open(args.traffic_json)).get(f"{math}:{args.roofline_layer}")
             except (ValueError, OSError):
                 traffic = None
         samples = world * B * args.steps
@@ -373,12 +375,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (x6: fp32 products from 3-way bf16 splits on bf16 MFMA, fp32 accumulate)" if x6 else "f32",
+            "dtype": {"h3": "f32 (h3: fp32 products from power-of-two-scaled 2-piece fp16 splits on fp16 MFMA, "
+                            "fp32 accumulate)",
+                      "x6": "f32 (x6: fp32 products from 3-way bf16 splits on bf16 MFMA, fp32 accumulate)"}.get(math, "f32"),
             "data": "synthetic (x~N(0,1), theta channel=1, t~N(0,1)), resident in HBM",
             "config": {"workload": "UNet 20->40 train step, fp32, batch 1024/GPU, 40x40",
                        "global_batch": world * B, "per_gpu_batch": B, "hw": "40x40",
                        "parallelism": f"dp{world}", "final_loss": round(float(loss.detach()), 6)},
-            "roofline": {"bound": "mfma", "kernel": f"{'conv_fwd_x6' if x6 else 'conv_fwd_v2'}[{args.roofline_layer}]",
+            "roofline": {"bound": "mfma", "kernel": f"{kname}[{args.roofline_layer}]",
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(kern_avg, 4),

@@ -32,7 +32,7 @@ def empty(*shape, device):
 
 
 # ---------------------------------- convolution ------------------------------------
-_CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "x6")
+_CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "h3")
 
 
 def set_conv_math(mode: str):

@@ -1,6 +1,7 @@
 """HBM bytes per launch of the roofline kernel from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/traffic_json.py gpurun_out/pmc_<tag> [layer] [out.json]
+    python tools/traffic_json.py gpurun_out/pmc_<tag> [layer] [out.json] [math]
+(out.json is updated in place under the key "<math>:<layer>", math defaulting to h3)
 FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of the bytes of wide
 streaming reads (MI355X_MICROARCH.md, HBM section) so it is doubled.  The launch is the
 conv kernel plus its tail-fixup kernel (both bracketed by bench.py's HIP events).
@@ -14,6 +15,7 @@ import sys
 d = sys.argv[1]
 layer = sys.argv[2] if len(sys.argv) > 2 else "bridge.3"
 out = sys.argv[3] if len(sys.argv) > 3 else None
+math = sys.argv[4] if len(sys.argv) > 4 else "h3"
 vals = collections.defaultdict(list)
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -24,8 +26,14 @@ for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
 fetch = 2 * 1024 * (mean.get(("main", "FETCH_SIZE"), 0) + mean.get(("fixup", "FETCH_SIZE"), 0))
 write = 1024 * (mean.get(("main", "WRITE_SIZE"), 0) + mean.get(("fixup", "WRITE_SIZE"), 0))
-rec = {layer: round(fetch + write), f"{layer}_detail": {"read_bytes": round(fetch), "write_bytes": round(write),
+key = f"{math}:{layer}"
+rec = {key: round(fetch + write), f"{key}_detail": {"read_bytes": round(fetch), "write_bytes": round(write),
        "source": d, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KiB->B, conv + tail fixup per launch"}}
 print(json.dumps(rec))
 if out:
-    json.dump(rec, open(out, "w"), indent=1)
+    try:
+        old = json.load(open(out))
+    except (OSError, ValueError):
+        old = {}
+    old.update(rec)
+    json.dump(old, open(out, "w"), indent=1)
