@@ -79,20 +79,30 @@ int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const v
  * product on v_mfma_f32_32x32x16_f16, halo-staged activation tiles (conv_h3.hip).
  * amax0/amax1: device words holding max|x0| / max|x1| as float bits (any upper bound within a
  * few orders of magnitude works; srpde_absmax or the amax output of srpde_bn_relu_fwd/_bwd).
- * wsplit/wexp: srpde_split_weights_h3 of the packed weights ([2][rows][K] fp16, [rows] int). */
+ * wsplit/wexp: srpde_split_weights_h3 of the packed weights ([2][rows][K] fp16, [rows] int).
+ * xsplit_out (nullable): receives the scaled hi / lo fp16 pieces of the input, [2][P][c0+c1],
+ * for srpde_conv_wgrad_h3p (the split is computed anyway; storing it costs one 4-B write per
+ * element). */
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* workspace, size_t ws_bytes, hipStream_t stream);
+                      void* xsplit_out, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* weight gradient with the h3 arithmetic (same workspace as srpde_conv_wgrad; c0, c1, cout % 32 == 0);
  * amax_dy / amax0 / amax1: the max|.| words of dy, x0, x1 as for srpde_conv_fwd_h3 */
 int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,
                         const unsigned* amax0, const float* x1, int c1, int ldx1, const unsigned* amax1, float* dw,
                         int cin_real, int accumulate, int n, int h, int w, int cout, int ksize, int dil,
                         void* workspace, size_t ws_bytes, hipStream_t stream);
+/* h3 weight gradient from pre-split operands: dyp = the xsplit_out of the dgrad call (sign -1,
+ * [2][P][cout]) and xp = the xsplit_out of the forward call ([2][P][c0+c1]), with the max|.| words
+ * those calls used.  No split work inside; workspace: srpde_conv_wgrad_h3p_workspace_size. */
+size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int cin, int ksize);
+int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* xp, int c0, const unsigned* amax0,
+                         int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
+                         int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
 int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                         int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,

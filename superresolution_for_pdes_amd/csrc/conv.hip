@@ -1528,6 +1528,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __res
   }
 }
 
+int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, int cin_real, int taps, int accumulate,
+                 hipStream_t stream) {
+  const long long total = (long long)cout * taps * cin;
+  const int blocks = (int)((total + 63) / 64);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, part, dw, splits, cout, cin, cin_real,
+                     taps, accumulate);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce)");
+  return 0;
+}
+
 // W[Cout][Cin_real][k][k] -> Wf[Cout][taps][Cin] and Wd[Cin][taps][Cout] (Cin >= Cin_real, zero pad)
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wf, float* __restrict__ wd,
                                     int cout, int cin, int cin_real, int taps) {
@@ -1927,13 +1937,7 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
     else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
   }
   if (rc) return rc;
-  const int taps = ksize * ksize;
-  const long long total = (long long)cout * p.K;
-  const int blocks = (int)((total + 63) / 64);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, p.part, dw, p.splits, cout,
-                     p.Cin, cin_real, taps, accumulate);
-  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce)");
-  return 0;
+  return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
 }
 
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,

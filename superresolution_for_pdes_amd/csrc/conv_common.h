@@ -313,6 +313,11 @@ __device__ __forceinline__ V tr_frag(const char* img, int col0, int lane) {
 int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigned* amax0, const unsigned* amax1,
                     hipStream_t st);
 
+// fixed-order sum of split-K weight-gradient slabs [splits][Cout][taps*Cin] into torch's
+// [Cout][Cin_real][k][k] layout (conv.hip)
+int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, int cin_real, int taps, int accumulate,
+                 hipStream_t stream);
+
 // ---------------- host: K-split of the last, under-filled round of tiles ----------------
 static bool tail_split_enabled() {
   static const bool on = [] {

@@ -20,9 +20,12 @@
 // operand of one 32-channel chunk is staged ONCE as a halo tile -- the tile's BM pixel rows
 // plus (W+1)*dil rows either side -- and the nine taps read it at nine row offsets (7x fewer
 // A bytes than per-tap staging).  Taps that fall outside the image (padding, row and image
-// wrap) read a zeroed LDS row instead.  The next chunk's halo tile is DMA'd in slices during
-// the current chunk's nine tap stages; the weight tile of each tap stage is double-buffered.
-// Both operands go HBM/L2 -> LDS with buffer_load ... lds (no VGPR staging).
+// wrap) read a zeroed LDS row instead.  The halo tile lands fp32 (buffer_load ... lds DMA,
+// no VGPR staging) and is scaled and split into hi / lo fp16 planes in LDS once per chunk, so
+// each element is split once, not once per tap; the nine tap stages then read MFMA fragments
+// of both operands straight from LDS.  The next chunk's halo tile is DMA'd in slices during
+// the current chunk's stages; the weight tile of each tap stage is double-buffered.  One
+// partial MFMA chain per chunk (two-level fp32 accumulation).
 #include "conv_common.h"
 
 namespace srpde {
@@ -57,24 +60,34 @@ struct H3Args {
   const unsigned* amax0;   // max|x0| (float bits), or null
   const unsigned* amax1;   // max|x1|, or null
   int halo;                // (W + 1) * dil
-  int arows;               // BM + 2 * halo, rounded up to 8
+  int arows;               // BM + 2 * halo, rounded up to 8 (<= 512: at most 8 slices per wave)
+  int relax;               // 1: a stage waits only for its weight DMA (halo slices land later)
+  _Float16* xsplit;        // optional [2][P][Cin] hi / lo planes of the (scaled) input, written
+                           // as a by-product of the split for the weight-gradient kernel
 };
 
-template <int BM, int BN, int WM, int SRB, int HP>
-__global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
-  constexpr int NW = WM;
-  constexpr int TM = BM / WM, TI = TM / 32, TJ = BN / 32;
+// TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
+// the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per stage (16 rows x 64 B)
   constexpr int BPW = (BTOT + NW - 1) / NW;
   constexpr int BP_BYTES = BN * 64;        // one fp16 plane of the B tile
   constexpr int B_STAGE = 2 * BP_BYTES;
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
+  // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its hi / lo fp16 planes (64-B rows)
+  //      | B = two weight stages | 64 zero bytes (the padding row) | 1 KiB DMA sink
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
-  const int a_bytes = h.arows * ROW2;
-  char* const abuf0 = lds;
-  char* const bbuf0 = lds + 2 * a_bytes;
+  const int arows = h.arows;
+  char* const fbuf = lds;
+  char* const shi = fbuf + arows * ROW2;
+  char* const slo = shi + arows * 64;
+  char* const bbuf0 = slo + arows * 64;
   char* const zrow = bbuf0 + 2 * B_STAGE;
+  char* const sink = zrow + 64;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -94,7 +107,7 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
   const int m0 = mt * BM, n0 = nt * BN;
   const int HW = p.H * p.W;
 
-  if (tid < 32) reinterpret_cast<float*>(zrow)[tid] = 0.f;
+  if (tid < 16) reinterpret_cast<float*>(zrow)[tid] = 0.f;
 
   const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
@@ -110,7 +123,8 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
 
   // per-lane tap masks of this wave's output rows
   const int lr = lane & 31, lh = lane >> 5;
-  const int wm0 = wave * TM;
+  const int wmi = wave % WM, wni = wave / WM;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
   unsigned tmask[TI];
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
@@ -142,11 +156,12 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
   const int nch = p.Cin / BK2;
   const int c_beg = tail ? (piece * nch) / p.tsplit : 0;
   const int c_end = tail ? ((piece + 1) * nch) / p.tsplit : nch;
-  const int na = h.arows / 8;                 // A DMA instructions per chunk (8 rows x 128 B)
+  const int na = arows / 8;                   // A DMA instructions per chunk (8 rows x 128 B)
   const int pix0 = m0 - h.halo;
 
-  // A slice `q` of chunk `ch` (8 halo rows) into buffer `buf`
-  auto issue_a = [&](int ch, int q, int buf) {
+  // A slice `q` of chunk `ch` (8 halo rows, fp32) into F; q >= na: a zero-fill DMA into the sink,
+  // so every wave issues the same number of vector-memory ops per stage (exact vmcnt counts)
+  auto issue_a = [&](int ch, int q) {
     const int ch0 = ch * BK2;
     const bool second = ch0 >= p.c0;
     const int32x4 rs = second ? rs1 : rs0;
@@ -154,8 +169,9 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
     const int cb = second ? ch0 - p.c0 : ch0;
     const int r = q * 8 + (lane >> 3);
     const int pix = pix0 + r;
-    const unsigned off = (pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
-    dma16(rs, off, lds_addr_of(abuf0 + buf * a_bytes + q * 1024));
+    const bool real = q < na;
+    const unsigned off = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
+    dma16(rs, off, lds_addr_of(real ? fbuf + q * 1024 : sink));
   };
   auto issue_b = [&](int ch, int tap, int buf) {
     const int k0 = tap * p.Cin + ch * BK2;
@@ -169,95 +185,138 @@ __global__ __launch_bounds__(WM * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H
       }
     }
   };
+  // F (fp32, landed) -> S: scale and split every halo element once per chunk
+  // (the N-tile-0 workgroup of each row tile also stores its own rows' pieces to h.xsplit)
+  const bool wsplit = h.xsplit != nullptr && nt == 0;
+  const size_t xplane = (size_t)p.P * p.Cin;
+  auto convert = [&](int ch) {
+    for (int sg = tid; sg < arows * 4; sg += NT) {
+      const int r = sg >> 2, c8 = sg & 3;
+      const float4 v0 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8) * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8 + 1) * 16);
+      half8 hv, lv;
+      split2h(v0, v1, sa, hv, lv);
+      const int o = r * 64 + swzh(r, c8) * 16;
+      *reinterpret_cast<half8*>(shi + o) = hv;
+      *reinterpret_cast<half8*>(slo + o) = lv;
+      if (wsplit) {
+        const int pix = pix0 + r;
+        if (r >= h.halo && r < h.halo + BM && pix < p.P) {
+          _Float16* dst = h.xsplit + (size_t)pix * p.Cin + ch * BK2 + c8 * 8;
+          *reinterpret_cast<half8*>(dst) = hv;
+          *reinterpret_cast<half8*>(dst + xplane) = lv;
+        }
+      }
+    }
+  };
 
-  floatx16 acc[TI][TJ], part[TI][TJ];
+  floatx16 acc[TI][TJ];
+  floatx16 part[TWO_LEVEL ? TI : 1][TWO_LEVEL ? TJ : 1];
+  auto chain = [&](int i, int j) -> floatx16& {
+    if constexpr (TWO_LEVEL) return part[i][j];
+    else return acc[i][j];
+  };
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f, part[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // prologue: whole halo tile of the first chunk + first weight stage
-  for (int q = wave; q < na; q += NW) issue_a(c_beg, q, c_beg & 1);
+  for (int q = wave; q < na; q += NW) issue_a(c_beg, q);
   issue_b(c_beg, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  convert(c_beg);
+  __syncthreads();
 
   int sidx = 0;      // stage counter (B buffer parity)
-  int hp = 0;        // stages in the current partial chain
-  for (int ch = c_beg; ch < c_end; ++ch) {
-    const char* a = abuf0 + (ch & 1) * a_bytes;
-    for (int tap = 0; tap < 9; ++tap, ++sidx) {
-      // prefetch: next weight stage, one slice of the next chunk's halo tile
-      if (tap < 8) issue_b(ch, tap + 1, (sidx + 1) & 1);
-      else if (ch + 1 < c_end) issue_b(ch + 1, 0, (sidx + 1) & 1);
-      if (ch + 1 < c_end) {
-        const int q = wave + tap * NW;
-        if (q < na) issue_a(ch + 1, q, (ch + 1) & 1);
-        if (tap == 8)
-          for (int q2 = wave + 9 * NW; q2 < na; q2 += NW) issue_a(ch + 1, q2, (ch + 1) & 1);
-      }
-      const int ky = tap / 3, kx = tap - ky * 3;
-      const int toff = p.sign > 0 ? (ky * p.W + kx) * p.dil : ((2 - ky) * p.W + (2 - kx)) * p.dil;
-      const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+  auto stage = [&](int ch, auto tap_tag) {
+    constexpr int TAP = decltype(tap_tag)::value;
+    constexpr int KY = TAP / 3, KX = TAP % 3;
+    // prefetch: next weight stage, one slice of the next chunk's halo tile (F is free: the
+    // current chunk was converted to S before its first stage)
+    if (TAP < 8) issue_b(ch, TAP + 1, (sidx + 1) & 1);
+    else if (ch + 1 < c_end) issue_b(ch + 1, 0, (sidx + 1) & 1);
+    const bool more = ch + 1 < c_end;
+    if (TAP < 8 && more) issue_a(ch + 1, wave + TAP * NW);   // slices 0..7 of the next halo tile
+    const int toff = p.sign > 0 ? (KY * p.W + KX) * p.dil : ((2 - KY) * p.W + (2 - KX)) * p.dil;
+    const char* b = bbuf0 + (sidx & 1) * B_STAGE;
 #pragma unroll
-      for (int g = 0; g < BK2 / 16; ++g) {
-        half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+    for (int g = 0; g < BK2 / 16; ++g) {
+      half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int r = wm0 + i * 32 + lr + toff;
+        const bool ok = (tmask[i] >> TAP) & 1u;
+        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
+        ah[i] = *reinterpret_cast<const half8*>(ok ? shi + o : zrow);
+        al[i] = *reinterpret_cast<const half8*>(ok ? slo + o : zrow);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 32 + lr;
+        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
+        bh[j] = *reinterpret_cast<const half8*>(b + o);
+        bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
-          const int r = wm0 + i * 32 + lr + toff;
-          const int c = 4 * g + 2 * lh;
-          const bool ok = (tmask[i] >> tap) & 1u;
-          const char* a0 = ok ? a + r * ROW2 + swz(r, c) * 16 : zrow;
-          const char* a1 = ok ? a + r * ROW2 + swz(r, c + 1) * 16 : zrow;
-          const float4 x0 = *reinterpret_cast<const float4*>(a0);
-          const float4 x1 = *reinterpret_cast<const float4*>(a1);
-          split2h(x0, x1, sa, ah[i], al[i]);
+          floatx16 c0;
+          if (TWO_LEVEL && TAP == 0 && g == 0)   // a chunk's partial chain starts from zero
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], floatx16{}, 0, 0, 0);
+          else   // small terms first
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], chain(i, j), 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
+          chain(i, j) = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
         }
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          const int r = j * 32 + lr;
-          const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-          bh[j] = *reinterpret_cast<const half8*>(b + o);
-          bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
-        }
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            floatx16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], part[i][j], 0, 0, 0);  // small first
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
-            part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
-          }
-      }
-      if (++hp == HP) {   // two-level accumulation: fold the partial chain
-        hp = 0;
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            acc[i][j] += part[i][j];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) part[i][j][r] = 0.f;
-          }
-      }
+    }
+    ++sidx;
+    // the next stage's weights must have landed; the halo slice issued after them may still be
+    // in flight (it is waited for by the next stage's count, long before the chunk ends)
+    if (TAP < 8 && more && h.relax)
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    stage(ch, std::integral_constant<int, 0>{});
+    stage(ch, std::integral_constant<int, 1>{});
+    stage(ch, std::integral_constant<int, 2>{});
+    stage(ch, std::integral_constant<int, 3>{});
+    stage(ch, std::integral_constant<int, 4>{});
+    stage(ch, std::integral_constant<int, 5>{});
+    stage(ch, std::integral_constant<int, 6>{});
+    stage(ch, std::integral_constant<int, 7>{});
+    stage(ch, std::integral_constant<int, 8>{});
+    // two-level accumulation: one partial chain per channel chunk (9 taps x 32 channels)
+    if constexpr (TWO_LEVEL) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+    }
+    if (ch + 1 < c_end) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
+      convert(ch + 1);
       __syncthreads();
     }
   }
-  // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact), then fold the last partial chain
+  // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact)
   const float ia = exp2i(-ea);
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + j * 32 + lr;
+    const int col = n0 + wn0 + j * 32 + lr;
     const float iw = col < p.Cout ? exp2i(-h.wexp[col]) : 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = ((acc[i][j][r] + part[i][j][r]) * ia) * iw;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * iw;
   }
-  x6_finish<BM, BN, WM, 1, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wave, 0, lane, smem);
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem);
 }
 
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
@@ -488,6 +547,203 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_h3_kernel(WgradParams p, H3
     }
 }
 
+// ------------- weight gradient h3p: both operands arrive pre-split (fp16 hi / lo planes) -------------
+// dW[m][k] = sum_p dY[p][m] * X[p + off(tap(k))][c(k)] as an fp16 GEMM over a pixel chunk (split-K):
+// A = dY pieces [2][P][Cout] (stored by the dgrad kernel), B = input pieces [2][P][Cin] (stored by
+// the forward kernel), each scaled by its tensor's power of two.  A stage is PS pixel rows of
+// both operands' hi and lo planes, DMA'd straight into swizzled LDS images (buffer_load ... lds;
+// taps that leave the image and rows past the chunk are zero-filled by the range check), and
+// the MFMA fragments come back through ds_read_b64_tr_b16.  A ring of NST stages keeps NST-1
+// stages of DMA in flight; every wave issues exactly DPW DMA ops per stage (spare ones go to a
+// sink) so the waits are exact vmcnt counts.  No VALU work in the loop.
+struct H3P {
+  const _Float16* dyp;     // [2][P][Cout]
+  const _Float16* xp;      // [2][P][Cin]
+  const unsigned* ady;     // max|dY| word (the dgrad split's scale)
+  const unsigned* ax0;     // max|x0|, max|x1| words (the forward split's scale)
+  const unsigned* ax1;
+};
+
+template <int RB>
+__device__ __forceinline__ int wx_swz(int row) { return (wx_off<RB>(row, 0) - row * RB) >> 4; }
+
+template <int BM, int BN, int WM, int WN, int PS, int NST, int HP>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradParams p, H3P q) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int RA = BM * 2, RBB = BN * 2;              // image row bytes
+  constexpr int IMG_A = PS * RA, IMG_B = PS * RBB;       // one plane
+  constexpr int STAGE = 2 * (IMG_A + IMG_B);
+  constexpr int NA = 2 * IMG_A / 1024, NB = 2 * IMG_B / 1024;   // DMA wave-instructions per stage
+  constexpr int DPW = (NA + NB + NW - 1) / NW;
+  static_assert(IMG_A % 1024 == 0 && IMG_B % 1024 == 0, "images must be whole KiB");
+  static_assert(PS % 16 == 0 && (NST - 2) * DPW <= 63, "stage geometry");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  char* const sink = lds + NST * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmi = wave % WM, wni = wave / WM;
+  const int nbm = (p.Cout + BM - 1) / BM, nbn = (p.K + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / nbn, nt = tile - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int nsteps = (pend - pbeg + PS - 1) / PS;
+  const int kc = p.ksize >> 1;
+
+  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.Cout * 2));
+  const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
+  const size_t aplane = (size_t)p.P * p.Cout * 2, bplane = (size_t)p.P * p.Cin * 2;   // bytes
+
+  // this wave's DMA ops: op j is instruction w = wave + j*NW (A instructions first, then B)
+  int d_row[DPW], d_kind[DPW];            // kind: 0 = A, 1 = B, 2 = spare (sink)
+  unsigned d_base[DPW];                   // A: byte offset of (row 0 of the chunk, this lane's chunk)
+  int d_dy[DPW], d_dx[DPW], d_lds[DPW];
+  int d_y[DPW], d_x[DPW];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int w = wave + j * NW;
+    d_kind[j] = 2; d_row[j] = 0; d_base[j] = 0; d_dy[j] = 0; d_dx[j] = 0; d_lds[j] = 0; d_y[j] = 0; d_x[j] = 0;
+    if (w < NA) {
+      const int pl = w / (NA / 2), idx = w - pl * (NA / 2);
+      const int byte = idx * 1024 + lane * 16;
+      const int row = byte / RA, slot = (byte - row * RA) >> 4;
+      const int ch = slot ^ wx_swz<RA>(row);
+      const int m = m0 + 8 * ch;
+      d_row[j] = row;
+      d_lds[j] = pl * IMG_A + idx * 1024;
+      d_kind[j] = m < p.Cout ? 0 : 2;
+      d_base[j] = (unsigned)(pl * aplane + (size_t)m * 2);
+    } else if (w < NA + NB) {
+      const int wb = w - NA;
+      const int pl = wb / (NB / 2), idx = wb - pl * (NB / 2);
+      const int byte = idx * 1024 + lane * 16;
+      const int row = byte / RBB, slot = (byte - row * RBB) >> 4;
+      const int ch = slot ^ wx_swz<RBB>(row);
+      const int k = n0 + 8 * ch;
+      d_row[j] = row;
+      d_lds[j] = 2 * IMG_A + pl * IMG_B + idx * 1024;
+      if (k < p.K) {
+        const int tap = k / p.Cin, c = k - tap * p.Cin;
+        const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+        d_kind[j] = 1;
+        d_dy[j] = (ky - kc) * p.dil;
+        d_dx[j] = (kx - kc) * p.dil;
+        d_base[j] = (unsigned)(pl * bplane + (size_t)c * 2);
+      }
+      const int pix = pbeg + row, rem = pix % (p.H * p.W);
+      d_y[j] = rem / p.W;
+      d_x[j] = rem - d_y[j] * p.W;
+    } else {
+      d_lds[j] = 0;
+    }
+  }
+  // issue stage `s` into ring slot s % NST (always DPW ops per wave; past the chunk: zero fill)
+  auto issue = [&](int s) {
+    char* st = lds + (s % NST) * STAGE;
+    const int pbase = pbeg + s * PS;
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int pix = pbase + d_row[j];
+      const bool in = s < nsteps && pix < pend;
+      if (d_kind[j] == 0) {
+        const unsigned off = in ? d_base[j] + (unsigned)pix * (unsigned)(p.Cout * 2) : OOB;
+        dma16(rsa, off, lds_addr_of(st + d_lds[j]));
+      } else if (d_kind[j] == 1) {
+        const int iy = d_y[j] + d_dy[j], ix = d_x[j] + d_dx[j];
+        const bool ok = in && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        const unsigned off = ok ? d_base[j] + (unsigned)(pix + d_dy[j] * p.W + d_dx[j]) * (unsigned)(p.Cin * 2) : OOB;
+        dma16(rsb, off, lds_addr_of(st + d_lds[j]));
+        int x = d_x[j] + PS, y = d_y[j];   // image coordinates of the next stage's pixel
+        while (x >= p.W) { x -= p.W; ++y; }
+        while (y >= p.H) y -= p.H;
+        d_x[j] = x; d_y[j] = y;
+      } else {
+        dma16(rsa, OOB, lds_addr_of(d_lds[j] ? st + d_lds[j] : sink));
+      }
+    }
+  };
+
+  const int ea = h3_exp(*q.ady);
+  unsigned xb = *q.ax0;
+  if (p.c1) xb = max(xb, *q.ax1);
+  const int eb = h3_exp(xb);
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s);
+  auto stage = [&](int s, auto fresh_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DPW) : "memory");
+    __syncthreads();
+    issue(s + NST - 1);
+    const char* st = lds + (s % NST) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < PS / 16; ++kk) {
+      half8 ah[TI], al[TI];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        ah[i] = tr_frag<half8, RA>(st + kk * 16 * RA, wm0 + 32 * i, lane);
+        al[i] = tr_frag<half8, RA>(st + IMG_A + kk * 16 * RA, wm0 + 32 * i, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const half8 bh = tr_frag<half8, RBB>(st + 2 * IMG_A + kk * 16 * RBB, wn0 + 32 * j, lane);
+        const half8 bl = tr_frag<half8, RBB>(st + 2 * IMG_A + IMG_B + kk * 16 * RBB, wn0 + 32 * j, lane);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          floatx16 c0;
+          if (FRESH && kk == 0)
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, floatx16{}, 0, 0, 0);   // small terms first
+          else
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, part[i][j], 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, c0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  for (int s = 0; s < nsteps; s += HP) {
+    stage(s, std::true_type{});
+#pragma unroll
+    for (int h2 = 1; h2 < HP; ++h2)
+      if (s + h2 < nsteps) stage(s + h2, std::false_type{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // spare DMAs land before the workgroup retires
+
+  // slab [split][Cout][K], scales undone (exact powers of two)
+  const float ua = exp2i(-ea), ub = exp2i(-eb);
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = n0 + wn0 + 32 * j + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.Cout && n < p.K) out[(size_t)m * p.K + n] = (acc[i][j][r] * ua) * ub;
+      }
+    }
+}
+
 // fp32 packed weights [rows][K] -> fp16 hi / lo planes [2][rows][K] with a power-of-two scale
 // per row (one wave per row)
 __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
@@ -533,16 +789,20 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 }
 
 // ---------------------------------- host side ---------------------------------------
-static int h3_cfg(int cout) { return cout % 128 == 0 ? 0 : (cout % 64 == 0 ? 1 : 2); }
+// tile configs: 1 = 256x128, 2 = 256x64, 3 = 256x32.  (A 256x256 single-level tile with a 4x2
+// wave grid measured no faster on bridge.3 -- 1.194 vs 1.197 ms -- at 3x the fp32 summation
+// error, so every config keeps the two-level accumulation.)
+static int h3_cfg(int cout) { return cout % 128 == 0 ? 1 : (cout % 64 == 0 ? 2 : 3); }
+static int h3_bn(int cfg) { return cfg == 1 ? 128 : cfg == 2 ? 64 : 32; }
 constexpr int H3_BM = 256;
 
 static int h3_arows(int w, int dil) { return (H3_BM + 2 * (w + 1) * dil + 7) / 8 * 8; }
 
-static size_t h3_lds(int bn, int arows) { return (size_t)2 * arows * ROW2 + (size_t)2 * 2 * bn * 64 + 128; }
+static size_t h3_lds(int bn, int arows) { return (size_t)arows * (ROW2 + 128) + (size_t)2 * 2 * bn * 64 + 64 + 1024; }
 
-template <int BM, int BN, int WM, int SRB>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL>
 static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
-  constexpr int NT = WM * 64;
+  constexpr int NT = WM * WN * 64;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
   const int T = nbm * nbn;
   const size_t lds = h3_lds(BN, h.arows);
@@ -557,7 +817,7 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, SRB, 2>), dim3(grid), dim3(NT), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL>), dim3(grid), dim3(NT), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -582,6 +842,83 @@ int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigne
   return 0;
 }
 
+// h3p tiles: Cout >= 256: 256x128 (4x2 waves); 128: 128x256 (2x4); 64: 64x256 (1x8); 32: 32x256 (1x8)
+static void h3p_tiles(int cout, int* bm, int* bn) {
+  if (cout >= 256) { *bm = 256; *bn = 128; }
+  else if (cout >= 128) { *bm = 128; *bn = 256; }
+  else if (cout >= 64) { *bm = 64; *bn = 256; }
+  else { *bm = 32; *bn = 256; }
+}
+
+void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
+  int bm, bn;
+  h3p_tiles(cout, &bm, &bn);
+  const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
+  // one workgroup per CU (LDS): ~4 rounds of 256 CUs, chunks a multiple of the 32-pixel stage
+  const long long want = std::max(1LL, 1024 / tiles);
+  long long c = (P + want - 1) / want;
+  c = (c + 31) / 32 * 32;
+  if (c < 256) c = 256;
+  *chunk = (int)c;
+  *splits = ceil_div(P, c);
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_h3p(const WgradParams& p, const H3P& q, hipStream_t st) {
+  constexpr int PS = 32, NST = 3;
+  const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
+  const size_t lds = (size_t)NST * 2 * PS * 2 * (BM + BN) + 1024;
+  hipLaunchKernelGGL((conv_wgrad_h3p_kernel<BM, BN, WM, WN, PS, NST, 4>), dim3(nb), dim3(WM * WN * 64), lds, st, p, q);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p");
+  return 0;
+}
+
+}  // namespace srpde
+
+using namespace srpde;
+
+extern "C" {
+
+size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int cin, int ksize) {
+  int chunk, splits;
+  h3p_split(n * h * w, cout, ksize * ksize * cin, &chunk, &splits);
+  return (size_t)splits * cout * ksize * ksize * cin * sizeof(float);
+}
+
+int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* xp, int c0, const unsigned* amax0,
+                         int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
+                         int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dyp && xp && dw && workspace && amax_dy && amax0 && (c1 == 0 || amax1),
+                  "srpde_conv_wgrad_h3p: null pointer");
+  SRPDE_CHECK_ARG(cout % 32 == 0 && (c0 + c1) % 8 == 0 && ksize == 3 && cin_real <= c0 + c1,
+                  "srpde_conv_wgrad_h3p: needs cout %% 32 == 0, cin %% 8 == 0, ksize 3 (cout=%d cin=%d)", cout, c0 + c1);
+  SRPDE_CHECK_ARG(aligned16(dyp) && aligned16(xp), "srpde_conv_wgrad_h3p: planes must be 16-byte aligned");
+  WgradParams p;
+  p.dy = nullptr; p.lddy = cout; p.x0 = nullptr; p.c0 = c0; p.ldx0 = c0 + c1; p.x1 = nullptr; p.c1 = c1;
+  p.ldx1 = c0 + c1;
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  SRPDE_CHECK_ARG(2LL * p.P * std::max(cout, p.Cin) * 2 < (1LL << 31), "srpde_conv_wgrad_h3p: tensor too large");
+  h3p_split(p.P, cout, p.K, &p.chunk, &p.splits);
+  const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
+  if (ws_bytes < need) {
+    set_error("srpde_conv_wgrad_h3p: workspace %zu < %zu bytes", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  p.part = static_cast<float*>(workspace);
+  const H3P q{static_cast<const _Float16*>(dyp), static_cast<const _Float16*>(xp), amax_dy, amax0, c1 ? amax1 : amax0};
+  int rc;
+  if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
+  else if (cout >= 128) rc = launch_h3p<128, 256, 2, 4>(p, q, stream);
+  else if (cout >= 64) rc = launch_h3p<64, 256, 1, 8>(p, q, stream);
+  else rc = launch_h3p<32, 256, 1, 8>(p, q, stream);
+  if (rc) return rc;
+  return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
+}
+
+}  // extern "C"
+
+namespace srpde {
 }  // namespace srpde
 
 using namespace srpde;
@@ -590,9 +927,9 @@ extern "C" {
 
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
   if (!(ksize == 3 && c0 % 32 == 0 && c1 % 32 == 0 && cout % 32 == 0 && c0 + c1 > 0 && w > 0 && dil >= 1)) return 0;
-  const int bn = h3_cfg(cout) == 0 ? 128 : (h3_cfg(cout) == 1 ? 64 : 32);
+  const int bn = h3_bn(h3_cfg(cout));
   const int arows = h3_arows(w, dil);
-  return (arows / 8 <= 9 * 8 && h3_lds(bn, arows) <= 160 * 1024) ? 1 : 0;
+  return (arows <= 512 && h3_lds(bn, arows) <= 160 * 1024) ? 1 : 0;
 }
 
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream) {
@@ -616,7 +953,7 @@ int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hi
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* workspace, size_t ws_bytes, hipStream_t stream) {
+                      void* xsplit_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
@@ -646,10 +983,17 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   a.amax1 = c1 ? amax1 : nullptr;
   a.halo = (w + 1) * dil;
   a.arows = h3_arows(w, dil);
+  static const int relax = [] {
+    const char* e = getenv("SRPDE_H3_RELAX");   // tuning/diagnostics: 0 = wait for every DMA each stage
+    return e ? atoi(e) : 1;
+  }();
+  a.relax = relax;
+  a.xsplit = static_cast<_Float16*>(xsplit_out);
+  SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
   switch (h3_cfg(cout)) {
-    case 0: return launch_fwd_h3<256, 128, 8, 128>(p, a, stream, workspace, ws_bytes);
-    case 1: return launch_fwd_h3<256, 64, 8, 256>(p, a, stream, workspace, ws_bytes);
-    default: return launch_fwd_h3<256, 32, 8, 256>(p, a, stream, workspace, ws_bytes);
+    case 1: return launch_fwd_h3<256, 128, 8, 1, 128, true>(p, a, stream, workspace, ws_bytes);
+    case 2: return launch_fwd_h3<256, 64, 8, 1, 256, true>(p, a, stream, workspace, ws_bytes);
+    default: return launch_fwd_h3<256, 32, 8, 1, 256, true>(p, a, stream, workspace, ws_bytes);
   }
 }
 

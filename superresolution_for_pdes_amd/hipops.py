@@ -93,7 +93,14 @@ def conv_stats_buffer(n, h, w, cout, device):
     return empty(nblk, cout, 2, device=device), nblk, int(query("srpde_conv_stats_rows_per_block", cout))
 
 
-def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None):
+def h3_capable(c0, c1, cout, w, dil, ksize=3):
+    return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, ksize))
+
+
+def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
+             planes_out=None):
+    """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
+    ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad."""
     p0, ld0 = _pl(x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
@@ -108,8 +115,12 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         a1 = amax_of(x1) if x1 is not None else None
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
-             ws.data_ptr(), ws.numel(), stream_ptr())
+             _p(planes_out), ws.data_ptr(), ws.numel(), stream_ptr())
+        if planes_out is not None:
+            planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
+            planes_out._srpde_c0 = x0.shape[1]
         return
+    assert planes_out is None, "planes_out needs the h3 kernels"
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
         planes = getattr(wpack, "x6", None)
         if planes is None:
@@ -214,6 +225,26 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     call("srpde_conv_wgrad_x6" if x6 else "srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1,
          dw.data_ptr(), cin_real,
          int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
+
+
+def split_planes_buffer(P, c, device):
+    """[2, P, c] fp16 buffer for the h3 kernels' stored input split (planes_out)."""
+    return torch.empty(2, P, c, dtype=torch.float16, device=device)
+
+
+def conv_wgrad_h3p(dyp, xp, dw, n, h, w, ksize=3, dil=1, accumulate=False):
+    """Weight gradient from the stored splits: ``dyp`` from the dgrad conv_fwd(planes_out=...),
+    ``xp`` from the forward conv_fwd(planes_out=...), each carrying its max|.| word(s)."""
+    cout, cin = dyp.shape[2], xp.shape[2]
+    ax = xp._srpde_amax
+    a0, a1 = (ax, None) if not isinstance(ax, tuple) else ax
+    c1 = 0 if a1 is None else cin - xp._srpde_c0
+    c0 = cin - c1
+    ws_bytes = int(query("srpde_conv_wgrad_h3p_workspace_size", n, h, w, cout, cin, ksize))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dyp.device)
+    call("srpde_conv_wgrad_h3p", dyp.data_ptr(), dyp._srpde_amax.data_ptr(), xp.data_ptr(), c0, a0.data_ptr(), c1,
+         _p(a1), dw.data_ptr(), dw.shape[1], int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes,
+         stream_ptr())
 
 
 # ---------------------------------- batch norm -------------------------------------

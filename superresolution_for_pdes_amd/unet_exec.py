@@ -78,9 +78,13 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots):
     wf, _ = H.pack_conv_weights(conv.weight, cin)
     P = n * h * w
     y = H.empty(P, cout, device=dev)
+    xp = None
     if training:
         stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev)
-        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats)
+        c1 = x1.shape[1] if x1 is not None else 0
+        if H.h3_capable(x0.shape[1], c1, cout, w, dil) and H.h3_capable(cout, 0, cin, w, dil):
+            xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
+        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp)
         mom = bn.momentum if bn.momentum is not None else 0.0
         mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
                                            bn.num_batches_tracked, mom, bn.eps)
@@ -89,20 +93,28 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots):
         mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
     a = H.empty(P, cout, device=dev)
     H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
-    return a, (x0, x1, y, mean, invstd)
+    return a, (x0, x1, y, mean, invstd, xp)
 
 
 def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False):
-    x0, x1, y, mean, invstd = saved
+    """dgrad first: its h3 kernel stores dy's split, which the weight gradient then reads together
+    with the input's split stored by the forward (h3p); otherwise the splitting wgrad kernels."""
+    x0, x1, y, mean, invstd, xp = saved
     P, cout = y.shape
     dy = H.empty(P, cout, device=y.device)
     H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
                   amax=slots.take())
-    H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
+    dyp = None
     if dx is not None:
         cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
         _, wd = H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)
-        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None)
+        if xp is not None:
+            dyp = H.split_planes_buffer(P, cout, y.device)
+        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp)
+    if xp is not None and dyp is not None:
+        H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)
+    else:
+        H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
 
 
 def _block_fwd(blk, x0, x1, n, h, w, training, slots):

@@ -364,3 +364,40 @@ def test_amax_words_match_outputs():
     got = slots.buf.cpu().numpy().view(np.float32)
     assert got[0] == float(out.abs().max()) and got[1] == float(dy.abs().max())
     assert out._srpde_amax.data_ptr() == slots.buf.data_ptr()
+
+
+@pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
+    (4, 512, 0, 512, 10, 2), (3, 512, 256, 256, 10, 1), (2, 256, 128, 128, 20, 1), (2, 128, 64, 64, 40, 1),
+    (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1)])
+def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
+    """h3p: the forward and dgrad kernels store their operand splits (planes_out) and the weight
+    gradient consumes them (no split work of its own).  Against fp64: within 3x the fp32-MFMA
+    kernel's error (+1e-7) and < 1e-6 relative L2; ragged P, Cout not a tile multiple, dil 2 on 7x7."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(n * 31 + cout + cin0)
+    cin = cin0 + cin1
+    x = torch.randn(n, cin, h, h, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * (2.0 / (9 * cin)) ** 0.5
+    dy = torch.randn(n, cout, h, h, generator=g, dtype=torch.float64) * 1e-3
+    dw64 = torch.nn.grad.conv2d_weight(x, wt.shape, dy, padding=dil, dilation=dil)
+    xr = rows(x.float()).to(DEV)
+    x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
+    dyr = rows(dy.float()).to(DEV)
+    P = n * h * h
+    H.set_conv_math("h3")
+    assert H.h3_capable(cin0, cin1, cout, h, dil) and H.h3_capable(cout, 0, cin, h, dil)
+    wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
+    xp, dyp = H.split_planes_buffer(P, cin, DEV), H.split_planes_buffer(P, cout, DEV)
+    y = H.empty(P, cout, device=DEV)
+    H.conv_fwd(x0, x1, wf, None, y, n, h, h, cout, 3, dil, 1, False, None, xp)
+    dx = H.empty(P, cin, device=DEV)
+    H.conv_fwd(dyr, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None, dyp)
+    dw = torch.empty(cout, cin, 3, 3, device=DEV)
+    H.conv_wgrad_h3p(dyp, xp, dw, n, h, h, 3, dil)
+    H.set_conv_math("f32")
+    dwf = torch.empty(cout, cin, 3, 3, device=DEV)
+    H.conv_wgrad(dyr, x0, x1, dwf, n, h, h, 3, dil)
+    torch.cuda.synchronize()
+    e_h3p, e_f32 = rel(dw, dw64), rel(dwf, dw64)
+    print(f"wgrad h3p {e_h3p:.3e} f32 {e_f32:.3e}")
+    assert e_h3p < 1e-6 and e_h3p < 3.0 * e_f32 + 1e-7, (e_h3p, e_f32)

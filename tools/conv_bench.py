@@ -38,9 +38,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--math", default="x6", choices=("h3", "x6", "f32", "x6p"))
+    ap.add_argument("--math", default=None, choices=("h3", "x6", "f32", "x6p"), help="default: the package default (h3)")
     args = ap.parse_args()
-    H.set_conv_math("x6" if args.math == "x6p" else args.math)
+    if args.math:
+        H.set_conv_math("x6" if args.math == "x6p" else args.math)
     dev = "cuda"
     n = args.batch
     tot = {}
@@ -64,6 +65,13 @@ def main():
         dx = torch.empty(P, cin, device=dev)
         dw = torch.empty_like(w)
         line = f"{name:11s}"
+        # h3 as training runs it: forward and dgrad store their operand splits, wgrad reads them
+        h3p = H.conv_math() == "h3" and H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, cin, hw, dil)
+        xp = H.split_planes_buffer(P, cin, dev) if h3p else None
+        dyp = H.split_planes_buffer(P, cout, dev) if h3p else None
+        if h3p:
+            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
+            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
         for kind in args.only.split(","):
             if kind == "fwd" and args.math == "x6p":   # inputs pre-split outside the timed call
                 p0, p1 = H.split_planes(x0), (H.split_planes(x1) if x1 is not None else None)
@@ -74,10 +82,13 @@ def main():
                 ms = timeit(lambda: H.conv_fwd_x6p(pdy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
                             args.iters)
             elif kind == "fwd":
-                ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats), args.iters)
-            elif kind == "dgrad":
-                ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
+                ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp),
                             args.iters)
+            elif kind == "dgrad":
+                ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp),
+                            args.iters)
+            elif h3p:
+                ms = timeit(lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, hw, hw, 3, dil), args.iters)
             else:
                 ms = timeit(lambda: H.conv_wgrad(dy, x0, x1, dw, n, hw, hw, 3, dil), args.iters)
             tf = flops / ms / 1e9
