@@ -62,17 +62,15 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // builtin, hipcc treats the DMA as an LDS store that may alias the following ds_reads and
 // emits s_waitcnt vmcnt(0) right after it, serialising the prefetch behind the compute;
 // as asm it is invisible to the waitcnt pass and we count vmcnt ourselves (vmcnt(0) before
-// the stage barrier).  M0 (the wave-uniform LDS destination) is saved/restored inside.
+// the stage barrier).  The wave-uniform LDS destination goes in M0 through the "{m0}" operand
+// constraint, so the compiler allocates M0 (no save / restore); the s_nop covers the M0-write
+// -> LDS-DMA read hazard the compiler cannot see inside the asm.
 __device__ __forceinline__ void dma16(int32x4 rsrc, unsigned voff, unsigned lds_addr) {
-  unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_addr)
+      "buffer_load_dwordx4 %0, %1, 0 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "{m0}"(__builtin_amdgcn_readfirstlane(lds_addr))
       : "memory");
 }
 

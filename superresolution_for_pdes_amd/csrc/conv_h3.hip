@@ -243,36 +243,53 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
     if (TAP < 8 && more) issue_a(ch + 1, wave + TAP * NW);   // slices 0..7 of the next halo tile
     const int toff = p.sign > 0 ? (KY * p.W + KX) * p.dil : ((2 - KY) * p.W + (2 - KX)) * p.dil;
     const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+    // every fragment of the stage is read up front (both 16-k groups), then the MFMAs run: the
+    // second group's reads complete under the first group's MFMAs
+    constexpr int NG = BK2 / 16;
+    half8 ah[NG][TI], al[NG][TI], bh[NG][TJ], bl[NG][TJ];
 #pragma unroll
-    for (int g = 0; g < BK2 / 16; ++g) {
-      half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+    for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int r = wm0 + i * 32 + lr + toff;
         const bool ok = (tmask[i] >> TAP) & 1u;
         const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        ah[i] = *reinterpret_cast<const half8*>(ok ? shi + o : zrow);
-        al[i] = *reinterpret_cast<const half8*>(ok ? slo + o : zrow);
+        ah[g][i] = *reinterpret_cast<const half8*>(ok ? shi + o : zrow);
+        al[g][i] = *reinterpret_cast<const half8*>(ok ? slo + o : zrow);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int r = wn0 + j * 32 + lr;
         const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        bh[j] = *reinterpret_cast<const half8*>(b + o);
-        bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
+        bh[g][j] = *reinterpret_cast<const half8*>(b + o);
+        bl[g][j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
       }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           floatx16 c0;
           if (TWO_LEVEL && TAP == 0 && g == 0)   // a chunk's partial chain starts from zero
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], floatx16{}, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], floatx16{}, 0, 0, 0);
           else   // small terms first
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], chain(i, j), 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
-          chain(i, j) = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], chain(i, j), 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bl[g][j], c0, 0, 0, 0);
+          chain(i, j) = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bh[g][j], c0, 0, 0, 0);
         }
+    // schedule: the first group's reads, then one MFMA per second-group read, then the rest
+    // (without this the scheduler parks each read right before its MFMA and exposes its latency)
+    {
+      constexpr int RD = 2 * (TI + TJ), MF = 3 * TI * TJ;
+      __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+#pragma unroll
+      for (int k = 0; k < RD; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
     }
     ++sidx;
     // the next stage's weights must have landed; the halo slice issued after them may still be
@@ -564,6 +581,26 @@ struct H3P {
   const unsigned* ax1;
 };
 
+// byte offsets (relative to an image base) of the two transposed 4-row reads that give lane
+// `lane` its 8 k-values of column col0 + (lane & 31) -- tr_frag's addressing, hoisted out of the loop
+template <int RB>
+__device__ __forceinline__ int2 tr_offsets(int col0, int lane) {
+  const int h = lane >> 5, q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = col0 + (lane & 16) + 4 * pp;
+  return make_int2(wx_off<RB>(8 * h + q, col >> 3) + 2 * (col & 7), wx_off<RB>(8 * h + 4 + q, col >> 3) + 2 * (col & 7));
+}
+// the fragment at LDS byte pointers p0 / p1 (a tr_offsets pair added to an image base; compile-time
+// parts of the base fold into the instructions' offset fields)
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ half8 tr_read(const lds_char* p0, const lds_char* p1) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)p0);
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)p1);
+  const v8i16 c = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(half8, c);
+}
+
 template <int RB>
 __device__ __forceinline__ int wx_swz(int row) { return (wx_off<RB>(row, 0) - row * RB) >> 4; }
 
@@ -575,9 +612,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
   constexpr int IMG_A = PS * RA, IMG_B = PS * RBB;       // one plane
   constexpr int STAGE = 2 * (IMG_A + IMG_B);
   constexpr int NA = 2 * IMG_A / 1024, NB = 2 * IMG_B / 1024;   // DMA wave-instructions per stage
-  constexpr int DPW = (NA + NB + NW - 1) / NW;
+  constexpr int DA = (NA + NW - 1) / NW, DB = (NB + NW - 1) / NW, DPW = DA + DB;   // DMA ops per wave per stage
   static_assert(IMG_A % 1024 == 0 && IMG_B % 1024 == 0, "images must be whole KiB");
   static_assert(PS % 16 == 0 && (NST - 2) * DPW <= 63, "stage geometry");
+  // (the per-issue coordinate advance wraps at most one image row and one image: PS < H * W)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   char* const sink = lds + NST * STAGE;
@@ -599,72 +637,73 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
   const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
   const size_t aplane = (size_t)p.P * p.Cout * 2, bplane = (size_t)p.P * p.Cin * 2;   // bytes
 
-  // this wave's DMA ops: op j is instruction w = wave + j*NW (A instructions first, then B)
-  int d_row[DPW], d_kind[DPW];            // kind: 0 = A, 1 = B, 2 = spare (sink)
-  unsigned d_base[DPW];                   // A: byte offset of (row 0 of the chunk, this lane's chunk)
-  int d_dy[DPW], d_dx[DPW], d_lds[DPW];
-  int d_y[DPW], d_x[DPW];
+  // this wave's DMA ops: A op j is A instruction wave + j*NW, B op j is B instruction wave + j*NW
+  // (past NA / NB: a spare zero-fill into the sink).  LDS destinations are wave-uniform; per lane: a
+  // running byte offset (advanced by one stage of pixels per issue) and, for B, the image
+  // coordinates of its pixel.
+  const int psy = PS / p.W, psx = PS - psy * p.W;       // one stage of pixels in image rows / columns
+  const unsigned astep = (unsigned)(PS * p.Cout * 2), bstep = (unsigned)(PS * p.Cin * 2);
+  int a_row[DA];
+  unsigned a_off[DA];
+  bool a_ok[DA];
 #pragma unroll
-  for (int j = 0; j < DPW; ++j) {
-    const int w = wave + j * NW;
-    d_kind[j] = 2; d_row[j] = 0; d_base[j] = 0; d_dy[j] = 0; d_dx[j] = 0; d_lds[j] = 0; d_y[j] = 0; d_x[j] = 0;
-    if (w < NA) {
-      const int pl = w / (NA / 2), idx = w - pl * (NA / 2);
-      const int byte = idx * 1024 + lane * 16;
-      const int row = byte / RA, slot = (byte - row * RA) >> 4;
-      const int ch = slot ^ wx_swz<RA>(row);
-      const int m = m0 + 8 * ch;
-      d_row[j] = row;
-      d_lds[j] = pl * IMG_A + idx * 1024;
-      d_kind[j] = m < p.Cout ? 0 : 2;
-      d_base[j] = (unsigned)(pl * aplane + (size_t)m * 2);
-    } else if (w < NA + NB) {
-      const int wb = w - NA;
-      const int pl = wb / (NB / 2), idx = wb - pl * (NB / 2);
-      const int byte = idx * 1024 + lane * 16;
-      const int row = byte / RBB, slot = (byte - row * RBB) >> 4;
-      const int ch = slot ^ wx_swz<RBB>(row);
-      const int k = n0 + 8 * ch;
-      d_row[j] = row;
-      d_lds[j] = 2 * IMG_A + pl * IMG_B + idx * 1024;
-      if (k < p.K) {
-        const int tap = k / p.Cin, c = k - tap * p.Cin;
-        const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
-        d_kind[j] = 1;
-        d_dy[j] = (ky - kc) * p.dil;
-        d_dx[j] = (kx - kc) * p.dil;
-        d_base[j] = (unsigned)(pl * bplane + (size_t)c * 2);
-      }
-      const int pix = pbeg + row, rem = pix % (p.H * p.W);
-      d_y[j] = rem / p.W;
-      d_x[j] = rem - d_y[j] * p.W;
-    } else {
-      d_lds[j] = 0;
-    }
+  for (int j = 0; j < DA; ++j) {
+    const int w = min(wave + j * NW, NA - 1);
+    const int pl = w / (NA / 2), idx = w - pl * (NA / 2);
+    const int byte = idx * 1024 + lane * 16;
+    const int row = byte / RA, slot = (byte - row * RA) >> 4;
+    const int m = m0 + 8 * (slot ^ wx_swz<RA>(row));
+    a_row[j] = row;
+    a_ok[j] = m < p.Cout && wave + j * NW < NA;
+    a_off[j] = (unsigned)(pl * aplane + ((size_t)(pbeg + row) * p.Cout + m) * 2);
   }
-  // issue stage `s` into ring slot s % NST (always DPW ops per wave; past the chunk: zero fill)
-  auto issue = [&](int s) {
-    char* st = lds + (s % NST) * STAGE;
-    const int pbase = pbeg + s * PS;
+  int b_row[DB], b_dy[DB], b_dx[DB], b_y[DB], b_x[DB];
+  unsigned b_off[DB];
+  bool b_ok[DB];
 #pragma unroll
-    for (int j = 0; j < DPW; ++j) {
-      const int pix = pbase + d_row[j];
-      const bool in = s < nsteps && pix < pend;
-      if (d_kind[j] == 0) {
-        const unsigned off = in ? d_base[j] + (unsigned)pix * (unsigned)(p.Cout * 2) : OOB;
-        dma16(rsa, off, lds_addr_of(st + d_lds[j]));
-      } else if (d_kind[j] == 1) {
-        const int iy = d_y[j] + d_dy[j], ix = d_x[j] + d_dx[j];
-        const bool ok = in && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        const unsigned off = ok ? d_base[j] + (unsigned)(pix + d_dy[j] * p.W + d_dx[j]) * (unsigned)(p.Cin * 2) : OOB;
-        dma16(rsb, off, lds_addr_of(st + d_lds[j]));
-        int x = d_x[j] + PS, y = d_y[j];   // image coordinates of the next stage's pixel
-        while (x >= p.W) { x -= p.W; ++y; }
-        while (y >= p.H) y -= p.H;
-        d_x[j] = x; d_y[j] = y;
-      } else {
-        dma16(rsa, OOB, lds_addr_of(d_lds[j] ? st + d_lds[j] : sink));
-      }
+  for (int j = 0; j < DB; ++j) {
+    const int w = min(wave + j * NW, NB - 1);
+    const int pl = w / (NB / 2), idx = w - pl * (NB / 2);
+    const int byte = idx * 1024 + lane * 16;
+    const int row = byte / RBB, slot = (byte - row * RBB) >> 4;
+    const int k = n0 + 8 * (slot ^ wx_swz<RBB>(row));
+    b_row[j] = row;
+    b_ok[j] = k < p.K && wave + j * NW < NB;
+    const int tap = k < p.K ? k / p.Cin : 0, c = k - tap * p.Cin;
+    const int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+    b_dy[j] = (ky - kc) * p.dil;
+    b_dx[j] = (kx - kc) * p.dil;
+    const long long src = (long long)(pbeg + row) + b_dy[j] * p.W + b_dx[j];   // may be < 0 (then unused)
+    b_off[j] = (unsigned)((long long)pl * (long long)bplane + (src * p.Cin + c) * 2);
+    const int rem = (pbeg + row) % (p.H * p.W);
+    b_y[j] = rem / p.W;
+    b_x[j] = rem - b_y[j] * p.W;
+  }
+  // issue stage `s` into ring slot s % NST (always DA + DB ops per wave; past the chunk: zero fill)
+  auto issue = [&](int s, int slot) {
+    char* st = lds + slot * STAGE;
+    const int pbase = pbeg + s * PS;
+    const bool full = pbase + PS <= pend;                // wave-uniform: no row of the stage is past the chunk
+#pragma unroll
+    for (int j = 0; j < DA; ++j) {
+      const int w = wave + j * NW;
+      const int pl = w / (NA / 2), idx = w - pl * (NA / 2);
+      const bool in = full || pbase + a_row[j] < pend;
+      dma16(rsa, (a_ok[j] && in) ? a_off[j] : OOB, lds_addr_of(w < NA ? st + pl * IMG_A + idx * 1024 : sink));
+      a_off[j] += astep;
+    }
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      const int w = wave + j * NW;
+      const int pl = w / (NB / 2), idx = w - pl * (NB / 2);
+      const bool ok = b_ok[j] && (full || pbase + b_row[j] < pend) && (unsigned)(b_y[j] + b_dy[j]) < (unsigned)p.H &&
+                      (unsigned)(b_x[j] + b_dx[j]) < (unsigned)p.W;
+      dma16(rsb, ok ? b_off[j] : OOB, lds_addr_of(w < NB ? st + 2 * IMG_A + pl * IMG_B + idx * 1024 : sink));
+      b_off[j] += bstep;
+      int x = b_x[j] + psx, y = b_y[j] + psy;   // image coordinates of the next stage's pixel
+      if (x >= p.W) { x -= p.W; ++y; }
+      if (y >= p.H) y -= p.H;
+      b_x[j] = x; b_y[j] = y;
     }
   };
 
@@ -682,26 +721,40 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   const int wm0 = wmi * TM, wn0 = wni * TN;
 
+  int2 oa[TI], ob[TJ];
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s) issue(s);
-  auto stage = [&](int s, auto fresh_tag) {
+  for (int i = 0; i < TI; ++i) oa[i] = tr_offsets<RA>(wm0 + 32 * i, lane);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) ob[j] = tr_offsets<RBB>(wn0 + 32 * j, lane);
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s, s);
+  // stage s lives in ring slot s % NST; the stage loop is unrolled by NST so the slot (and with
+  // it every LDS address offset) is a compile-time constant
+  auto stage = [&](int s, auto fresh_tag, auto slot_tag) {
     constexpr bool FRESH = decltype(fresh_tag)::value;
+    constexpr int SLOT = decltype(slot_tag)::value;
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DPW) : "memory");
     __syncthreads();
-    issue(s + NST - 1);
-    const char* st = lds + (s % NST) * STAGE;
+    issue(s + NST - 1, (SLOT + NST - 1) % NST);
+    const lds_char* sb = (const lds_char*)(uintptr_t)lds_addr_of(lds) + SLOT * STAGE;
+    const lds_char* va[TI][2];   // this stage's per-lane fragment addresses (+ immediates below)
+    const lds_char* vb[TJ][2];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) { va[i][0] = sb + oa[i].x; va[i][1] = sb + oa[i].y; }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) { vb[j][0] = sb + 2 * IMG_A + ob[j].x; vb[j][1] = sb + 2 * IMG_A + ob[j].y; }
 #pragma unroll
     for (int kk = 0; kk < PS / 16; ++kk) {
       half8 ah[TI], al[TI];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        ah[i] = tr_frag<half8, RA>(st + kk * 16 * RA, wm0 + 32 * i, lane);
-        al[i] = tr_frag<half8, RA>(st + IMG_A + kk * 16 * RA, wm0 + 32 * i, lane);
+        ah[i] = tr_read(va[i][0] + kk * 16 * RA, va[i][1] + kk * 16 * RA);
+        al[i] = tr_read(va[i][0] + IMG_A + kk * 16 * RA, va[i][1] + IMG_A + kk * 16 * RA);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const half8 bh = tr_frag<half8, RBB>(st + 2 * IMG_A + kk * 16 * RBB, wn0 + 32 * j, lane);
-        const half8 bl = tr_frag<half8, RBB>(st + 2 * IMG_A + IMG_B + kk * 16 * RBB, wn0 + 32 * j, lane);
+        const half8 bh = tr_read(vb[j][0] + kk * 16 * RBB, vb[j][1] + kk * 16 * RBB);
+        const half8 bl = tr_read(vb[j][0] + IMG_B + kk * 16 * RBB, vb[j][1] + IMG_B + kk * 16 * RBB);
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           floatx16 c0;
@@ -715,11 +768,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
       }
     }
   };
-  for (int s = 0; s < nsteps; s += HP) {
-    stage(s, std::true_type{});
-#pragma unroll
-    for (int h2 = 1; h2 < HP; ++h2)
-      if (s + h2 < nsteps) stage(s + h2, std::false_type{});
+  static_assert(HP == NST && NST == 3, "one partial chain per ring revolution (3 stages)");
+  for (int s = 0; s < nsteps; s += 3) {
+    stage(s, std::true_type{}, std::integral_constant<int, 0>{});
+    if (s + 1 < nsteps) stage(s + 1, std::false_type{}, std::integral_constant<int, 1>{});
+    if (s + 2 < nsteps) stage(s + 2, std::false_type{}, std::integral_constant<int, 2>{});
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -868,7 +921,7 @@ static int launch_h3p(const WgradParams& p, const H3P& q, hipStream_t st) {
   constexpr int PS = 32, NST = 3;
   const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
   const size_t lds = (size_t)NST * 2 * PS * 2 * (BM + BN) + 1024;
-  hipLaunchKernelGGL((conv_wgrad_h3p_kernel<BM, BN, WM, WN, PS, NST, 4>), dim3(nb), dim3(WM * WN * 64), lds, st, p, q);
+  hipLaunchKernelGGL((conv_wgrad_h3p_kernel<BM, BN, WM, WN, PS, NST, 3>), dim3(nb), dim3(WM * WN * 64), lds, st, p, q);
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p");
   return 0;
 }
