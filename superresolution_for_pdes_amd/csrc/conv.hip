@@ -1709,9 +1709,8 @@ static bool wgrad_v2_ok(const WgradParams& p) {
 
 static void wgrad_tiles(int cout, int K, int* bm, int* bn) {
   if (cout >= 128) { *bm = 128; *bn = 128; }
-  else if (cout >= 64) { *bm = 64; *bn = 256; }
+  else if (cout >= 64) { *bm = 64; *bn = K <= 64 ? 64 : 256; }   // K <= 64: enc1.conv1 (3 -> 4 channels)
   else { *bm = 32; *bn = 256; }
-  (void)K;
 }
 
 static void wgrad_split(int P, int cout, int K, int* chunk, int* splits) {
@@ -1916,8 +1915,8 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
   int bm, bn, rc;
   wgrad_tiles(cout, p.K, &bm, &bn);
   if (amax_dy) {
-    SRPDE_CHECK_ARG(srpde_conv_x6_supported(c0, c1, cout) && wgrad_v2_ok(p) && amax0 && (c1 == 0 || amax1),
-                    "srpde_conv_wgrad_h3: needs c0, c1, cout multiples of 32 and the amax words (c0=%d c1=%d cout=%d)",
+    SRPDE_CHECK_ARG(c0 % 32 == 0 && c1 % 32 == 0 && cout % 16 == 0 && wgrad_v2_ok(p) && amax0 && (c1 == 0 || amax1),
+                    "srpde_conv_wgrad_h3: needs c0, c1 multiples of 32, cout of 16 and the amax words (c0=%d c1=%d cout=%d)",
                     c0, c1, cout);
     rc = launch_wgrad_h3(p, amax_dy, amax0, amax1, stream);
   } else if (x6) {
@@ -1933,7 +1932,7 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
     else rc = launch_wgrad_v2<32, 256, 1, 4>(p, stream);
   } else {
     if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream);
-    else if (bm == 64) rc = launch_wgrad<64, 256, 1, 4>(p, stream);
+    else if (bm == 64) rc = bn == 64 ? launch_wgrad<64, 64, 2, 2>(p, stream) : launch_wgrad<64, 256, 1, 4>(p, stream);
     else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
   }
   if (rc) return rc;

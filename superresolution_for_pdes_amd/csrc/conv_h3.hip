@@ -979,7 +979,9 @@ using namespace srpde;
 extern "C" {
 
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
-  if (!(ksize == 3 && c0 % 32 == 0 && c1 % 32 == 0 && cout % 32 == 0 && c0 + c1 > 0 && w > 0 && dil >= 1)) return 0;
+  // cout % 16: a 16-channel output (out_conv2) runs on the 32-column tile with the weight rows past
+  // Cout zero-filled by the DMA range check
+  if (!(ksize == 3 && c0 % 32 == 0 && c1 % 32 == 0 && cout % 16 == 0 && c0 + c1 > 0 && w > 0 && dil >= 1)) return 0;
   const int bn = h3_bn(h3_cfg(cout));
   const int arows = h3_arows(w, dil);
   return (arows <= 512 && h3_lds(bn, arows) <= 160 * 1024) ? 1 : 0;

@@ -76,9 +76,9 @@ def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
     wd = empty(cout * taps * cin_pad, device=w.device) if want_dgrad else None
     call("srpde_pack_conv_weights", w.data_ptr(), _p(wf), _p(wd), cout, cin_pad, cin_real, kh, stream_ptr())
     if _CONV_MATH == "h3" and kh == 3:
-        if wf is not None and cin_pad % 32 == 0 and cout % 32 == 0:
+        if wf is not None and cin_pad % 32 == 0 and cout % 16 == 0:
             wf.h3 = split_weights_h3(wf, cout)
-        if wd is not None and cin_pad % 32 == 0 and cout % 32 == 0:
+        if wd is not None and cin_pad % 16 == 0 and cout % 32 == 0:
             wd.h3 = split_weights_h3(wd, cin_pad)
     if _CONV_MATH == "x6":
         if wf is not None and query("srpde_conv_x6_supported", cin_pad, 0, cout):
@@ -215,7 +215,7 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cin_real = dw.shape[1]
     ws_bytes = int(query("srpde_conv_wgrad_workspace_size", n, h, w, cout, cin, ksize))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dy.device)
-    if _CONV_MATH == "h3" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
+    if _CONV_MATH == "h3" and x0.shape[1] % 32 == 0 and c1 % 32 == 0 and cout % 16 == 0 and ksize == 3:
         a1 = amax_of(x1) if x1 is not None else None
         call("srpde_conv_wgrad_h3", pdy, lddy, amax_of(dy).data_ptr(), p0, x0.shape[1], ld0, amax_of(x0).data_ptr(),
              p1, c1, ld1, _p(a1), dw.data_ptr(), cin_real, int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(),
