@@ -246,15 +246,16 @@ def test_attention(c, gc, h):
     b2 = torch.randn(c, generator=g) * 0.1
     wg = torch.randn(1, gc, generator=g) * 0.1
     bg = torch.randn(1, generator=g) * 0.1
-    ts = [t.clone().requires_grad_(True) for t in (x, gt, w1, b1, w2, b2, wg, bg)]
+    # reference in fp64: fp32 CPU sums vary with the host's thread count at the 1e-5 level
+    ts = [t.double().requires_grad_(True) for t in (x, gt, w1, b1, w2, b2, wg, bg)]
     xv, gv, w1v, b1v, w2v, b2v, wgv, bgv = ts
     m = xv.mean(dim=(2, 3), keepdim=True)
     hh = F.relu(F.conv2d(m, w1v[:, :, None, None], b1v))
     ca = torch.sigmoid(F.conv2d(hh, w2v[:, :, None, None], b2v))
     sa = torch.sigmoid(F.conv2d(gv, wgv[:, :, None, None], bgv))
     ref = xv * ca * sa
-    dout = torch.randn_like(ref)
-    ref.backward(dout)
+    dout = torch.randn(ref.shape, generator=g)
+    ref.backward(dout.double())
     d = {k: v.to(DEV) for k, v in dict(w1=w1, b1=b1, w2=w2, b2=b2, wg=wg, bg=bg).items()}
     xr, gr = rows(x).to(DEV), rows(gt).to(DEV)
     out, saved = H.att_fwd(xr, gr, n, h * h, d["w1"], d["b1"], d["w2"], d["b2"], d["wg"], d["bg"])
