@@ -68,15 +68,20 @@ struct H3Args {
 
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL>
+// TPS: taps per stage (one barrier per stage; the weight stage holds TPS taps).
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per stage (16 rows x 64 B)
   constexpr int BPW = (BTOT + NW - 1) / NW;
-  constexpr int BP_BYTES = BN * 64;        // one fp16 plane of the B tile
-  constexpr int B_STAGE = 2 * BP_BYTES;
+  constexpr int BP_BYTES = BN * 64;        // one fp16 plane of the B tile (one tap)
+  constexpr int B_TAP = 2 * BP_BYTES;      // hi + lo planes of one tap
+  constexpr int B_STAGE = TPS * B_TAP;
+  constexpr int NS = (9 + TPS - 1) / TPS;  // stages per channel chunk
+  constexpr int AQ = (8 + NS - 2) / (NS - 1);   // halo-slice DMAs per wave in stages 0..NS-2 (8 per wave per chunk)
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
+  static_assert(TPS >= 1 && TPS <= 3, "taps per stage");
   // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its hi / lo fp16 planes (64-B rows)
   //      | B = two weight stages | 64 zero bytes (the padding row) | 1 KiB DMA sink
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -173,15 +178,21 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
     const unsigned off = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
     dma16(rs, off, lds_addr_of(real ? fbuf + q * 1024 : sink));
   };
-  auto issue_b = [&](int ch, int tap, int buf) {
-    const int k0 = tap * p.Cin + ch * BK2;
-    char* bbase = bbuf0 + buf * B_STAGE;
+  auto issue_b = [&](int ch, int st, int buf) {   // the TPS taps of stage `st` of chunk `ch`
 #pragma unroll
-    for (int j = 0; j < BPW; ++j) {
-      const int q = wave + j * NW;
-      if (q < BTOT) {
-        const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
-        dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+    for (int u = 0; u < TPS; ++u) {
+      const int tap = st * TPS + u;
+      if (tap < 9) {
+        const int k0 = tap * p.Cin + ch * BK2;
+        char* bbase = bbuf0 + buf * B_STAGE + u * B_TAP;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) {
+          const int q = wave + j * NW;
+          if (q < BTOT) {
+            const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+            dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+          }
+        }
       }
     }
   };
@@ -232,19 +243,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
   __syncthreads();
 
   int sidx = 0;      // stage counter (B buffer parity)
-  auto stage = [&](int ch, auto tap_tag) {
+  // one tap: read its fragments up front (both 16-k groups), then the MFMAs (the second group's
+  // reads complete under the first group's MFMAs)
+  auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
     constexpr int KY = TAP / 3, KX = TAP % 3;
-    // prefetch: next weight stage, one slice of the next chunk's halo tile (F is free: the
-    // current chunk was converted to S before its first stage)
-    if (TAP < 8) issue_b(ch, TAP + 1, (sidx + 1) & 1);
-    else if (ch + 1 < c_end) issue_b(ch + 1, 0, (sidx + 1) & 1);
-    const bool more = ch + 1 < c_end;
-    if (TAP < 8 && more) issue_a(ch + 1, wave + TAP * NW);   // slices 0..7 of the next halo tile
     const int toff = p.sign > 0 ? (KY * p.W + KX) * p.dil : ((2 - KY) * p.W + (2 - KX)) * p.dil;
-    const char* b = bbuf0 + (sidx & 1) * B_STAGE;
-    // every fragment of the stage is read up front (both 16-k groups), then the MFMAs run: the
-    // second group's reads complete under the first group's MFMAs
     constexpr int NG = BK2 / 16;
     half8 ah[NG][TI], al[NG][TI], bh[NG][TJ], bl[NG][TJ];
 #pragma unroll
@@ -281,35 +285,50 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
         }
     // schedule: the first group's reads, then one MFMA per second-group read, then the rest
     // (without this the scheduler parks each read right before its MFMA and exposes its latency)
-    {
-      constexpr int RD = 2 * (TI + TJ), MF = 3 * TI * TJ;
-      __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+    constexpr int RD = 2 * (TI + TJ), MF = 3 * TI * TJ;
+    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
 #pragma unroll
-      for (int k = 0; k < RD; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
+    for (int k = 0; k < RD; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
+  };
+  auto stage = [&](int ch, auto st_tag) {
+    constexpr int ST = decltype(st_tag)::value;
+    // prefetch: the next weight stage, then AQ slices of the next chunk's halo tile (F is free:
+    // the current chunk was converted to S before its first stage)
+    const bool more = ch + 1 < c_end;
+    const bool dma = !(p.dbg & 1);   // diagnostics (SRPDE_CONV_DBG, results wrong): 1 = no DMA in the loop
+    if (dma && ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
+    else if (dma && more) issue_b(ch + 1, 0, (sidx + 1) & 1);
+    if (dma && ST < NS - 1 && more) {
+#pragma unroll
+      for (int u = 0; u < AQ; ++u) issue_a(ch + 1, wave + (ST * AQ + u) * NW);
+    }
+    const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+    tap_body(b, std::integral_constant<int, ST * TPS>{});
+    if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
+    if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
     ++sidx;
-    // the next stage's weights must have landed; the halo slice issued after them may still be
-    // in flight (it is waited for by the next stage's count, long before the chunk ends)
-    if (TAP < 8 && more && h.relax)
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    // the next stage's weights must have landed; the halo slices issued after them may still be
+    // in flight (they are waited for by the next stage's count, long before the chunk ends)
+    if (ST < NS - 1 && more && h.relax)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (!(p.dbg & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
   };
   for (int ch = c_beg; ch < c_end; ++ch) {
     stage(ch, std::integral_constant<int, 0>{});
-    stage(ch, std::integral_constant<int, 1>{});
-    stage(ch, std::integral_constant<int, 2>{});
-    stage(ch, std::integral_constant<int, 3>{});
-    stage(ch, std::integral_constant<int, 4>{});
-    stage(ch, std::integral_constant<int, 5>{});
-    stage(ch, std::integral_constant<int, 6>{});
-    stage(ch, std::integral_constant<int, 7>{});
-    stage(ch, std::integral_constant<int, 8>{});
+    if constexpr (NS > 1) stage(ch, std::integral_constant<int, 1>{});
+    if constexpr (NS > 2) stage(ch, std::integral_constant<int, 2>{});
+    if constexpr (NS > 3) stage(ch, std::integral_constant<int, 3>{});
+    if constexpr (NS > 4) stage(ch, std::integral_constant<int, 4>{});
+    if constexpr (NS > 5) stage(ch, std::integral_constant<int, 5>{});
+    if constexpr (NS > 6) stage(ch, std::integral_constant<int, 6>{});
+    if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
+    if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
     // two-level accumulation: one partial chain per channel chunk (9 taps x 32 channels)
     if constexpr (TWO_LEVEL) {
 #pragma unroll
@@ -317,8 +336,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
     }
-    if (ch + 1 < c_end) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
-      convert(ch + 1);
+    if (ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
+      convert(ch + 1);                      // (diagnostics: 4 = no per-chunk convert)
       __syncthreads();
     }
   }
@@ -332,6 +351,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * iw;
+  }
+  if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] + acc[i][j][15];
+    if (t == 123.f) p.y[tid] = t;
+    return;
   }
   x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem);
 }
@@ -851,14 +879,26 @@ constexpr int H3_BM = 256;
 
 static int h3_arows(int w, int dil) { return (H3_BM + 2 * (w + 1) * dil + 7) / 8 * 8; }
 
-static size_t h3_lds(int bn, int arows) { return (size_t)arows * (ROW2 + 128) + (size_t)2 * 2 * bn * 64 + 64 + 1024; }
+static size_t h3_lds(int bn, int arows, int tps = 1) {
+  return (size_t)arows * (ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
+}
+// taps per stage: the most (<= SRPDE_H3_TPS, default 2) whose weight double-buffer fits in LDS
+static int h3_tps(int bn, int arows) {
+  static const int want = [] {
+    const char* e = getenv("SRPDE_H3_TPS");   // tuning/diagnostics
+    return e ? std::max(1, std::min(3, atoi(e))) : 2;
+  }();
+  int t = want;
+  while (t > 1 && h3_lds(bn, arows, t) > 160 * 1024) --t;
+  return t;
+}
 
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
 static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int NT = WM * WN * 64;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
   const int T = nbm * nbn;
-  const size_t lds = h3_lds(BN, h.arows);
+  const size_t lds = h3_lds(BN, h.arows, TPS);
   static int slots = [&] {
     int dev = 0, cus = 0;
     hipGetDevice(&dev);
@@ -866,11 +906,13 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
     return std::max(1, cus);      // one workgroup per CU (LDS)
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
+  p.dbg = dbg;   // diagnostics only (timing experiments; results wrong when non-zero)
   const int nch = p.Cin / BK2;
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL>), dim3(grid), dim3(NT), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS>), dim3(grid), dim3(NT), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -1045,11 +1087,17 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   a.relax = relax;
   a.xsplit = static_cast<_Float16*>(xsplit_out);
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
+  const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
+#define H3_LAUNCH(BN_, SRB_)                                                                  \
+  (tps >= 3 ? launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 3>(p, a, stream, workspace, ws_bytes) \
+   : tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 2>(p, a, stream, workspace, ws_bytes) \
+              : launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 1>(p, a, stream, workspace, ws_bytes))
   switch (h3_cfg(cout)) {
-    case 1: return launch_fwd_h3<256, 128, 8, 1, 128, true>(p, a, stream, workspace, ws_bytes);
-    case 2: return launch_fwd_h3<256, 64, 8, 1, 256, true>(p, a, stream, workspace, ws_bytes);
-    default: return launch_fwd_h3<256, 32, 8, 1, 256, true>(p, a, stream, workspace, ws_bytes);
+    case 1: return H3_LAUNCH(128, 128);
+    case 2: return H3_LAUNCH(64, 256);
+    default: return H3_LAUNCH(32, 256);
   }
+#undef H3_LAUNCH
 }
 
 }  // extern "C"
