@@ -204,6 +204,121 @@ __global__ void upsample_bwd_kernel(const float* __restrict__ dout, int lddo, fl
   }
 }
 
+// ---------------- pixel-blocked variants (C/4 a power of two <= 256) ----------------
+// block = (C/4 channel quads) x (256 / (C/4) pixels): the channel quad is threadIdx.x and every
+// thread derives its pixel once with 32-bit index math (the grid-stride kernels above divide a
+// 64-bit element index per float4, which costs more than the memory access at these sizes).
+__device__ __forceinline__ unsigned px_index() { return blockIdx.x * blockDim.y + threadIdx.y; }
+
+__global__ __launch_bounds__(256) void maxpool2_fwd_px_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out,
+                                                              int ldo, unsigned npix, int H, int W) {
+  const unsigned q = px_index();
+  if (q >= npix) return;
+  const unsigned Wo = W >> 1, Ho = H >> 1;
+  const unsigned ox = q % Wo, t = q / Wo, oy = t % Ho, n = t / Ho;
+  const int c = threadIdx.x * 4;
+  const size_t p00 = ((size_t)n * H + 2 * oy) * W + 2 * ox;
+  const float4 a = *reinterpret_cast<const float4*>(x + p00 * ldx + c);
+  const float4 b = *reinterpret_cast<const float4*>(x + (p00 + 1) * ldx + c);
+  const float4 d = *reinterpret_cast<const float4*>(x + (p00 + W) * ldx + c);
+  const float4 f = *reinterpret_cast<const float4*>(x + (p00 + W + 1) * ldx + c);
+  float4 m;
+#define MX(X) { float v = a.X; if (b.X > v) v = b.X; if (d.X > v) v = d.X; if (f.X > v) v = f.X; m.X = v; }
+  MX(x) MX(y) MX(z) MX(w)
+#undef MX
+  *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = m;
+}
+
+__global__ __launch_bounds__(256) void maxpool2_bwd_px_kernel(const float* __restrict__ x, int ldx,
+                                                              const float* __restrict__ dout, int lddo,
+                                                              float* __restrict__ dx, int lddx, unsigned npix, int H,
+                                                              int W, int accumulate) {
+  const unsigned q = px_index();
+  if (q >= npix) return;
+  const unsigned Wo = W >> 1, Ho = H >> 1;
+  const unsigned ox = q % Wo, t = q / Wo, oy = t % Ho, n = t / Ho;
+  const int c = threadIdx.x * 4;
+  const size_t p0 = ((size_t)n * H + 2 * oy) * W + 2 * ox;
+  const size_t p[4] = {p0, p0 + 1, p0 + W, p0 + W + 1};
+  float4 v[4], o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(x + p[k] * ldx + c);
+  const float4 g = *reinterpret_cast<const float4*>(dout + (size_t)q * lddo + c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = accumulate ? *reinterpret_cast<const float4*>(dx + p[k] * lddx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#define ARG(X)                                                     \
+  {                                                                \
+    int am = 0; float mv = v[0].X;                                 \
+    if (v[1].X > mv) { mv = v[1].X; am = 1; }                      \
+    if (v[2].X > mv) { mv = v[2].X; am = 2; }                      \
+    if (v[3].X > mv) { mv = v[3].X; am = 3; }                      \
+    o[am].X += g.X;                                                \
+  }
+  ARG(x) ARG(y) ARG(z) ARG(w)
+#undef ARG
+#pragma unroll
+  for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(dx + p[k] * lddx + c) = o[k];
+}
+
+__global__ __launch_bounds__(256) void upsample_fwd_px_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out,
+                                                              int ldo, unsigned npix, int H, int W, int Ho, int Wo) {
+  const unsigned q = px_index();
+  if (q >= npix) return;
+  const unsigned ox = q % (unsigned)Wo, t = q / (unsigned)Wo, oy = t % (unsigned)Ho, n = t / (unsigned)Ho;
+  const int c = threadIdx.x * 4;
+  const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
+  const float* base = x + (size_t)n * H * W * ldx + c;
+  const float4 a = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i0) * ldx);
+  const float4 b = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i1) * ldx);
+  const float4 d = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i0) * ldx);
+  const float4 f = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i1) * ldx);
+  float4 o;
+#define UP(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
+  UP(x) UP(y) UP(z) UP(w)
+#undef UP
+  *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
+}
+
+__global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __restrict__ dout, int lddo,
+                                                              float* __restrict__ dx, int lddx, unsigned npix, int H,
+                                                              int W, int Ho, int Wo, int accumulate) {
+  const unsigned q = px_index();
+  if (q >= npix) return;
+  const unsigned ix = q % (unsigned)W, t = q / (unsigned)W, iy = t % (unsigned)H, n = t / (unsigned)H;
+  const int c = threadIdx.x * 4;
+  int oyi[8], oxi[8];
+  float wy[8], wx[8];
+  const int ny = gather_weights(iy, H, Ho, oyi, wy);
+  const int nx = gather_weights(ix, W, Wo, oxi, wx);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* base = dout + (size_t)n * Ho * Wo * lddo + c;
+  for (int a = 0; a < ny; ++a) {
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int b = 0; b < nx; ++b) {
+      const float4 g = *reinterpret_cast<const float4*>(base + (size_t)(oyi[a] * Wo + oxi[b]) * lddo);
+      r.x += wx[b] * g.x; r.y += wx[b] * g.y; r.z += wx[b] * g.z; r.w += wx[b] * g.w;
+    }
+    s.x += wy[a] * r.x; s.y += wy[a] * r.y; s.z += wy[a] * r.z; s.w += wy[a] * r.w;
+  }
+  float* o = dx + (size_t)q * lddx + c;
+  if (accumulate) {
+    const float4 old = *reinterpret_cast<const float4*>(o);
+    s.x += old.x; s.y += old.y; s.z += old.z; s.w += old.w;
+  }
+  *reinterpret_cast<float4*>(o) = s;
+}
+
+// launch geometry of the pixel-blocked kernels, or false when C/4 is not a power of two <= 256
+static bool px_geometry(long long npix, int c, dim3* grid, dim3* block) {
+  const int c4 = c / 4;
+  if (c % 4 != 0 || c4 < 1 || c4 > 256 || (c4 & (c4 - 1)) != 0 || npix >= (1LL << 31)) return false;
+  const int py = 256 / c4;
+  *block = dim3(c4, py);
+  *grid = dim3((unsigned)((npix + py - 1) / py));
+  return true;
+}
+
 // ------------------------------- attention gate ----------------------------------
 // channel branch: m = mean_hw(x); h = relu(W1 m + b1); ca = sigmoid(W2 h + b2)  (models.py:106-112)
 // one block per sample
@@ -626,6 +741,12 @@ int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w,
 int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int c,
                          hipStream_t stream) {
   SRPDE_CHECK_ARG(x && out && c % 4 == 0 && h % 2 == 0 && w % 2 == 0, "srpde_maxpool2x2_fwd: bad args");
+  dim3 g, b;
+  if (px_geometry((long long)n * (h / 2) * (w / 2), c, &g, &b)) {
+    hipLaunchKernelGGL(maxpool2_fwd_px_kernel, g, b, 0, stream, x, ldx, out, ldo, (unsigned)(n * (h / 2) * (w / 2)), h, w);
+    SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_fwd");
+    return 0;
+  }
   hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for((long long)n * (h / 2) * (w / 2) * (c / 4))), dim3(256), 0,
                      stream, x, ldx, out, ldo, n, h, w, c);
   SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_fwd");
@@ -635,6 +756,13 @@ int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, in
 int srpde_maxpool2x2_bwd(const float* x, int ldx, const float* dout, int lddo, float* dx, int lddx, int n, int h,
                          int w, int c, int accumulate, hipStream_t stream) {
   SRPDE_CHECK_ARG(x && dout && dx && c % 4 == 0 && h % 2 == 0 && w % 2 == 0, "srpde_maxpool2x2_bwd: bad args");
+  dim3 g, b;
+  if (px_geometry((long long)n * (h / 2) * (w / 2), c, &g, &b)) {
+    hipLaunchKernelGGL(maxpool2_bwd_px_kernel, g, b, 0, stream, x, ldx, dout, lddo, dx, lddx,
+                       (unsigned)(n * (h / 2) * (w / 2)), h, w, accumulate);
+    SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_bwd");
+    return 0;
+  }
   hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)n * (h / 2) * (w / 2) * (c / 4))), dim3(256), 0,
                      stream, x, ldx, dout, lddo, dx, lddx, n, h, w, c, accumulate);
   SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_bwd");
@@ -650,6 +778,12 @@ int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, in
     SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
     return 0;
   }
+  dim3 g, b;
+  if (px_geometry((long long)n * ho * wo, c, &g, &b)) {
+    hipLaunchKernelGGL(upsample_fwd_px_kernel, g, b, 0, stream, x, ldx, out, ldo, (unsigned)(n * ho * wo), h, w, ho, wo);
+    SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
+    return 0;
+  }
   hipLaunchKernelGGL(upsample_fwd_kernel, dim3(grid_for((long long)n * ho * wo * (c / 4))), dim3(256), 0, stream, x,
                      ldx, out, ldo, n, h, w, ho, wo, c);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
@@ -659,6 +793,13 @@ int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, in
 int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
                                 int wo, int c, int accumulate, hipStream_t stream) {
   SRPDE_CHECK_ARG(dout && dx && c % 4 == 0 && ho >= h && wo >= w, "srpde_upsample_bilinear_bwd: bad args");
+  dim3 g, b;
+  if (px_geometry((long long)n * h * w, c, &g, &b)) {
+    hipLaunchKernelGGL(upsample_bwd_px_kernel, g, b, 0, stream, dout, lddo, dx, lddx, (unsigned)(n * h * w), h, w, ho,
+                       wo, accumulate);
+    SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd");
+    return 0;
+  }
   hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for((long long)n * h * w * (c / 4))), dim3(256), 0, stream, dout,
                      lddo, dx, lddx, n, h, w, ho, wo, c, accumulate);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd");
