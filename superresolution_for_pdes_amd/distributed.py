@@ -109,15 +109,15 @@ class DataParallel(torch.nn.Module):
 
     @torch.no_grad()
     def _sync_buffers(self):
-        bufs = [b for b in self.module.buffers()]
-        if not bufs:
-            return
-        flat = torch.cat([b.reshape(-1).to(torch.float64) for b in bufs])
-        dist.broadcast(flat, 0, group=self.pg)
-        off = 0
-        for b in bufs:
-            b.copy_(flat[off:off + b.numel()].view_as(b).to(b.dtype))
-            off += b.numel()
+        # one broadcast per dtype (fp32 running stats, int64 batch counters), multi-tensor copies
+        by_dtype = {}
+        for b in self.module.buffers():
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for bufs in by_dtype.values():
+            flat = torch.cat([b.reshape(-1) for b in bufs])
+            dist.broadcast(flat, 0, group=self.pg)
+            parts = torch.split(flat, [b.numel() for b in bufs])
+            torch._foreach_copy_(bufs, [s.view_as(b) for s, b in zip(parts, bufs)])
 
     def forward(self, x):
         if self.broadcast_buffers and self.module.training and dist.get_world_size(self.pg) > 1:
