@@ -86,6 +86,10 @@ int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const v
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
+/* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]
+ * weights: desc = device int64 [nlayers][9] = {w, cout, cin_real, cin_pad, planes_f, exp_f,
+ * planes_d, exp_d, first row}; a layer owns cout forward rows then cin_pad dgrad rows */
+int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows, hipStream_t stream);
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,

@@ -850,6 +850,55 @@ __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __re
   if (lane == 0) wexp[row] = e;
 }
 
+// All conv layers' h3 weight planes in one launch, straight from torch's [Cout][Cin][3][3]:
+// forward rows  n in [0, Cout):   k = tap*Cin_pad + c  ->  W[n][c][tap]   (c >= Cin_real: 0)
+// dgrad rows    c in [0, Cin_pad): k = tap*Cout + n    ->  W[n][c][tap]
+// one wave per row: max|row| -> power-of-two scale -> hi / lo fp16 planes.  desc (device int64,
+// H3W_DESC per layer): w, cout, cin_real, cin_pad, planes_f, exp_f, planes_d, exp_d, row_begin
+// (rows of a layer: Cout forward rows then Cin_pad dgrad rows; planes_f / planes_d may be 0).
+constexpr int H3W_DESC = 9;
+
+__global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long* __restrict__ desc, int nlayers,
+                                                                 int total_rows) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= total_rows) return;
+  int l = 0;
+  while (l + 1 < nlayers && desc[(l + 1) * H3W_DESC + 8] <= row) ++l;
+  const long long* d = desc + l * H3W_DESC;
+  const float* w = reinterpret_cast<const float*>(d[0]);
+  const int cout = (int)d[1], cin_real = (int)d[2], cin_pad = (int)d[3];
+  int r = row - (int)d[8];
+  const bool fwd = r < cout;
+  if (!fwd) r -= cout;
+  _Float16* planes = reinterpret_cast<_Float16*>(fwd ? d[4] : d[6]);
+  int* wexp = reinterpret_cast<int*>(fwd ? d[5] : d[7]);
+  if (planes == nullptr) return;
+  const int inner = fwd ? cin_pad : cout;          // k = tap * inner + i
+  const int K = 9 * inner;
+  const int rows = fwd ? cout : cin_pad;
+  auto val = [&](int k) -> float {
+    const int tap = k / inner, i = k - tap * inner;
+    const int n = fwd ? r : i, c = fwd ? i : r;
+    return c < cin_real ? w[((size_t)n * cin_real + c) * 9 + tap] : 0.f;
+  };
+  float m = 0.f;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(val(k)));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int e = h3_exp(__float_as_uint(m));
+  const float sc = exp2i(e);
+  _Float16* hi = planes + (size_t)r * K;
+  _Float16* lo = planes + (size_t)rows * K + (size_t)r * K;
+  for (int k = lane; k < K; k += 64) {
+    const float v = val(k) * sc;
+    const _Float16 hv = (_Float16)v;
+    hi[k] = hv;
+    lo[k] = (_Float16)(v - (float)hv);
+  }
+  if (lane == 0) wexp[r] = e;
+}
+
 // *amax = max(*amax, max|x|) over a [P][c] view (float bits; caller zeroes *amax)
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int ldx, int c, long long P,
                                                      unsigned* amax) {
@@ -1034,6 +1083,14 @@ int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, in
   hipLaunchKernelGGL(split_weights_h3_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, stream, w,
                      static_cast<_Float16*>(planes), wexp, rows, K);
   SRPDE_LAUNCH_CHECK("srpde_split_weights_h3");
+  return 0;
+}
+
+int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows, hipStream_t stream) {
+  SRPDE_CHECK_ARG(desc && nlayers > 0 && total_rows > 0, "srpde_prepare_weights_h3: bad arguments");
+  hipLaunchKernelGGL(prepare_weights_h3_kernel, dim3(ceil_div(total_rows, 4)), dim3(256), 0, stream, desc, nlayers,
+                     total_rows);
+  SRPDE_LAUNCH_CHECK("srpde_prepare_weights_h3");
   return 0;
 }
 

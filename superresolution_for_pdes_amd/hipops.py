@@ -66,6 +66,11 @@ def split_weights_h3(wpack, rows):
     return planes, wexp
 
 
+def prepare_weights_h3(desc, nlayers, total_rows):
+    """Batched h3 weight split of every conv layer (see unet_exec.prepare_h3_weights)."""
+    call("srpde_prepare_weights_h3", desc.data_ptr(), nlayers, total_rows, stream_ptr())
+
+
 def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
     """Packed fp32 weights (fwd [Cout][tap][Cin], dgrad [Cin][tap][Cout]); in x6 mode each
     packed tensor carries its bf16 split planes as ``.x6``, in h3 mode its fp16 planes and

@@ -70,12 +70,69 @@ def _conv_launch(conv, *args):
     sink.append((a, b))
 
 
+class _Planes:
+    """Holder of one packed weight tensor's h3 split: ``.h3 = (planes, row exponents)``."""
+    __slots__ = ("h3",)
+
+    def __init__(self, planes, wexp):
+        self.h3 = (planes, wexp)
+
+
+def prepare_h3_weights(m):
+    """Split every 3x3 conv's weights into h3 planes (forward and dgrad packings) with ONE
+    launch per step (srpde_prepare_weights_h3), instead of a pack + split per layer and pass.
+    Buffers and the layer table persist on the model; they are rebuilt if a weight moves."""
+    if H.conv_math() != "h3":
+        return
+    convs = [mod for mod in m.modules() if isinstance(mod, torch.nn.Conv2d) and mod.kernel_size == (3, 3)]
+    sig = tuple(c.weight.data_ptr() for c in convs)
+    cache = getattr(m, "_srpde_h3w", None)
+    if cache is None or cache[0] != sig:
+        dev = convs[0].weight.device
+        rows, desc, keep = 0, [], []
+        for c in convs:
+            cout, cin = c.out_channels, c.in_channels
+            pf = ef = pd = ed = None
+            if cin % 32 == 0 and cout % 16 == 0:
+                pf = torch.empty(2, cout * 9 * cin, dtype=torch.float16, device=dev)
+                ef = torch.empty(cout, dtype=torch.int32, device=dev)
+            if cout % 32 == 0 and cin % 16 == 0:
+                pd = torch.empty(2, cin * 9 * cout, dtype=torch.float16, device=dev)
+                ed = torch.empty(cin, dtype=torch.int32, device=dev)
+            c._srpde_h3f = _Planes(pf, ef) if pf is not None else None
+            c._srpde_h3d = _Planes(pd, ed) if pd is not None else None
+            if pf is None and pd is None:
+                continue
+            # a layer owns cout forward rows then cin dgrad rows (rows of a missing packing idle)
+            desc.append([c.weight.data_ptr(), cout, cin, cin, H._p(pf), H._p(ef), H._p(pd), H._p(ed), rows])
+            rows += cout + cin
+            keep += [t for t in (pf, ef, pd, ed) if t is not None]
+        cache = (sig, torch.tensor(desc, dtype=torch.int64, device=dev), len(desc), rows, keep)
+        m._srpde_h3w = cache
+    _, desc_t, nl, rows, _ = cache
+    H.prepare_weights_h3(desc_t, nl, rows)
+
+
+def _fwd_weights(conv, cin, c0, c1, w, dil):
+    wp = getattr(conv, "_srpde_h3f", None)
+    if wp is not None and H.h3_capable(c0, c1, conv.out_channels, w, dil):
+        return wp
+    return H.pack_conv_weights(conv.weight, cin)[0]
+
+
+def _dgrad_weights(conv, cin, w, dil):
+    wp = getattr(conv, "_srpde_h3d", None)
+    if wp is not None and H.h3_capable(conv.out_channels, 0, cin, w, dil):
+        return wp
+    return H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)[1]
+
+
 def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots):
     """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48)."""
     dev = x0.device
     cout = conv.out_channels
     cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    wf, _ = H.pack_conv_weights(conv.weight, cin)
+    wf = _fwd_weights(conv, cin, x0.shape[1], x1.shape[1] if x1 is not None else 0, w, dil)
     P = n * h * w
     y = H.empty(P, cout, device=dev)
     xp = None
@@ -107,7 +164,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     dyp = None
     if dx is not None:
         cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
-        _, wd = H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)
+        wd = _dgrad_weights(conv, cin, w, dil)
         if xp is not None:
             dyp = H.split_planes_buffer(P, cout, y.device)
         H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp)
@@ -169,6 +226,7 @@ def unet_forward(m, x, training, save=False):
     S.x = x
     x4 = H.nchw_to_nhwc(x, 4)
     S.x4 = x4
+    prepare_h3_weights(m)
     slots = H.AmaxSlots(16, x.device)   # max|x| words of the 16 BN+ReLU outputs (h3 operand scales)
     # encoder
     e1, S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots)

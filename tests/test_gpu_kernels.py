@@ -402,3 +402,26 @@ def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
     e_h3p, e_f32 = rel(dw, dw64), rel(dwf, dw64)
     print(f"wgrad h3p {e_h3p:.3e} f32 {e_f32:.3e}")
     assert e_h3p < 1e-6 and e_h3p < 3.0 * e_f32 + 1e-7, (e_h3p, e_f32)
+
+
+def test_batched_weight_prep_matches_per_layer(conv_math):
+    """srpde_prepare_weights_h3 (every layer's forward and dgrad planes in one launch) is
+    bit-identical to pack + split per layer."""
+    from superresolution_for_pdes_amd import hipops as H
+    from superresolution_for_pdes_amd import unet_exec as X
+    from superresolution_for_pdes_amd.models import UNet
+    H.set_conv_math("h3")
+    torch.manual_seed(0)
+    m = UNet().to(DEV)
+    X.prepare_h3_weights(m)
+    checked = 0
+    for name, c in m.named_modules():
+        if not isinstance(c, torch.nn.Conv2d) or c.kernel_size != (3, 3):
+            continue
+        wf, wd = H.pack_conv_weights(c.weight.detach(), c.in_channels, want_fwd=True, want_dgrad=True)
+        for got, ref in ((c._srpde_h3f, getattr(wf, "h3", None)), (c._srpde_h3d, getattr(wd, "h3", None))):
+            assert (got is None) == (ref is None), name
+            if got is not None:
+                assert torch.equal(got.h3[0], ref[0]) and torch.equal(got.h3[1], ref[1]), name
+                checked += 1
+    assert checked >= 25, checked
