@@ -93,7 +93,10 @@ int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows,
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* xsplit_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+                      void* xsplit_out, const float* in_scale, const float* in_shift, void* workspace,
+                      size_t ws_bytes, hipStream_t stream);
+/* in_scale / in_shift (nullable, c1 == 0 only): the input is relu(x0 * in_scale[c] + in_shift[c])
+ * -- the producing BatchNorm + ReLU applied on the fly (srpde_bn_affine); padding stays zero */
 /* weight gradient with the h3 arithmetic (same workspace as srpde_conv_wgrad; c0, c1, cout % 32 == 0);
  * amax_dy / amax0 / amax1: the max|.| words of dy, x0, x1 as for srpde_conv_fwd_h3 */
 int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,
@@ -126,6 +129,11 @@ int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, i
 int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, float* out, int ldo, long long P, int C, int relu, unsigned* amax,
                       hipStream_t stream);
+/* train-mode BN folded into a per-channel affine for a consumer that applies it on the fly
+ * (a = relu(y*scale + shift), srpde_conv_fwd_h3's in_scale / in_shift), plus a rigorous bound
+ * on max|a| (|gamma| sqrt(P-1) + |beta|, Samuelson's inequality) into *amax_bound (nullable) */
+int srpde_bn_affine(const float* mean, const float* invstd, const float* gamma, const float* beta, int C, long long P,
+                    float* scale, float* shift, unsigned* amax_bound, hipStream_t stream);
 size_t srpde_bn_relu_bwd_workspace_size(long long P, int C);
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,

@@ -72,6 +72,28 @@ __global__ void bn_eval_prepare_kernel(const float* rm, const float* rv, int C, 
   }
 }
 
+// per-channel affine of train-mode BN (a = relu(y*scale + shift)) for a consumer that applies it
+// on the fly (the h3 convolution's input transform), and a rigorous bound on max|a|:
+// Samuelson, |y - mean| <= sqrt(P-1) * std_biased, so |a| <= |gamma| sqrt(P-1) + |beta|
+__global__ __launch_bounds__(256) void bn_affine_kernel(const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        int C, float sqrt_pm1, float* __restrict__ scale,
+                                                        float* __restrict__ shift, unsigned* amax) {
+  float m = 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float sc = gamma[c] * invstd[c];
+    scale[c] = sc;
+    shift[c] = beta[c] - mean[c] * sc;
+    m = fmaxf(m, fabsf(gamma[c]) * sqrt_pm1 + fabsf(beta[c]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0 && amax) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+
 __global__ void increment_i64_kernel(long long* p) { *p += 1; }
 
 // *amax = max(*amax, block max of v) as float bits (v >= 0): the max|x| word the h3
@@ -322,6 +344,15 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
   hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
                      out, ldo, P, C, relu, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_fwd");
+  return 0;
+}
+
+int srpde_bn_affine(const float* mean, const float* invstd, const float* gamma, const float* beta, int C, long long P,
+                    float* scale, float* shift, unsigned* amax_bound, hipStream_t stream) {
+  SRPDE_CHECK_ARG(mean && invstd && gamma && beta && scale && shift && C > 0 && P > 0, "srpde_bn_affine: bad args");
+  hipLaunchKernelGGL(bn_affine_kernel, dim3(1), dim3(256), 0, stream, mean, invstd, gamma, beta, C,
+                     (float)sqrt((double)(P - 1)), scale, shift, amax_bound);
+  SRPDE_LAUNCH_CHECK("srpde_bn_affine");
   return 0;
 }
 

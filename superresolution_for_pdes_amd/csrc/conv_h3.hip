@@ -64,6 +64,8 @@ struct H3Args {
   int relax;               // 1: a stage waits only for its weight DMA (halo slices land later)
   _Float16* xsplit;        // optional [2][P][Cin] hi / lo planes of the (scaled) input, written
                            // as a by-product of the split for the weight-gradient kernel
+  const float* in_scale;   // optional per-channel affine + ReLU applied to x0 in the split
+  const float* in_shift;   // (the producing BatchNorm, fused; c1 == 0)
 };
 
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
@@ -203,8 +205,20 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams
   auto convert = [&](int ch) {
     for (int sg = tid; sg < arows * 4; sg += NT) {
       const int r = sg >> 2, c8 = sg & 3;
-      const float4 v0 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8) * 16);
-      const float4 v1 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8 + 1) * 16);
+      float4 v0 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8) * 16);
+      float4 v1 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8 + 1) * 16);
+      if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
+        const int cc = ch * BK2 + c8 * 8, pix = pix0 + r;
+        const bool inside = pix >= 0 && pix < p.P;
+        const float4 s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
+        const float4 s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
+        const float4 t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
+        const float4 t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
+#define AFF(V, S, T, X) V.X = inside ? fmaxf(V.X * S.X + T.X, 0.f) : 0.f;
+        AFF(v0, s0, t0, x) AFF(v0, s0, t0, y) AFF(v0, s0, t0, z) AFF(v0, s0, t0, w)
+        AFF(v1, s1, t1, x) AFF(v1, s1, t1, y) AFF(v1, s1, t1, z) AFF(v1, s1, t1, w)
+#undef AFF
+      }
       half8 hv, lv;
       split2h(v0, v1, sa, hv, lv);
       const int o = r * 64 + swzh(r, c8) * 16;
@@ -1107,7 +1121,8 @@ int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hi
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* xsplit_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                      void* xsplit_out, const float* in_scale, const float* in_shift, void* workspace,
+                      size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
@@ -1143,6 +1158,10 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   }();
   a.relax = relax;
   a.xsplit = static_cast<_Float16*>(xsplit_out);
+  SRPDE_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr) && (in_scale == nullptr || c1 == 0),
+                  "srpde_conv_fwd_h3: in_scale / in_shift go together and need c1 == 0");
+  a.in_scale = in_scale;
+  a.in_shift = in_shift;
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_, SRB_)                                                                  \

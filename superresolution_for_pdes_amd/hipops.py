@@ -103,9 +103,10 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
 
 
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
-             planes_out=None):
+             planes_out=None, in_affine=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
-    ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad."""
+    ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad;
+    ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly."""
     p0, ld0 = _pl(x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
@@ -120,12 +121,13 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         a1 = amax_of(x1) if x1 is not None else None
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
-             _p(planes_out), ws.data_ptr(), ws.numel(), stream_ptr())
+             _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
+             ws.data_ptr(), ws.numel(), stream_ptr())
         if planes_out is not None:
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert planes_out is None, "planes_out needs the h3 kernels"
+    assert planes_out is None and in_affine is None, "planes_out / in_affine need the h3 kernels"
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
         planes = getattr(wpack, "x6", None)
         if planes is None:
@@ -260,6 +262,16 @@ def bn_train_finalize(stats, nblk, rows_per_blk, P, running_mean, running_var, n
     call("srpde_bn_train_finalize", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
          _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), stream_ptr())
     return mean, invstd
+
+
+def bn_affine(mean, invstd, gamma, beta, P, amax=None):
+    """(scale, shift) with relu(y * scale + shift) == the train-mode BN + ReLU output, and a
+    rigorous max|output| bound written into ``amax`` (the fused consumer's operand scale)."""
+    C = mean.numel()
+    scale, shift = empty(C, device=mean.device), empty(C, device=mean.device)
+    call("srpde_bn_affine", mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), C, P,
+         scale.data_ptr(), shift.data_ptr(), _p(amax), stream_ptr())
+    return scale, shift
 
 
 def bn_eval_prepare(running_mean, running_var, eps):

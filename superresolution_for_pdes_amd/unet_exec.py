@@ -127,30 +127,49 @@ def _dgrad_weights(conv, cin, w, dil):
     return H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)[1]
 
 
-def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots):
-    """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48)."""
+def _splits_both_ways(c0, c1, cout, w, dil):
+    """The layer's forward and dgrad both run on h3, so its weight gradient reads stored splits."""
+    return H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(cout, 0, c0 + c1, w, dil)
+
+
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True):
+    """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48).
+
+    ``activate=False`` (train mode): stop after the BN statistics and return the conv output y
+    with the (scale, shift) that a fused consumer applies (``in_affine``) instead of a
+    materialised relu(bn(y)); y carries the rigorous max|relu(bn(y))| bound as its amax word."""
     dev = x0.device
     cout = conv.out_channels
-    cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    wf = _fwd_weights(conv, cin, x0.shape[1], x1.shape[1] if x1 is not None else 0, w, dil)
+    c1 = x1.shape[1] if x1 is not None else 0
+    cin = x0.shape[1] + c1
+    wf = _fwd_weights(conv, cin, x0.shape[1], c1, w, dil)
     P = n * h * w
     y = H.empty(P, cout, device=dev)
     xp = None
     if training:
         stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev)
-        c1 = x1.shape[1] if x1 is not None else 0
-        if H.h3_capable(x0.shape[1], c1, cout, w, dil) and H.h3_capable(cout, 0, cin, w, dil):
+        if _splits_both_ways(x0.shape[1], c1, cout, w, dil):
             xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
-        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp)
+        assert in_affine is None or xp is not None, "a fused input needs the stored split for its wgrad"
+        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp, in_affine)
         mom = bn.momentum if bn.momentum is not None else 0.0
         mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
                                            bn.num_batches_tracked, mom, bn.eps)
     else:
+        assert in_affine is None and activate
         H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
         mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
+    # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
+    # the weight gradient reads the stored split
+    saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp)
+    if not activate:
+        slot = slots.take()
+        aff = H.bn_affine(mean, invstd, bn.weight, bn.bias, P, amax=slot)
+        y._srpde_amax = slot
+        return (y, aff), saved
     a = H.empty(P, cout, device=dev)
     H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
-    return a, (x0, x1, y, mean, invstd, xp)
+    return a, saved
 
 
 def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False):
@@ -162,8 +181,8 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
                   amax=slots.take())
     dyp = None
+    cin = conv.in_channels if x0 is None else x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
     if dx is not None:
-        cin = x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
         wd = _dgrad_weights(conv, cin, w, dil)
         if xp is not None:
             dyp = H.split_planes_buffer(P, cout, y.device)
@@ -171,13 +190,30 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     if xp is not None and dyp is not None:
         H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)
     else:
+        assert x0 is not None, "fused-input layer without stored splits"
         H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
 
 
-def _block_fwd(blk, x0, x1, n, h, w, training, slots):
-    a1, s1 = _cbr_fwd(blk.conv1, blk.bn1, x0, x1, n, h, w, training, 1, slots)
-    a2, s2 = _cbr_fwd(blk.conv2, blk.bn2, a1, None, n, h, w, training, 1, slots)
+def _fuse_pair(conv2, training, w, dil):
+    """conv1's BN + ReLU can be applied inside conv2 (never materialised) in train mode when
+    conv2 keeps its input split for the weight gradient (so nothing else reads relu(bn(y1)))."""
+    return training and _splits_both_ways(conv2.in_channels, 0, conv2.out_channels, w, dil)
+
+
+def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots):
+    """conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU, with the middle BN + ReLU fused into conv2's
+    input transform when possible (saves a read and a write of the middle activation)."""
+    if _fuse_pair(conv2, training, w, dil):
+        (y1, aff), s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots, activate=False)
+        a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff)
+        return a2, (s1, s2)
+    a1, s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots)
+    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots)
     return a2, (s1, s2)
+
+
+def _block_fwd(blk, x0, x1, n, h, w, training, slots):
+    return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots)
 
 
 def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False):
@@ -235,8 +271,8 @@ def unet_forward(m, x, training, save=False):
     p2 = H.maxpool_fwd(e2, n, h2, w2)
     e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots)
     # bridge (dilated)
-    ab1, S.br1 = _cbr_fwd(m.bridge[0], m.bridge[1], e3, None, n, h3, w3, training, 2, slots)
-    b, S.br2 = _cbr_fwd(m.bridge[3], m.bridge[4], ab1, None, n, h3, w3, training, 2, slots)
+    b, (S.br1, S.br2) = _pair_fwd(m.bridge[0], m.bridge[1], m.bridge[3], m.bridge[4], e3, None, n, h3, w3,
+                                  training, 2, slots)
     # decoder with attention, virtual concat
     e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3)
     d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
