@@ -1001,16 +1001,20 @@ int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigne
 }
 
 // h3p tiles: Cout >= 256: 256x128 (4x2 waves); 128: 128x256 (2x4); 64: 64x256 (1x8); 32: 32x256 (1x8)
-static void h3p_tiles(int cout, int* bm, int* bn) {
+// (192-column tiles with 6 waves for K = 576 / 1728 / 3456, which avoid a partly empty last
+// 256-column tile, measured slower on every layer: the waves' efficiency loss outweighs the waste)
+
+static void h3p_tiles(int cout, int K, int* bm, int* bn) {
   if (cout >= 256) { *bm = 256; *bn = 128; }
   else if (cout >= 128) { *bm = 128; *bn = 256; }
   else if (cout >= 64) { *bm = 64; *bn = 256; }
   else { *bm = 32; *bn = 256; }
+  (void)K;
 }
 
 void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
   int bm, bn;
-  h3p_tiles(cout, &bm, &bn);
+  h3p_tiles(cout, K, &bm, &bn);
   const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
   // one workgroup per CU (LDS): ~4 rounds of 256 CUs, chunks a multiple of the 32-pixel stage
   const long long want = std::max(1LL, 1024 / tiles);
