@@ -93,10 +93,16 @@ int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows,
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* xsplit_out, const float* in_scale, const float* in_shift, void* workspace,
-                      size_t ws_bytes, hipStream_t stream);
+                      void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
+                      int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                      const float* bn_beta, void* bn_part, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* in_scale / in_shift (nullable, c1 == 0 only): the input is relu(x0 * in_scale[c] + in_shift[c])
- * -- the producing BatchNorm + ReLU applied on the fly (srpde_bn_affine); padding stays zero */
+ * -- the producing BatchNorm + ReLU applied on the fly (srpde_bn_affine); padding stays zero.
+ * bn_part (nullable; dgrad of a conv whose input was a BN + ReLU output, accumulate == 0): the
+ * output is that activation's gradient, and the epilogue also writes the BN backward's
+ * reduction, (sum dz, sum dz*xhat) per (srpde_conv_stats_rows_per_block(cout)-row block,
+ * channel) into bn_part [srpde_conv_stats_blocks][cout] float2 (bn_y = the BN's input, its batch
+ * mean / invstd, gamma / beta) -- for srpde_bn_relu_bwd_part */
 /* weight gradient with the h3 arithmetic (same workspace as srpde_conv_wgrad; c0, c1, cout % 32 == 0);
  * amax_dy / amax0 / amax1: the max|.| words of dy, x0, x1 as for srpde_conv_fwd_h3 */
 int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,
@@ -135,6 +141,12 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
 int srpde_bn_affine(const float* mean, const float* invstd, const float* gamma, const float* beta, int C, long long P,
                     float* scale, float* shift, unsigned* amax_bound, hipStream_t stream);
 size_t srpde_bn_relu_bwd_workspace_size(long long P, int C);
+/* srpde_bn_relu_bwd with the (sum dz, sum dz*xhat) reduction already done by the producer of da
+ * (srpde_conv_fwd_h3's bn_part, nblk row blocks): skips the reduction pass over y and da */
+int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
+                           float* dbias, long long P, int C, int relu, unsigned* amax, const void* part, int nblk,
+                           void* workspace, size_t ws_bytes, hipStream_t stream);
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
                       float* dbias, long long P, int C, int relu, unsigned* amax, void* workspace,

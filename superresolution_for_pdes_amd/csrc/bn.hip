@@ -397,4 +397,37 @@ int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const 
   return 0;
 }
 
+int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
+                           float* dbias, long long P, int C, int relu, unsigned* amax, const void* part, int nblk,
+                           void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && dy && workspace && part && nblk > 0,
+                  "srpde_bn_relu_bwd_part: null");
+  SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0 && lddy % 4 == 0,
+                  "srpde_bn_relu_bwd_part: C/ld must be multiples of 4 (C<=1024)");
+  int rpb;
+  const int ablk = bwd_blocks(P, C, &rpb);
+  const size_t need = srpde_bn_relu_bwd_workspace_size(P, C);
+  if (ws_bytes < need) {
+    set_error("srpde_bn_relu_bwd_part: workspace %zu < %zu", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  float2* bpart = static_cast<float2*>(workspace) + (size_t)ablk * C;
+  double* sdz = reinterpret_cast<double*>(bpart + (size_t)ablk * C);
+  double* sdzx = sdz + C;
+  hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, static_cast<const float2*>(part), nblk, C, dbeta,
+                     dgamma, sdz, sdzx);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd_part(colsum)");
+  const size_t lds = 2 * 256 * sizeof(float4);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ablk), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd, gamma,
+                     beta, sdz, sdzx, P, C, rpb, relu, dy, lddy, dbias ? bpart : nullptr, amax);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd_part(apply)");
+  if (dbias) {
+    hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, bpart, ablk, C, dbias, (float*)nullptr,
+                       (double*)nullptr, (double*)nullptr);
+    SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd_part(bias)");
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -555,7 +555,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN >= 8 ? 1 : 2) void conv_fwd_x
   constexpr int A_BYTES = BM * ROW2;
   constexpr int BP_BYTES = BN * 64;        // one bf16 plane of the B tile
   constexpr int STAGE = A_BYTES + 3 * BP_BYTES;
-  constexpr int NSB = BM / SRB, WPS = WM / NSB;
+  constexpr int NSB = BM / SRB;
   static_assert(AI >= 1 && BM % (8 * NW) == 0, "A DMA split");
   static_assert(BM % SRB == 0 && WM % NSB == 0, "statistics sub-blocks");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1573,9 +1573,9 @@ static int launch_fwd_v2(ConvParams p, hipStream_t st, void* ws, size_t ws_bytes
   // workgroups resident at once (occupancy x CUs), queried once per instantiation
   static int slots = [&] {
     int per_cu = 0, dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_v2_kernel<BM, BN, WM, WN, HP>, 256, lds);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_v2_kernel<BM, BN, WM, WN, HP>, 256, lds);
     return std::max(1, per_cu) * std::max(1, cus);
   }();
   // tail split: when the last round of workgroups would be under half full, cut its tiles
@@ -1600,8 +1600,8 @@ static int launch_fwd_x6(ConvParams p, const __bf16* wsp, hipStream_t st, void* 
   const size_t lds = (size_t)2 * (BM * ROW2 + 3 * BN * 64);
   static int slots = [&] {
     int per_cu = 0, dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_x6_kernel<BM, BN, WM, WN, SRB, 2>, NT, lds);
     if (getenv("SRPDE_CONV_VERBOSE"))
       fprintf(stderr, "conv_fwd_x6<%d,%d,%d,%d>: %d workgroups/CU (LDS %zu B)\n", BM, BN, WM, WN, per_cu, lds);
@@ -1628,8 +1628,8 @@ static int launch_fwd_x6p(ConvParams p, const __bf16* wsp, hipStream_t st, void*
   const size_t lds = (size_t)2 * 3 * (BM + BN) * 64;
   static int slots = [&] {
     int per_cu = 0, dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_fwd_x6p_kernel<BM, BN, WM, WN, SRB, 2>, NT, lds);
     return std::max(1, per_cu) * std::max(1, cus);
   }();

@@ -27,6 +27,16 @@ struct ConvParams {
   const __bf16* x0p;
   const __bf16* x1p;
   float* part;
+  // optional fused BatchNorm-backward reduction (h3 dgrad): the output is the gradient of a
+  // BN + ReLU output a = relu(gamma * (bn_y - mean) * invstd + beta); per (SRB-row block, channel)
+  // the epilogue writes (sum dz, sum dz * xhat), dz = out * [a > 0], xhat = (bn_y - mean) * invstd
+  const float* bn_y = nullptr;
+  int bn_ldy = 0;
+  const float* bn_mean = nullptr;
+  const float* bn_invstd = nullptr;
+  const float* bn_gamma = nullptr;
+  const float* bn_beta = nullptr;
+  float2* bn_part = nullptr;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int total) {
@@ -124,8 +134,58 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
       }
     }
   }
-  if (p.stats == nullptr) return;
   constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
+  if (p.bn_part != nullptr) {         // fused BN-backward reduction (as x6_finish)
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 mu = cok ? *reinterpret_cast<const float4*>(p.bn_mean + col) : z4;
+    const float4 is = cok ? *reinterpret_cast<const float4*>(p.bn_invstd + col) : z4;
+    const float4 ga = cok ? *reinterpret_cast<const float4*>(p.bn_gamma + col) : z4;
+    const float4 be = cok ? *reinterpret_cast<const float4*>(p.bn_beta + col) : z4;
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) {
+      const int rb = m0 + sb * SRB;
+      if (rb >= p.P) break;           // uniform over the block
+      float4 s1 = z4, s2 = z4;
+#pragma unroll
+      for (int i = sb * IPS; i < (sb + 1) * IPS; ++i) {
+        const int row = m0 + g + i * G;
+        if (row < p.P && cok) {
+          const float4 yv = *reinterpret_cast<const float4*>(p.bn_y + (size_t)row * p.bn_ldy + col);
+          float xh, dz;
+#define BNP_ACC(X)                                     \
+  xh = (yv.X - mu.X) * is.X;                           \
+  dz = xh * ga.X + be.X > 0.f ? v[i].X : 0.f;          \
+  s1.X += dz;                                          \
+  s2.X += dz * xh;
+          BNP_ACC(x) BNP_ACC(y) BNP_ACC(z) BNP_ACC(w)
+#undef BNP_ACC
+        }
+      }
+      red[g][cq] = s1;
+      __syncthreads();
+      float4 t1 = z4;
+      if (g == 0)
+        for (int k = 0; k < G; ++k) {
+          const float4 q = red[k][cq];
+          t1.x += q.x; t1.y += q.y; t1.z += q.z; t1.w += q.w;
+        }
+      __syncthreads();
+      red[g][cq] = s2;
+      __syncthreads();
+      if (g == 0 && cok) {
+        float4 t2 = z4;
+        for (int k = 0; k < G; ++k) {
+          const float4 q = red[k][cq];
+          t2.x += q.x; t2.y += q.y; t2.z += q.z; t2.w += q.w;
+        }
+        float2* bp = p.bn_part + (size_t)(rb / SRB) * p.Cout + col;
+        bp[0] = make_float2(t1.x, t2.x); bp[1] = make_float2(t1.y, t2.y);
+        bp[2] = make_float2(t1.z, t2.z); bp[3] = make_float2(t1.w, t2.w);
+      }
+      __syncthreads();
+    }
+  }
+  if (p.stats == nullptr) return;
 #pragma unroll
   for (int sb = 0; sb < NSB; ++sb) {
     const int rb = m0 + sb * SRB;
@@ -200,6 +260,22 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
     const int col = n0 + wn0 + j * 32 + lr;
     bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
   }
+  // fused BN-backward reduction: issue every load of the BN input up front (clamped addresses,
+  // masked in the sums) so they overlap each other and the stores instead of serialising
+  float byv[TI][TJ][16];
+  if (p.bn_part != nullptr) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = min(n0 + wn0 + j * 32 + lr, p.Cout - 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, p.P - 1);
+          byv[i][j][r] = __builtin_nontemporal_load(p.bn_y + (size_t)row * p.bn_ldy + col);
+        }
+      }
+  }
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -216,6 +292,52 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
         }
       }
     }
+  if (p.bn_part != nullptr) {         // fused BN-backward reduction of the layer below (see ConvParams)
+    float* red = smem;                // [2][WM][BN]
+    const int sb = wmi / WPS;
+    const int rb0 = m0 + sb * SRB;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+      const bool cok = col < p.Cout;
+      const float mu = cok ? p.bn_mean[col] : 0.f, is = cok ? p.bn_invstd[col] : 0.f;
+      const float ga = cok ? p.bn_gamma[col] : 0.f, be = cok ? p.bn_beta[col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < p.P && cok) {
+            const float xh = (byv[i][j][r] - mu) * is;
+            const float dz = xh * ga + be > 0.f ? acc[i][j][r] : 0.f;
+            s1 += dz;
+            s2 += dz * xh;
+          }
+        }
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lh == 0) {
+        red[wmi * BN + wn0 + j * 32 + lr] = s1;
+        red[WM * BN + wmi * BN + wn0 + j * 32 + lr] = s2;
+      }
+    }
+    __syncthreads();
+    if (wmi % WPS == 0 && lh == 0 && rb0 < p.P) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int cl = wn0 + j * 32 + lr, col = n0 + cl;
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPS; ++w) {
+          t1 += red[(sb * WPS + w) * BN + cl];
+          t2 += red[WM * BN + (sb * WPS + w) * BN + cl];
+        }
+        if (col < p.Cout) p.bn_part[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(t1, t2);
+      }
+    }
+    __syncthreads();
+  }
   if (p.stats == nullptr) return;
   float* red = smem;                  // [WM][BN] per-wave-row column partials
   const int sb = wmi / WPS;           // this wave's statistics sub-block

@@ -964,8 +964,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   const size_t lds = h3_lds(BN, h.arows, TPS);
   static int slots = [&] {
     int dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return std::max(1, cus);      // one workgroup per CU (LDS)
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
@@ -1125,8 +1125,9 @@ int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hi
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
-                      void* xsplit_out, const float* in_scale, const float* in_shift, void* workspace,
-                      size_t ws_bytes, hipStream_t stream) {
+                      void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
+                      int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                      const float* bn_beta, void* bn_part, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
@@ -1166,6 +1167,11 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "srpde_conv_fwd_h3: in_scale / in_shift go together and need c1 == 0");
   a.in_scale = in_scale;
   a.in_shift = in_shift;
+  SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
+                                          bn_ldy % 4 == 0 && cout % 4 == 0),
+                  "srpde_conv_fwd_h3: the fused BN reduction needs bn_y/mean/invstd/gamma/beta and no accumulate");
+  p.bn_y = bn_y; p.bn_ldy = bn_ldy; p.bn_mean = bn_mean; p.bn_invstd = bn_invstd;
+  p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_, SRB_)                                                                  \

@@ -103,10 +103,12 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
 
 
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
-             planes_out=None, in_affine=None):
+             planes_out=None, in_affine=None, bn_bwd=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
     ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad;
-    ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly."""
+    ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly;
+    ``bn_bwd = (bn_y, mean, invstd, gamma, beta, part)`` (dgrad into a BN + ReLU output's
+    gradient) also writes that BN backward's reduction into ``part`` (bn_bwd_partials)."""
     p0, ld0 = _pl(x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
@@ -122,12 +124,13 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
-             ws.data_ptr(), ws.numel(), stream_ptr())
+             *_bn_bwd_args(bn_bwd), ws.data_ptr(), ws.numel(), stream_ptr())
         if planes_out is not None:
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert planes_out is None and in_affine is None, "planes_out / in_affine need the h3 kernels"
+    assert planes_out is None and in_affine is None and bn_bwd is None, \
+        "planes_out / in_affine / bn_bwd need the h3 kernels"
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
         planes = getattr(wpack, "x6", None)
         if planes is None:
@@ -137,6 +140,20 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         return
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+def _bn_bwd_args(bn_bwd):
+    if bn_bwd is None:
+        return (0, 0, 0, 0, 0, 0, 0)
+    by, mean, invstd, gamma, beta, part = bn_bwd
+    pby, ldby = _pl(by)
+    return (pby, ldby, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), part.data_ptr())
+
+
+def bn_bwd_partials(n, h, w, c, device):
+    """Buffer for conv_fwd(bn_bwd=...): [blocks, c, 2] fp32, blocks from the conv stats geometry."""
+    nblk = int(query("srpde_conv_stats_blocks", n, h, w, c))
+    return empty(nblk, c, 2, device=device)
 
 
 # ---------------------- operand-scale words of the h3 convolutions ----------------------
@@ -291,16 +308,20 @@ def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True, amax=None):
     tag_amax(out, amax)
 
 
-def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True, amax=None):
+def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True, amax=None, part=None):
+    """BN (+ReLU) backward; ``part`` = the reduction already produced by conv_fwd(bn_bwd=...)."""
     P, C = y.shape
     py, ldy = _pl(y)
     pda, ldda = _pl(da)
     pdy, lddy = _pl(dy)
     ws_bytes = int(query("srpde_bn_relu_bwd_workspace_size", P, C))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
-    call("srpde_bn_relu_bwd", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
-         beta.data_ptr(), pdy, lddy, _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), _p(amax), ws.data_ptr(),
-         ws_bytes, stream_ptr())
+    args = (py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pdy, lddy,
+            _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), _p(amax))
+    if part is None:
+        call("srpde_bn_relu_bwd", *args, ws.data_ptr(), ws_bytes, stream_ptr())
+    else:
+        call("srpde_bn_relu_bwd_part", *args, part.data_ptr(), part.shape[0], ws.data_ptr(), ws_bytes, stream_ptr())
     tag_amax(dy, amax)
 
 

@@ -18,6 +18,8 @@ reverse schedule.  Design points:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import hipops as H
@@ -172,26 +174,42 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     return a, saved
 
 
-def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False):
+def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False, part=None,
+             below=None):
     """dgrad first: its h3 kernel stores dy's split, which the weight gradient then reads together
-    with the input's split stored by the forward (h3p); otherwise the splitting wgrad kernels."""
+    with the input's split stored by the forward (h3p); otherwise the splitting wgrad kernels.
+
+    ``part``: this BN's backward reduction, already produced by the dgrad that wrote ``da``.
+    ``below = (bn, saved)``: the BN + ReLU whose output this layer reads; when the dgrad runs on
+    h3 into a fresh ``dx`` it also produces that BN's reduction, returned for the next call."""
     x0, x1, y, mean, invstd, xp = saved
     P, cout = y.shape
     dy = H.empty(P, cout, device=y.device)
     H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
-                  amax=slots.take())
+                  amax=slots.take(), part=part)
     dyp = None
+    out_part = None
     cin = conv.in_channels if x0 is None else x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
     if dx is not None:
         wd = _dgrad_weights(conv, cin, w, dil)
         if xp is not None:
             dyp = H.split_planes_buffer(P, cout, y.device)
-        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp)
+        bn_bwd = None
+        if below is not None and not dx_accumulate and _FUSE_BN_BWD and H.h3_capable(cout, 0, cin, w, dil):
+            bnb, sb = below
+            out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
+            bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
+        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp, bn_bwd=bn_bwd)
     if xp is not None and dyp is not None:
         H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)
     else:
         assert x0 is not None, "fused-input layer without stored splits"
         H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
+    return out_part
+
+
+# the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
+_FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"
 
 
 def _fuse_pair(conv2, training, w, dil):
@@ -220,8 +238,8 @@ def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False):
     s1, s2 = saved
     P = n * h * w
     da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
-    _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1)
-    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate)
+    part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, below=(blk.bn1, s1))
+    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part)
 
 
 def _att_params(att):
@@ -308,10 +326,10 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.head_bwd(dout, S.o2, m.final.weight, n, hw1, do2, grads[m.final.weight], grads[m.final.bias])
     ready("final")
     do1 = H.empty(P1, m.out_conv1.out_channels, device=dev)
-    _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1)
+    part = _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1, below=(m.out_bn1, S.out1))
     ready("out_bn2"); ready("out_conv2")
     dd1 = H.empty(P1, 64, device=dev)
-    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1)
+    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part)
     ready("out_bn1"); ready("out_conv1")
     # dec1: grad of cat[u2 (128), e1a (64)]
     dcat1 = H.empty(P1, 192, device=dev)
@@ -340,8 +358,9 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     ready("att3")
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
-    _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1)
-    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True)
+    part = _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1,
+                    below=(m.bridge[1], S.br1))
+    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True, part=part)
     ready("bridge")
     # encoder
     dp2 = H.empty(P3, 128, device=dev)

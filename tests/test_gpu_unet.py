@@ -137,3 +137,26 @@ def test_large_batch_properties():
         mt.load_state_dict(fixture_state_torch())
         b = mt(x[perm].to(DEV))
     assert rmse(a[perm.to(DEV)].cpu(), b.cpu()) < 1e-5 * float(a.std())
+
+
+def test_fused_bn_backward_reduction_matches_separate_pass():
+    """The BN backward reduction produced in the dgrad epilogue (unet_exec._FUSE_BN_BWD) gives the
+    same gradients as the separate reduction kernel (only the summation order differs)."""
+    from superresolution_for_pdes_amd import unet_exec
+    x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(7)).to(DEV)
+    grads = []
+    saved = unet_exec._FUSE_BN_BWD
+    try:
+        for fuse in (True, False):
+            unet_exec._FUSE_BN_BWD = fuse
+            m = make_model(True)
+            (m(x) ** 2).mean().backward()
+            grads.append({n: p.grad.detach().double().clone() for n, p in m.named_parameters()})
+    finally:
+        unet_exec._FUSE_BN_BWD = saved
+    for n, g in grads[0].items():
+        r = grads[1][n]
+        if n.endswith(".bias") and ("conv" in n or n.startswith("bridge.0") or n.startswith("bridge.3")):
+            continue   # true gradient 0 (bias feeding BatchNorm): noise only
+        e = float((g - r).norm() / max(float(r.norm()), 1e-30))
+        assert e < 1e-4, (n, e)
