@@ -8,7 +8,7 @@ buffer is all-reduced in buckets *while the backward is still running*:
   order (unet_exec.FLAT_GROUPS), and calls ``ready(offset)`` whenever a module group's
   gradients are final -- a growing prefix;
 * ``GradReducer`` records an event on the compute stream, makes its side stream wait on
-  it, and issues ``all_reduce`` of every finished ``bucket_bytes`` chunk on that side
+  it (and on the executor's weight-gradient stream), and issues ``all_reduce`` of every finished ``bucket_bytes`` chunk on that side
   stream, so RCCL traffic over xGMI overlaps the remaining dgrad/wgrad kernels;
 * ``finish()`` flushes the tail and makes the compute stream wait for the side stream.
 
@@ -36,6 +36,7 @@ class GradReducer:
         self.works = []
         self.stream = None
         self.n_buckets = 0
+        self.wait_streams = ()
 
     def _side_stream(self, dev):
         if dev.type != "cuda":
@@ -44,8 +45,11 @@ class GradReducer:
             self.stream = torch.cuda.Stream(device=dev)
         return self.stream
 
-    def begin(self, flat):
+    def begin(self, flat, wait_streams=()):
+        """``wait_streams``: further streams that write the flat gradient (the executor's
+        weight-gradient side stream); every bucket also waits for them."""
         self.flat = flat
+        self.wait_streams = tuple(wait_streams)
         self.launched = 0
         self.works = []
         self.n_buckets = 0
@@ -57,6 +61,8 @@ class GradReducer:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.device))
             st.wait_event(ev)
+            for s in self.wait_streams:
+                st.wait_stream(s)
             with torch.cuda.stream(st):
                 op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
                 self.works.append((dist.all_reduce(chunk, op=op, group=self.pg, async_op=True), chunk))

@@ -174,14 +174,52 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     return a, saved
 
 
+class WgradStream:
+    """Weight gradients on a second HIP stream.
+
+    Nothing in the backward reads a weight gradient, so the wgrad launches leave the critical
+    path (dgrad -> BN backward -> dgrad ...): each is queued on a side stream behind the compute
+    stream's work so far, and its MFMA work fills the CUs the dgrad chain leaves idle (tail
+    waves, the HBM-bound BN / attention / upsample kernels).  Operands allocated on the compute
+    stream are ``record_stream``-ed so the caching allocator does not recycle them early;
+    ``join()`` makes the compute stream wait for every queued wgrad (before anything reads the
+    gradients)."""
+
+    _streams = {}
+
+    def __init__(self, dev):
+        self.main = torch.cuda.current_stream(dev)
+        key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+        side = WgradStream._streams.get(key)
+        if side is None:
+            side = WgradStream._streams[key] = torch.cuda.Stream(device=dev)
+        self.side = side
+
+    def submit(self, fn, keep=()):
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn()
+        for t in keep:
+            if t is not None:
+                t.record_stream(self.side)
+
+    def join(self):
+        self.main.wait_stream(self.side)
+
+
+# weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
+_WGRAD_STREAM = os.environ.get("SRPDE_WGRAD_STREAM", "1") != "0"
+
+
 def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False, part=None,
-             below=None):
+             below=None, wq=None):
     """dgrad first: its h3 kernel stores dy's split, which the weight gradient then reads together
     with the input's split stored by the forward (h3p); otherwise the splitting wgrad kernels.
 
     ``part``: this BN's backward reduction, already produced by the dgrad that wrote ``da``.
     ``below = (bn, saved)``: the BN + ReLU whose output this layer reads; when the dgrad runs on
-    h3 into a fresh ``dx`` it also produces that BN's reduction, returned for the next call."""
+    h3 into a fresh ``dx`` it also produces that BN's reduction, returned for the next call.
+    ``wq``: a WgradStream that takes the weight-gradient launch off the compute stream."""
     x0, x1, y, mean, invstd, xp = saved
     P, cout = y.shape
     dy = H.empty(P, cout, device=y.device)
@@ -200,11 +238,16 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
             out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
             bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
         H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp, bn_bwd=bn_bwd)
+    dw = grads[conv.weight]
     if xp is not None and dyp is not None:
-        H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax)
     else:
         assert x0 is not None, "fused-input layer without stored splits"
-        H.conv_wgrad(dy, x0, x1, grads[conv.weight], n, h, w, 3, dil)
+        fn, keep = (lambda: H.conv_wgrad(dy, x0, x1, dw, n, h, w, 3, dil)), (dy, getattr(dy, "_srpde_amax", None))
+    if wq is None:
+        fn()
+    else:
+        wq.submit(fn, keep)
     return out_part
 
 
@@ -234,12 +277,12 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots):
     return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots)
 
 
-def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False):
+def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None):
     s1, s2 = saved
     P = n * h * w
     da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
-    part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, below=(blk.bn1, s1))
-    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part)
+    part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, below=(blk.bn1, s1), wq=wq)
+    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part, wq=wq)
 
 
 def _att_params(att):
@@ -310,9 +353,11 @@ def unet_forward(m, x, training, save=False):
     return out.view(n, 1, h, w), S
 
 
-def unet_backward(m, S, dout, grads, grad_ready=None):
+def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     """Reverse schedule.  ``grads``: param -> writable view (every one is fully written).
-    ``grad_ready(group)`` is called as soon as a module group's gradients are final."""
+    ``grad_ready(group)`` is called as soon as a module group's gradients are queued (with
+    ``wq``, a WgradStream, the weight gradients run on its side stream: a consumer waits for
+    that stream too; the compute stream joins it before this returns)."""
     n, h, w = S.shape
     h2, w2, h3, w3 = h // 2, w // 2, h // 4, w // 4
     hw1, hw2, hw3 = h * w, h2 * w2, h3 * w3
@@ -326,14 +371,15 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.head_bwd(dout, S.o2, m.final.weight, n, hw1, do2, grads[m.final.weight], grads[m.final.bias])
     ready("final")
     do1 = H.empty(P1, m.out_conv1.out_channels, device=dev)
-    part = _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1, below=(m.out_bn1, S.out1))
+    part = _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1, below=(m.out_bn1, S.out1),
+                    wq=wq)
     ready("out_bn2"); ready("out_conv2")
     dd1 = H.empty(P1, 64, device=dev)
-    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part)
+    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part, wq=wq)
     ready("out_bn1"); ready("out_conv1")
     # dec1: grad of cat[u2 (128), e1a (64)]
     dcat1 = H.empty(P1, 192, device=dev)
-    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1)
+    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1, wq=wq)
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
     _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, dcat1[:, :128], True)
@@ -342,7 +388,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False)
     # dec2: grad of cat[u3 (256), e2a (128)]
     dcat2 = H.empty(P2, 384, device=dev)
-    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2)
+    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2, wq=wq)
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
     _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, dcat2[:, :256], True)
@@ -351,7 +397,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False)
     # dec3: grad of cat[b (512), e3a (256)]
     dcat3 = H.empty(P3, 768, device=dev)
-    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3)
+    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq)
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)
     _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True)
@@ -359,20 +405,22 @@ def unet_backward(m, S, dout, grads, grad_ready=None):
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
     part = _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1,
-                    below=(m.bridge[1], S.br1))
-    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True, part=part)
+                    below=(m.bridge[1], S.br1), wq=wq)
+    _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True, part=part, wq=wq)
     ready("bridge")
     # encoder
     dp2 = H.empty(P3, 128, device=dev)
-    _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, slots, dp2)
+    _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, slots, dp2, wq=wq)
     ready("enc3")
     H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
     dp1 = H.empty(P2, 64, device=dev)
-    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1)
+    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1, wq=wq)
     ready("enc2")
     H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
-    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, None)
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, None, wq=wq)
     ready("enc1")
+    if wq is not None:
+        wq.join()
 
 
 class UNetFunction(torch.autograd.Function):
@@ -397,11 +445,12 @@ class UNetFunction(torch.autograd.Function):
         views = {p: flat[off:off + nn].view_as(p) for _, p, off, nn in layout}
         reducer = getattr(model, "_grad_reducer", None)
         ends = _group_end_offsets(layout)
+        wq = WgradStream(dout.device) if _WGRAD_STREAM and dout.is_cuda else None
         hook = None
         if reducer is not None:
-            reducer.begin(flat)
+            reducer.begin(flat, wait_streams=() if wq is None else (wq.side,))
             hook = lambda grp: reducer.ready(ends[grp])  # noqa: E731
-        unet_backward(model, ctx.saved, dout, views, hook)
+        unet_backward(model, ctx.saved, dout, views, hook, wq=wq)
         if reducer is not None:
             reducer.finish()
         ctx.saved = None
