@@ -84,6 +84,13 @@ int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const v
  * for srpde_conv_wgrad_h3p (the split is computed anyway; storing it costs one 4-B write per
  * element). */
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize);
+/* Rows per BatchNorm-statistics block written by srpde_conv_fwd_h3 (stats / bn_part buffers
+ * hold ceil(P / rows) blocks); the other conv families use srpde_conv_stats_rows_per_block. */
+int srpde_conv_h3_stats_rows(void);
+/* Tile choice of srpde_conv_fwd_h3: layers with at most max_chunks 32-channel chunks of input run
+ * on 128-row tiles, two workgroups per CU (0: never).  Returns the previous value.  Tuning and
+ * tests; the default comes from SRPDE_H3_HALF. */
+int srpde_conv_h3_set_half(int max_chunks);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]

@@ -26,6 +26,8 @@
 // of both operands straight from LDS.  The next chunk's halo tile is DMA'd in slices during
 // the current chunk's stages; the weight tile of each tap stage is double-buffered.  One
 // partial MFMA chain per chunk (two-level fp32 accumulation).
+#include <atomic>
+
 #include "conv_common.h"
 
 namespace srpde {
@@ -72,7 +74,7 @@ struct H3Args {
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
 // TPS: taps per stage (one barrier per stage; the weight stage holds TPS taps).
 template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
-__global__ __launch_bounds__(WM * WN * 64, 1) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
+__global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per stage (16 rows x 64 B)
@@ -939,8 +941,27 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 static int h3_cfg(int cout) { return cout % 128 == 0 ? 1 : (cout % 64 == 0 ? 2 : 3); }
 static int h3_bn(int cfg) { return cfg == 1 ? 128 : cfg == 2 ? 64 : 32; }
 constexpr int H3_BM = 256;
+// rows per BatchNorm-statistics block of every h3 forward launch (srpde_conv_h3_stats_rows)
+constexpr int H3_SRB = 128;
 
-static int h3_arows(int w, int dil) { return (H3_BM + 2 * (w + 1) * dil + 7) / 8 * 8; }
+static int h3_arows(int w, int dil, int bm = H3_BM) { return (bm + 2 * (w + 1) * dil + 7) / 8 * 8; }
+
+// Layers with at most this many 32-channel chunks of K run on 128-row tiles with 4 waves and one
+// tap per stage (<= 78 KiB of LDS: two workgroups per CU), so one workgroup's prologue / epilogue
+// overlaps the other's MFMAs; deeper layers keep the 256-row, 8-wave tile (one per CU).
+// SRPDE_H3_HALF or srpde_conv_h3_set_half override the threshold (0: never).
+static std::atomic<int> g_h3_half{-1};
+static int h3_half_max() {
+  int v = g_h3_half.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("SRPDE_H3_HALF");
+    v = e ? std::max(0, atoi(e)) : 0;
+    int expect = -1;
+    g_h3_half.compare_exchange_strong(expect, v);
+    v = g_h3_half.load(std::memory_order_relaxed);
+  }
+  return v;
+}
 
 static size_t h3_lds(int bn, int arows, int tps = 1) {
   return (size_t)arows * (ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
@@ -966,7 +987,7 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max(1, cus);      // one workgroup per CU (LDS)
+    return std::max(1, cus) * (8 / (WM * WN));   // resident workgroups: one (8 waves) or two (4) per CU
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
   static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
@@ -1087,6 +1108,14 @@ using namespace srpde;
 
 extern "C" {
 
+int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
+
+int srpde_conv_h3_set_half(int max_chunks) {
+  const int prev = h3_half_max();
+  g_h3_half.store(std::max(0, max_chunks));
+  return prev;
+}
+
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
   // cout % 16: a 16-channel output (out_conv2) runs on the 32-column tile with the weight rows past
   // Cout zero-filled by the DMA range check
@@ -1173,15 +1202,23 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.bn_y = bn_y; p.bn_ldy = bn_ldy; p.bn_mean = bn_mean; p.bn_invstd = bn_invstd;
   p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
+  if (p.Cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) {   // shallow K: 128-row tiles, 2 per CU
+    a.arows = h3_arows(w, dil, 128);
+    switch (h3_cfg(cout)) {
+      case 1: return launch_fwd_h3<128, 128, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
+      case 2: return launch_fwd_h3<128, 64, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
+      default: return launch_fwd_h3<128, 32, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
+    }
+  }
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
-#define H3_LAUNCH(BN_, SRB_)                                                                  \
-  (tps >= 3 ? launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 3>(p, a, stream, workspace, ws_bytes) \
-   : tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 2>(p, a, stream, workspace, ws_bytes) \
-              : launch_fwd_h3<256, BN_, 8, 1, SRB_, true, 1>(p, a, stream, workspace, ws_bytes))
+#define H3_LAUNCH(BN_)                                                                         \
+  (tps >= 3 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 3>(p, a, stream, workspace, ws_bytes) \
+   : tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
+              : launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes))
   switch (h3_cfg(cout)) {
-    case 1: return H3_LAUNCH(128, 128);
-    case 2: return H3_LAUNCH(64, 256);
-    default: return H3_LAUNCH(32, 256);
+    case 1: return H3_LAUNCH(128);
+    case 2: return H3_LAUNCH(64);
+    default: return H3_LAUNCH(32);
   }
 #undef H3_LAUNCH
 }

@@ -93,9 +93,21 @@ def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
     return wf, wd
 
 
-def conv_stats_buffer(n, h, w, cout, device):
-    nblk = int(query("srpde_conv_stats_blocks", n, h, w, cout))
-    return empty(nblk, cout, 2, device=device), nblk, int(query("srpde_conv_stats_rows_per_block", cout))
+def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
+    """BN-statistics partials for the forward conv of input channels (c0, c1) -> cout: the
+    kernel family that will run decides the row-block size.  -> (buffer, blocks, rows/block)."""
+    h3 = h3_capable(c0, c1, cout, w, dil)
+    rows = int(query("srpde_conv_h3_stats_rows")) if h3 else int(query("srpde_conv_stats_rows_per_block", cout))
+    nblk = -(-(n * h * w) // rows)
+    buf = empty(nblk, cout, 2, device=device)
+    buf._srpde_rows = rows
+    return buf, nblk, rows
+
+
+def set_h3_half(max_chunks: int) -> int:
+    """h3 tile choice: input depth (in 32-channel chunks) up to which the 128-row, two-per-CU
+    tile runs (0: never).  Returns the previous value."""
+    return int(query("srpde_conv_h3_set_half", int(max_chunks)))
 
 
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
@@ -119,6 +131,10 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
     if _CONV_MATH == "h3" and query("srpde_conv_h3_supported", x0.shape[1], c1, cout, w, dil, ksize):
         planes, wexp = getattr(wpack, "h3", None) or split_weights_h3(wpack, cout)
+        for buf in (stats, bn_bwd[5] if bn_bwd is not None else None):
+            if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
+                raise ValueError("statistics buffer not laid out for the h3 kernel (use conv_stats_buffer "
+                                 "with the input channels / bn_bwd_partials)")
         a0 = amax_of(x0)
         a1 = amax_of(x1) if x1 is not None else None
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
@@ -131,6 +147,8 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         return
     assert planes_out is None and in_affine is None and bn_bwd is None, \
         "planes_out / in_affine / bn_bwd need the h3 kernels"
+    if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
+        raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
         planes = getattr(wpack, "x6", None)
         if planes is None:
@@ -151,9 +169,11 @@ def _bn_bwd_args(bn_bwd):
 
 
 def bn_bwd_partials(n, h, w, c, device):
-    """Buffer for conv_fwd(bn_bwd=...): [blocks, c, 2] fp32, blocks from the conv stats geometry."""
-    nblk = int(query("srpde_conv_stats_blocks", n, h, w, c))
-    return empty(nblk, c, 2, device=device)
+    """Buffer for conv_fwd(bn_bwd=...) (an h3 dgrad): [blocks, c, 2] fp32, h3 row blocks."""
+    rows = int(query("srpde_conv_h3_stats_rows"))
+    buf = empty(-(-(n * h * w) // rows), c, 2, device=device)
+    buf._srpde_rows = rows
+    return buf
 
 
 # ---------------------- operand-scale words of the h3 convolutions ----------------------

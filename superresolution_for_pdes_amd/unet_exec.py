@@ -149,7 +149,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     y = H.empty(P, cout, device=dev)
     xp = None
     if training:
-        stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev)
+        stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev, x0.shape[1], c1, dil)
         if _splits_both_ways(x0.shape[1], c1, cout, w, dil):
             xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
         assert in_affine is None or xp is not None, "a fused input needs the stored split for its wgrad"

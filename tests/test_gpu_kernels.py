@@ -48,7 +48,7 @@ def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
     wd = wt.to(DEV)
     wf, wdg = H.pack_conv_weights(wd, cin, want_dgrad=True)
     y = H.empty(n * h * h, cout, device=DEV)
-    stats, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV)
+    stats, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV, cin0, cin1, dil)
     H.conv_fwd(x0, x1, wf, b.to(DEV), y, n, h, h, cout, 3, dil, 1, False, stats)
     torch.cuda.synchronize()
     assert rel(unrows(y, n, h, h), y_ref) < 2e-6
@@ -125,7 +125,7 @@ def test_conv_x6p_equals_x6(cin0, cin1, cout, h, dil, conv_math):
     wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(DEV)
     b = torch.randn(cout, generator=g).to(DEV)
     wf, wd = H.pack_conv_weights(wt, cin, want_dgrad=True)
-    st1, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV)
+    st1, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV, cin0, cin1, dil)
     st2 = torch.empty_like(st1)
     y1, y2 = H.empty(n * h * h, cout, device=DEV), H.empty(n * h * h, cout, device=DEV)
     H.conv_fwd(x0, x1, wf, b, y1, n, h, h, cout, 3, dil, 1, False, st1)

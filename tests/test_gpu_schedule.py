@@ -47,3 +47,43 @@ def test_wgrad_side_stream_is_bit_identical():
         assert torch.equal(a[1][n], b[1][n]), n
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), n
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (6, 256, 0, 512, 10, 2),
+                                                 (4, 256, 128, 128, 20, 1), (3, 64, 0, 32, 40, 1),
+                                                 (5, 128, 64, 64, 40, 1)])
+def test_conv_h3_half_tiles_equal_full_tiles(n, c0, c1, cout, hw, dil):
+    """The 128-row, two-per-CU h3 tile computes every output element, BN partial and stored
+    split in the same order as the 256-row tile (no K-split tail at these sizes): equal bits."""
+    from superresolution_for_pdes_amd import hipops as H
+    if H.conv_math() != "h3" or not (H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, c0 + c1, hw, dil)):
+        pytest.skip("not an h3 shape")
+    g = torch.Generator(device=DEV).manual_seed(3)
+    P, cin = n * hw * hw, c0 + c1
+    x = torch.randn(P, cin, device=DEV, generator=g)
+    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, wd = H.pack_conv_weights(w, cin, True, True)
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    for t in (x0, x1, dy):
+        if t is not None:
+            t._srpde_amax = H.amax_of(t)
+    outs = []
+    prev = H.set_h3_half(0)
+    try:
+        for half in (0, 99):
+            H.set_h3_half(half)
+            y = torch.empty(P, cout, device=DEV)
+            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
+            xp = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
+            dx = torch.empty(P, cin, device=DEV)
+            dyp = H.split_planes_buffer(P, cout, DEV)
+            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
+            torch.cuda.synchronize()
+            outs.append((y, stats, xp, dx, dyp))
+    finally:
+        H.set_h3_half(prev)
+    for k, (a, b_) in enumerate(zip(*outs)):
+        assert torch.equal(a, b_), k

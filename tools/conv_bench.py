@@ -57,7 +57,7 @@ def main():
         b = torch.randn(cout, device=dev)
         wf, wd = H.pack_conv_weights(w, cin, True, True)
         y = torch.empty(P, cout, device=dev)
-        stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, dev)
+        stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, dev, c0, c1, dil)
         dy = torch.randn(P, cout, device=dev)
         for t in (x0, x1, dy):   # h3: max|x| words computed once, as the producers would
             if t is not None:

@@ -27,7 +27,7 @@ for cin, cout in ((64, 32), (32, 16), (192, 64)):
     da = torch.randn(n, cout, h, h, generator=g) * 1e-4
     a64, y64, g64, b64 = bnf(yv, torch.float64); a64.backward(da.double())
     a32, y32, g32, b32 = bnf(yv, torch.float32); a32.backward(da)
-    stats, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, D)
+    stats, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, D, cin)
     yy = H.empty(n * h * h, cout, device=D)
     H.conv_fwd(rows(x).to(D), None, wf, b.to(D), yy, n, h, h, cout, 3, 1, 1, False, stats)
     yy.copy_(rows(yv).to(D))  # identical conv output for the BN comparison
