@@ -229,12 +229,14 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
   }
 }
 
-// epilogue shared by the x6 forward kernels: raw tail-piece tiles, or bias + store + BN
-// partial statistics per SRB rows
+// epilogue shared by the x6 / h3 forward kernels: raw tail-piece tiles, or bias + store + BN
+// partial statistics per SRB rows.  `stage` (nullable): 2 KiB of LDS per wave, past the
+// reduction scratch, through which the output leaves as 16-B row stores (needs ldy % 4 == 0 and
+// a 16-B aligned y): 4 dwordx4 stores per lane and 32x32 block instead of 16 dword stores.
 template <int BM, int BN, int WM, int WN, int SRB>
 __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32], bool tail,
                                           int wg, int nfull, int piece, int m0, int n0, int wmi, int wni, int lane,
-                                          float* smem) {
+                                          float* smem, float* stage = nullptr) {
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int NSB = BM / SRB, WPS = WM / NSB;
   const int lr = lane & 31, lh = lane >> 5;
@@ -279,19 +281,59 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + lr;
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float v = acc[i][j][r] + bcol[j];
-        acc[i][j][r] = v;
-        if (row < p.P && col < p.Cout) {
-          float* dst = p.y + (size_t)row * p.ldy + col;
-          *dst = p.accumulate ? *dst + v : v;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] += bcol[j];
+  if (stage != nullptr) {
+    // each 16-row half of a wave's 32x32 block goes through the wave's LDS stage as [16][32]
+    // floats and comes back as one float4 of a row per lane (8 lanes per 128-B row)
+    float* st = stage + (wni * WM + wmi) * 512;
+    const int rr = lane >> 3, c4 = (lane & 7) * 4;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = n0 + wn0 + j * 32 + c4;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+          for (int r = 8 * hf; r < 8 * hf + 8; ++r)
+            st[((r & 3) + 8 * ((r >> 2) & 1) + 4 * lh) * 32 + lr] = acc[i][j][r];
+          __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's stage writes are done
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const float4 v = *reinterpret_cast<const float4*>(st + (8 * k + rr) * 32 + c4);
+            const int row = m0 + wm0 + i * 32 + 16 * hf + 8 * k + rr;
+            if (row < p.P && col < p.Cout) {
+              float4* dst = reinterpret_cast<float4*>(p.y + (size_t)row * p.ldy + col);
+              if (p.accumulate) {
+                const float4 o = *dst;
+                *dst = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+              } else {
+                *dst = v;
+              }
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
         }
       }
-    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = n0 + wn0 + j * 32 + lr;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row < p.P && col < p.Cout) {
+            float* dst = p.y + (size_t)row * p.ldy + col;
+            *dst = p.accumulate ? *dst + acc[i][j][r] : acc[i][j][r];
+          }
+        }
+      }
+  }
   if (p.bn_part != nullptr) {         // fused BN-backward reduction of the layer below (see ConvParams)
     float* red = smem;                // [2][WM][BN]
     const int sb = wmi / WPS;

@@ -68,6 +68,7 @@ struct H3Args {
                            // as a by-product of the split for the weight-gradient kernel
   const float* in_scale;   // optional per-channel affine + ReLU applied to x0 in the split
   const float* in_shift;   // (the producing BatchNorm, fused; c1 == 0)
+  int wide;                // 1: the epilogue stores 16-B rows through LDS (ldy % 4 == 0, y 16-B aligned)
 };
 
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
@@ -377,7 +378,9 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     if (t == 123.f) p.y[tid] = t;
     return;
   }
-  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem);
+  // the halo buffer F is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
+                                 h.wide ? smem + 2 * WM * BN : nullptr);
 }
 
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
@@ -983,6 +986,7 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
   const int T = nbm * nbn;
   const size_t lds = h3_lds(BN, h.arows, TPS);
+  if ((size_t)h.arows * ROW2 < (size_t)(2 * WM * BN + WM * WN * 512) * 4) h.wide = 0;   // F too small to stage
   static int slots = [&] {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
@@ -1196,6 +1200,11 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "srpde_conv_fwd_h3: in_scale / in_shift go together and need c1 == 0");
   a.in_scale = in_scale;
   a.in_shift = in_shift;
+  static const int wide_on = [] {
+    const char* e = getenv("SRPDE_H3_WIDE");   // tuning/diagnostics: 0 = one dword store per element
+    return e ? atoi(e) : 1;
+  }();
+  a.wide = wide_on && ldy % 4 == 0 && aligned16(y);
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
                                           bn_ldy % 4 == 0 && cout % 4 == 0),
                   "srpde_conv_fwd_h3: the fused BN reduction needs bn_y/mean/invstd/gamma/beta and no accumulate");
