@@ -91,11 +91,6 @@ int srpde_conv_h3_stats_rows(void);
  * on 128-row tiles, two workgroups per CU (0: never).  Returns the previous value.  Tuning and
  * tests; the default comes from SRPDE_H3_HALF. */
 int srpde_conv_h3_set_half(int max_chunks);
-/* srpde_conv_fwd_h3 tile schedule: 0 = one tile per workgroup, 1 = persistent walk (one
- * workgroup per resident slot, each prefetching its next tile's first chunk during the current
- * tile's last one) once there are two rounds of tiles, >= 2 = that many persistent workgroups
- * (tests).  Returns the previous mode; the default comes from SRPDE_H3_PERSIST. */
-int srpde_conv_h3_set_persistent(int mode);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]

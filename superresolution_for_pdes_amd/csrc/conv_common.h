@@ -23,7 +23,6 @@ struct ConvParams {
   // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
   int ntail, tsplit;
   int dbg;              // diagnostics (SRPDE_CONV_DBG): 1 = x6 kernel skips the per-stage DMA
-  int pgrid = 0;        // h3 forward: workgroups walking the full tiles persistently (0: one tile per block)
   // x6p: the inputs as pre-split bf16 planes [3][P][c0] / [3][P][c1] (srpde_split_planes)
   const __bf16* x0p;
   const __bf16* x1p;

@@ -74,9 +74,7 @@ struct H3Args {
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
 // TPS: taps per stage (one barrier per stage; the weight stage holds TPS taps).
-// PERSIST: the persistent tile walk is compiled in (a separate instantiation: its longer live
-// ranges must not cost the one-tile-per-workgroup kernel registers)
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool PERSIST>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
 __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -106,20 +104,17 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int nbn = (p.Cout + BN - 1) / BN;
   const int nbm = (p.P + BM - 1) / BM;
   const int nfull = nbm * nbn - p.ntail;
-  // full tiles: block b < G walks the virtual tiles b, b + G, b + 2G, ... (G = p.pgrid for a
-  // persistent launch, else G = nfull: one tile per block); blocks from G on are the K-pieces of
-  // the split tail tiles
-  const int G = PERSIST && p.pgrid > 0 ? p.pgrid : nfull;
-  int vt = blockIdx.x, wg, piece = 0;
-  if ((int)blockIdx.x < G) {
-    wg = xcd_remap(vt, nfull);
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
   } else {
-    const int q = blockIdx.x - G;
+    const int q = blockIdx.x - nfull;
     wg = nfull + q / p.tsplit;
     piece = q - (q / p.tsplit) * p.tsplit;
   }
   const bool tail = wg >= nfull;
-  int m0 = 0, n0 = 0;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
   const int HW = p.H * p.W;
 
   if (tid < 16) reinterpret_cast<float*>(zrow)[tid] = 0.f;
@@ -136,71 +131,59 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int ea = h3_exp(ab);
   const float sa = exp2i(ea);
 
+  // per-lane tap masks of this wave's output rows
   const int lr = lane & 31, lh = lane >> 5;
   const int wmi = wave % WM, wni = wave / WM;
   const int wm0 = wmi * TM, wn0 = wni * TN;
-  // per-tile state: origins, the halo tile's first pixel, whether this tile stores the input
-  // split (N tile 0), and the per-lane tap masks of this wave's output rows
   unsigned tmask[TI];
-  int pix0 = 0;
-  bool wsplit = false;
-  auto set_tile = [&](int t) {
-    const int mt = t / nbn, nt = t - mt * nbn;
-    m0 = mt * BM;
-    n0 = nt * BN;
-    pix0 = m0 - h.halo;
-    wsplit = h.xsplit != nullptr && nt == 0;
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int m = m0 + wm0 + i * 32 + lr;
-      unsigned mask = 0;
-      if (m < p.P) {
-        const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
-        (void)n;
+  for (int i = 0; i < TI; ++i) {
+    const int m = m0 + wm0 + i * 32 + lr;
+    unsigned mask = 0;
+    if (m < p.P) {
+      const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
+      (void)n;
 #pragma unroll
-        for (int t9 = 0; t9 < 9; ++t9) {
-          const int iy = yy + (t9 / 3 - 1) * p.dil * p.sign, ix = xx + (t9 % 3 - 1) * p.dil * p.sign;
-          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t9;
-        }
+      for (int t = 0; t < 9; ++t) {
+        const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
       }
-      tmask[i] = mask;
     }
-  };
-  set_tile(wg);
-  // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1.
-  // b_off: byte offset for N-tile origin 0 (the tile's n0 * K is added at issue); -1: spare
-  int b_off[BPW], b_row[BPW];
+    tmask[i] = mask;
+  }
+  // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1
+  int b_off[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
     const int q = wave + j * NW;
     const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
     const int r = rb * 16 + (lane >> 2);
     const int c = swzh(r, lane & 3);
-    b_row[j] = r;
-    b_off[j] = q < BTOT ? (int)((pl * plane + (size_t)r * p.K + c * 8) * 2) : -1;
+    const int nn = n0 + r;
+    b_off[j] = (q < BTOT && nn < p.Cout) ? (int)((pl * plane + (size_t)nn * p.K + c * 8) * 2) : -1;
   }
 
   const int nch = p.Cin / BK2;
   const int c_beg = tail ? (piece * nch) / p.tsplit : 0;
   const int c_end = tail ? ((piece + 1) * nch) / p.tsplit : nch;
   const int na = arows / 8;                   // A DMA instructions per chunk (8 rows x 128 B)
+  const int pix0 = m0 - h.halo;
 
-  // A slice `q` of chunk `ch` of the halo tile that starts at pixel `pbase` (8 halo rows, fp32)
-  // into F; q >= na: a zero-fill DMA into the sink, so every wave issues the same number of
-  // vector-memory ops per stage (exact vmcnt counts)
-  auto issue_a = [&](int ch, int q, int pbase) {
+  // A slice `q` of chunk `ch` (8 halo rows, fp32) into F; q >= na: a zero-fill DMA into the sink,
+  // so every wave issues the same number of vector-memory ops per stage (exact vmcnt counts)
+  auto issue_a = [&](int ch, int q) {
     const int ch0 = ch * BK2;
     const bool second = ch0 >= p.c0;
     const int32x4 rs = second ? rs1 : rs0;
     const int ld = second ? ld1 : p.ldx0;
     const int cb = second ? ch0 - p.c0 : ch0;
     const int r = q * 8 + (lane >> 3);
-    const int pix = pbase + r;
+    const int pix = pix0 + r;
     const bool real = q < na;
     const unsigned off = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
     dma16(rs, off, lds_addr_of(real ? fbuf + q * 1024 : sink));
   };
-  auto issue_b = [&](int ch, int st, int buf, int nb0) {   // the TPS taps of stage `st` of chunk `ch`, N tile nb0
+  auto issue_b = [&](int ch, int st, int buf) {   // the TPS taps of stage `st` of chunk `ch`
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
       const int tap = st * TPS + u;
@@ -211,8 +194,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
         for (int j = 0; j < BPW; ++j) {
           const int q = wave + j * NW;
           if (q < BTOT) {
-            const unsigned off =
-                (b_off[j] >= 0 && nb0 + b_row[j] < p.Cout) ? (unsigned)(b_off[j] + (nb0 * p.K + k0) * 2) : OOB;
+            const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
             dma16(rsw, off, lds_addr_of(bbase + q * 1024));
           }
         }
@@ -221,6 +203,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   };
   // F (fp32, landed) -> S: scale and split every halo element once per chunk
   // (the N-tile-0 workgroup of each row tile also stores its own rows' pieces to h.xsplit)
+  const bool wsplit = h.xsplit != nullptr && nt == 0;
   const size_t xplane = (size_t)p.P * p.Cin;
   auto convert = [&](int ch) {
     for (int sg = tid; sg < arows * 4; sg += NT) {
@@ -261,10 +244,16 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     if constexpr (TWO_LEVEL) return part[i][j];
     else return acc[i][j];
   };
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // prologue: whole halo tile of the first chunk + first weight stage
-  for (int q = wave; q < na; q += NW) issue_a(c_beg, q, pix0);
-  issue_b(c_beg, 0, 0, n0);
+  for (int q = wave; q < na; q += NW) issue_a(c_beg, q);
+  issue_b(c_beg, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   convert(c_beg);
@@ -322,24 +311,17 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     }
     __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
   };
-  // the prefetch target past a tile's last chunk: chunk 0 of this workgroup's next tile
-  // (persistent launch; set per tile below)
-  bool has_next = false;
-  int npix0 = 0, nn0 = 0;
   auto stage = [&](int ch, auto st_tag) {
     constexpr int ST = decltype(st_tag)::value;
     // prefetch: the next weight stage, then AQ slices of the next chunk's halo tile (F is free:
-    // the current chunk was converted to S before its first stage); after a tile's last chunk
-    // the next chunk is the first chunk of the workgroup's next tile
+    // the current chunk was converted to S before its first stage)
     const bool more = ch + 1 < c_end;
-    const bool pref = more || has_next;
-    const int tch = more ? ch + 1 : c_beg, tpix = more ? pix0 : npix0, tn0 = more ? n0 : nn0;
     const bool dma = !(p.dbg & 1);   // diagnostics (SRPDE_CONV_DBG, results wrong): 1 = no DMA in the loop
-    if (dma && ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1, n0);
-    else if (dma && pref) issue_b(tch, 0, (sidx + 1) & 1, tn0);
-    if (dma && ST < NS - 1 && pref) {
+    if (dma && ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
+    else if (dma && more) issue_b(ch + 1, 0, (sidx + 1) & 1);
+    if (dma && ST < NS - 1 && more) {
 #pragma unroll
-      for (int u = 0; u < AQ; ++u) issue_a(tch, wave + (ST * AQ + u) * NW, tpix);
+      for (int u = 0; u < AQ; ++u) issue_a(ch + 1, wave + (ST * AQ + u) * NW);
     }
     const char* b = bbuf0 + (sidx & 1) * B_STAGE;
     tap_body(b, std::integral_constant<int, ST * TPS>{});
@@ -348,88 +330,57 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     ++sidx;
     // the next stage's weights must have landed; the halo slices issued after them may still be
     // in flight (they are waited for by the next stage's count, long before the chunk ends)
-    if (ST < NS - 1 && pref && h.relax)
+    if (ST < NS - 1 && more && h.relax)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!(p.dbg & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
   };
-  for (;;) {
-    // the workgroup's next tile (persistent launch): its first halo chunk and weight stage are
-    // prefetched during this tile's last chunk
-    const int vnext = vt + G;
-    has_next = PERSIST && !tail && vnext < nfull;
-    int nwg = 0;
-    if (has_next) {
-      nwg = xcd_remap(vnext, nfull);
-      const int nmt = nwg / nbn;
-      nn0 = (nwg - nmt * nbn) * BN;
-      npix0 = nmt * BM - h.halo;
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    stage(ch, std::integral_constant<int, 0>{});
+    if constexpr (NS > 1) stage(ch, std::integral_constant<int, 1>{});
+    if constexpr (NS > 2) stage(ch, std::integral_constant<int, 2>{});
+    if constexpr (NS > 3) stage(ch, std::integral_constant<int, 3>{});
+    if constexpr (NS > 4) stage(ch, std::integral_constant<int, 4>{});
+    if constexpr (NS > 5) stage(ch, std::integral_constant<int, 5>{});
+    if constexpr (NS > 6) stage(ch, std::integral_constant<int, 6>{});
+    if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
+    if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
+    // two-level accumulation: one partial chain per channel chunk (9 taps x 32 channels)
+    if constexpr (TWO_LEVEL) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
     }
+    if (ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
+      convert(ch + 1);                      // (diagnostics: 4 = no per-chunk convert)
+      __syncthreads();
+    }
+  }
+  // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact)
+  const float ia = exp2i(-ea);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    const float iw = col < p.Cout ? exp2i(-h.wexp[col]) : 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    for (int ch = c_beg; ch < c_end; ++ch) {
-      stage(ch, std::integral_constant<int, 0>{});
-      if constexpr (NS > 1) stage(ch, std::integral_constant<int, 1>{});
-      if constexpr (NS > 2) stage(ch, std::integral_constant<int, 2>{});
-      if constexpr (NS > 3) stage(ch, std::integral_constant<int, 3>{});
-      if constexpr (NS > 4) stage(ch, std::integral_constant<int, 4>{});
-      if constexpr (NS > 5) stage(ch, std::integral_constant<int, 5>{});
-      if constexpr (NS > 6) stage(ch, std::integral_constant<int, 6>{});
-      if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
-      if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
-      // two-level accumulation: one partial chain per channel chunk (9 taps x 32 channels)
-      if constexpr (TWO_LEVEL) {
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
-      }
-      if (ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
-        convert(ch + 1);                      // (diagnostics: 4 = no per-chunk convert)
-        __syncthreads();
-      }
-    }
-    // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact)
-    const float ia = exp2i(-ea);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + lr;
-      const float iw = col < p.Cout ? exp2i(-h.wexp[col]) : 0.f;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * iw;
-    }
-    if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) t += acc[i][j][0] + acc[i][j][15];
-      if (t == 123.f) p.y[tid] = t;
-      return;
-    }
-    const int cm0 = m0, cn0 = n0, cwg = wg;
-    if (PERSIST && has_next) {
-      // the next tile's first chunk landed during this tile's last stages (the final stage waited
-      // for every DMA): split it into S now; F then becomes the epilogue's scratch
-      vt = vnext;
-      wg = nwg;
-      set_tile(nwg);
-      if (!(p.dbg & 4)) convert(c_beg);
-      __syncthreads();
-    }
-    // the halo buffer F is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
-    x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, cwg, nfull, piece, cm0, cn0, wmi, wni, lane, smem,
-                                   h.wide ? smem + 2 * WM * BN : nullptr);
-    if (!PERSIST || !has_next) break;
-    __syncthreads();   // the epilogue's scratch reads are done before the next DMA into F
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * iw;
   }
+  if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] + acc[i][j][15];
+    if (t == 123.f) p.y[tid] = t;
+    return;
+  }
+  // the halo buffer F is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
+                                 h.wide ? smem + 2 * WM * BN : nullptr);
 }
 
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
@@ -1018,28 +969,6 @@ static int h3_half_max() {
 static size_t h3_lds(int bn, int arows, int tps = 1) {
   return (size_t)arows * (ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
 }
-// Persistent walk of the full tiles: mode 1 = one workgroup per resident slot once there are at
-// least two rounds of tiles; 0 = one tile per workgroup; >= 2 = that many workgroups (tests).
-// SRPDE_H3_PERSIST or srpde_conv_h3_set_persistent.
-static std::atomic<int> g_h3_persist{-1};
-static int h3_persist_mode() {
-  int v = g_h3_persist.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("SRPDE_H3_PERSIST");
-    v = e ? std::max(0, atoi(e)) : 0;
-    int expect = -1;
-    g_h3_persist.compare_exchange_strong(expect, v);
-    v = g_h3_persist.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-static int h3_pgrid(int nfull, int slots) {
-  const int m = h3_persist_mode();
-  if (m == 0) return 0;
-  const int g = m == 1 ? slots : m;
-  return nfull >= 2 * g ? g : 0;
-}
-
 // taps per stage: the most (<= SRPDE_H3_TPS, default 2) whose weight double-buffer fits in LDS
 static int h3_tps(int bn, int arows) {
   static const int want = [] {
@@ -1070,13 +999,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   const int nch = p.Cin / BK2;
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
-  const int nfull = T - p.ntail;
-  p.pgrid = h3_pgrid(nfull, slots);
-  const int grid = (p.pgrid > 0 ? p.pgrid : nfull) + p.ntail * p.tsplit;
-  if (p.pgrid > 0)
-    hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, true>), dim3(grid), dim3(NT), lds, st, p, h);
-  else
-    hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, false>), dim3(grid), dim3(NT), lds, st, p, h);
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS>), dim3(grid), dim3(NT), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -1189,12 +1113,6 @@ using namespace srpde;
 extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
-
-int srpde_conv_h3_set_persistent(int mode) {
-  const int prev = h3_persist_mode();
-  g_h3_persist.store(std::max(0, mode));
-  return prev;
-}
 
 int srpde_conv_h3_set_half(int max_chunks) {
   const int prev = h3_half_max();

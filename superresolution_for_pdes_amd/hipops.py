@@ -104,12 +104,6 @@ def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
     return buf, nblk, rows
 
 
-def set_h3_persistent(mode: int) -> int:
-    """h3 tile schedule: 0 one tile per workgroup, 1 persistent walk, >= 2 that many persistent
-    workgroups (tests).  Returns the previous mode."""
-    return int(query("srpde_conv_h3_set_persistent", int(mode)))
-
-
 def set_h3_half(max_chunks: int) -> int:
     """h3 tile choice: input depth (in 32-channel chunks) up to which the 128-row, two-per-CU
     tile runs (0: never).  Returns the previous value."""

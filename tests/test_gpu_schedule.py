@@ -87,66 +87,3 @@ def test_conv_h3_half_tiles_equal_full_tiles(n, c0, c1, cout, hw, dil):
         H.set_h3_half(prev)
     for k, (a, b_) in enumerate(zip(*outs)):
         assert torch.equal(a, b_), k
-
-
-@pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (8, 256, 0, 512, 10, 2),
-                                                 (16, 256, 128, 128, 20, 1), (48, 64, 0, 64, 40, 1),
-                                                 (8, 64, 0, 32, 40, 1)])
-def test_conv_h3_persistent_equals_one_tile_per_block(n, c0, c1, cout, hw, dil):
-    """The persistent walk (each workgroup computes a sequence of tiles, prefetching the next
-    tile's first chunk) writes exactly what one-tile-per-workgroup writes.  (48, ...) has a
-    K-split tail round behind the persistent workgroups; (8, 256, 0, 512, ...) walks N tiles."""
-    from superresolution_for_pdes_amd import hipops as H
-    if H.conv_math() != "h3" or not (H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, c0 + c1, hw, dil)):
-        pytest.skip("not an h3 shape")
-    g = torch.Generator(device=DEV).manual_seed(4)
-    P, cin = n * hw * hw, c0 + c1
-    x = torch.randn(P, cin, device=DEV, generator=g)
-    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
-    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
-    b = torch.randn(cout, device=DEV, generator=g)
-    wf, wd = H.pack_conv_weights(w, cin, True, True)
-    dy = torch.randn(P, cout, device=DEV, generator=g)
-    for t in (x0, x1, dy):
-        if t is not None:
-            t._srpde_amax = H.amax_of(t)
-    outs = []
-    prev = H.set_h3_persistent(0)
-    try:
-        for mode in (0, 5, 3):
-            H.set_h3_persistent(mode)
-            y = torch.empty(P, cout, device=DEV)
-            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
-            xp = H.split_planes_buffer(P, cin, DEV)
-            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
-            dx = torch.empty(P, cin, device=DEV)
-            dyp = H.split_planes_buffer(P, cout, DEV)
-            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
-            torch.cuda.synchronize()
-            outs.append((y, stats, xp, dx, dyp))
-    finally:
-        H.set_h3_persistent(prev)
-    for other in outs[1:]:
-        for k, (a, b_) in enumerate(zip(outs[0], other)):
-            assert torch.equal(a, b_), k
-
-
-def test_unet_step_persistent_and_side_stream_bit_identical():
-    from superresolution_for_pdes_amd import hipops as H
-    from superresolution_for_pdes_amd.models import UNet, init_weights
-    torch.manual_seed(1)
-    ref = UNet()
-    ref.apply(init_weights)
-    state = {k: v.clone() for k, v in ref.state_dict().items()}
-    x = torch.randn(8, 3, 40, 40, generator=torch.Generator().manual_seed(6)).to(DEV)
-    x[:, 1] = 1.0
-    prev = H.set_h3_persistent(0)
-    try:
-        a = _train_step(x, state, False)
-        H.set_h3_persistent(3)
-        b = _train_step(x, state, True)
-    finally:
-        H.set_h3_persistent(prev)
-    assert torch.equal(a[0], b[0])
-    for n in a[1]:
-        assert torch.equal(a[1][n], b[1][n]), n
