@@ -174,12 +174,21 @@ int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, in
                                 int c, hipStream_t stream);
 int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
                                 int wo, int c, int accumulate, hipStream_t stream);
+/* srpde_upsample_bilinear_bwd of (dout + dsa (x) wg): the attention gating gradient
+ * dg[q][c] += dsa[q] * wg[c] (models.py:116, srpde_att_bwd called with dg == NULL leaves dsa in
+ * workspace[0, P)) folded into the upsample backward that consumes dg (models.py:89,92), so the
+ * gating gradient is never written.  Needs c / 4 a power of two <= 256. */
+int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
+                                      int lddx, int n, int h, int w, int ho, int wo, int c, int accumulate,
+                                      hipStream_t stream);
 
 /* ---- AttentionGate.forward / backward (src/models.py:103-130) ----------------------- */
 int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,
                   const float* b1, const float* w2, const float* b2, const float* wg, const float* bg, float* m,
                   float* hbuf, float* ca, float* sa, float* out, int ldo, hipStream_t stream);
 size_t srpde_att_bwd_workspace_size(int n, int hw, int c, int gc);
+/* dg == NULL: the gating gradient is not written; workspace[0, n*hw) floats then holds dsa (the
+ * spatial gate's pre-sigmoid gradient) for srpde_upsample_bilinear_bwd_gated. */
 int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const float* g, int ldg, int n, int hw,
                   int c, int gc, const float* w1, const float* w2, const float* wg, const float* m, const float* hbuf,
                   const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,

@@ -280,9 +280,13 @@ __global__ __launch_bounds__(256) void upsample_fwd_px_kernel(const float* __res
   *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
 }
 
+// gsa / gw (nullable): the attention gating gradient folded in, the upsampled tensor's gradient
+// being dout[q][c] + gsa[q] * gw[c] (srpde_upsample_bilinear_bwd_gated)
 __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __restrict__ dout, int lddo,
                                                               float* __restrict__ dx, int lddx, unsigned npix, int H,
-                                                              int W, int Ho, int Wo, int accumulate) {
+                                                              int W, int Ho, int Wo, int accumulate,
+                                                              const float* __restrict__ gsa = nullptr,
+                                                              const float* __restrict__ gw = nullptr) {
   const unsigned q = px_index();
   if (q >= npix) return;
   const unsigned ix = q % (unsigned)W, t = q / (unsigned)W, iy = t % (unsigned)H, n = t / (unsigned)H;
@@ -293,10 +297,16 @@ __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __res
   const int nx = gather_weights(ix, W, Wo, oxi, wx);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* base = dout + (size_t)n * Ho * Wo * lddo + c;
+  const float4 wv = gw != nullptr ? *reinterpret_cast<const float4*>(gw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* sbase = gsa != nullptr ? gsa + (size_t)n * Ho * Wo : nullptr;
   for (int a = 0; a < ny; ++a) {
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int b = 0; b < nx; ++b) {
-      const float4 g = *reinterpret_cast<const float4*>(base + (size_t)(oyi[a] * Wo + oxi[b]) * lddo);
+      float4 g = *reinterpret_cast<const float4*>(base + (size_t)(oyi[a] * Wo + oxi[b]) * lddo);
+      if (sbase != nullptr) {
+        const float sv = sbase[oyi[a] * Wo + oxi[b]];
+        g.x = sv * wv.x + g.x; g.y = sv * wv.y + g.y; g.z = sv * wv.z + g.z; g.w = sv * wv.w + g.w;
+      }
       r.x += wx[b] * g.x; r.y += wx[b] * g.y; r.z += wx[b] * g.z; r.w += wx[b] * g.w;
     }
     s.x += wy[a] * r.x; s.y += wy[a] * r.y; s.z += wy[a] * r.z; s.w += wy[a] * r.w;
@@ -790,6 +800,20 @@ int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, in
   return 0;
 }
 
+int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
+                                      int lddx, int n, int h, int w, int ho, int wo, int c, int accumulate,
+                                      hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && dsa && wg && dx && c % 4 == 0 && lddo % 4 == 0 && lddx % 4 == 0 && ho >= h && wo >= w,
+                  "srpde_upsample_bilinear_bwd_gated: bad args");
+  dim3 g, b;
+  SRPDE_CHECK_ARG(px_geometry((long long)n * h * w, c, &g, &b),
+                  "srpde_upsample_bilinear_bwd_gated: needs c / 4 a power of two <= 256 (c=%d)", c);
+  hipLaunchKernelGGL(upsample_bwd_px_kernel, g, b, 0, stream, dout, lddo, dx, lddx, (unsigned)(n * h * w), h, w, ho,
+                     wo, accumulate, dsa, wg);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd_gated");
+  return 0;
+}
+
 int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
                                 int wo, int c, int accumulate, hipStream_t stream) {
   SRPDE_CHECK_ARG(dout && dx && c % 4 == 0 && ho >= h && wo >= w, "srpde_upsample_bilinear_bwd: bad args");
@@ -844,7 +868,7 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                   const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
                   int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
                   void* workspace, size_t ws_bytes, hipStream_t stream) {
-  SRPDE_CHECK_ARG(dout && x && g && dx && dg && workspace, "srpde_att_bwd: null");
+  SRPDE_CHECK_ARG(dout && x && g && dx && workspace, "srpde_att_bwd: null");
   SRPDE_CHECK_ARG(c % 32 == 0 && gc % 4 == 0, "srpde_att_bwd: channel counts");
   if (ws_bytes < srpde_att_bwd_workspace_size(n, hw, c, gc)) {
     set_error("srpde_att_bwd: workspace too small");
@@ -871,9 +895,11 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
   hipLaunchKernelGGL(att_bwd_dx_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, lddo, ca, sa, dm,
                      dx, lddx, P, hw, c, dx_accumulate);
   SRPDE_LAUNCH_CHECK("srpde_att_bwd(dx)");
-  hipLaunchKernelGGL(att_bwd_gating_kernel, dim3(grid_for(P * (gc / 4))), dim3(256), 0, stream, dsa, wg, dg, lddg, P,
-                     gc, dg_accumulate);
-  SRPDE_LAUNCH_CHECK("srpde_att_bwd(gating)");
+  if (dg != nullptr) {   // else the caller folds dg = dsa * wg into its consumer (workspace[0, P) = dsa)
+    hipLaunchKernelGGL(att_bwd_gating_kernel, dim3(grid_for(P * (gc / 4))), dim3(256), 0, stream, dsa, wg, dg, lddg,
+                       P, gc, dg_accumulate);
+    SRPDE_LAUNCH_CHECK("srpde_att_bwd(gating)");
+  }
   // parameter grads: fixed-order sums over samples / pixel blocks
   (void)dw1r; (void)dw2r;
   // dW1[r][c] = sum_n dh[n][r] m[n][c];  dW2[c][r] = sum_n dpre[n][c] h[n][r]

@@ -378,9 +378,16 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
 
 
-def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate):
+def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate, gate=None):
+    """``gate = (dsa, wg)``: the upsampled tensor's gradient is dout + dsa (x) wg (the attention
+    gating gradient left unapplied by att_bwd(dg=None))."""
     pdo, lddo = _pl(dout)
     pdx, lddx = _pl(dx)
+    if gate is not None:
+        dsa, wg = gate
+        call("srpde_upsample_bilinear_bwd_gated", pdo, lddo, dsa.data_ptr(), wg.data_ptr(), pdx, lddx, n, h, w, ho,
+             wo, dx.shape[1], int(accumulate), stream_ptr())
+        return
     call("srpde_upsample_bilinear_bwd", pdo, lddo, pdx, lddx, n, h, w, ho, wo, dx.shape[1], int(accumulate),
          stream_ptr())
 
@@ -414,11 +421,14 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
     px, ldx = _pl(x)
     pg, ldg = _pl(g)
     pdx, lddx = _pl(dx)
-    pdg, lddg = _pl(dg)
+    pdg, lddg = _pl(dg) if dg is not None else (0, 0)
     call("srpde_att_bwd", pdo, lddo, px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), w2.data_ptr(), wg.data_ptr(),
          m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(), pdx, lddx, int(dx_acc), pdg, lddg, int(dg_acc),
          dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr(),
          ws.data_ptr(), ws_bytes, stream_ptr())
+    if dg is None:   # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
+        return ws[:4 * x.shape[0]].view(torch.float32)
+    return None
 
 
 # ------------------------------------- head ----------------------------------------

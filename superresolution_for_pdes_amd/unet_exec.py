@@ -297,9 +297,12 @@ def _att_fwd(att, x, g, n, hw):
 
 
 def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc):
+    """``dg=None``: the gating gradient is not applied; returns the gate for upsample_bwd."""
     c1, c3, s0 = _att_params(att)
-    H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
-              grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight], grads[s0.bias])
+    dsa = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
+                    grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
+                    grads[s0.bias])
+    return None if dsa is None else (dsa, s0.weight)
 
 
 def check_input(x):
@@ -382,19 +385,21 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1, wq=wq)
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
-    _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, dcat1[:, :128], True)
+    # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below
+    gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, None, True)
     ready("att1")
     dd2 = H.empty(P2, 128, device=dev)
-    H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False)
+    H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate)
     # dec2: grad of cat[u3 (256), e2a (128)]
     dcat2 = H.empty(P2, 384, device=dev)
     _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2, wq=wq)
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
-    _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, dcat2[:, :256], True)
+    # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
+    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, None, True)
     ready("att2")
     dd3 = H.empty(P3, 256, device=dev)
-    H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False)
+    H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate)
     # dec3: grad of cat[b (512), e3a (256)]
     dcat3 = H.empty(P3, 768, device=dev)
     _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq)

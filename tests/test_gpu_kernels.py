@@ -233,6 +233,26 @@ def test_pool_upsample():
     assert rel(unrows(dxu, n, h, h), uv.grad) < 1e-6
 
 
+@pytest.mark.parametrize("c,h", [(128, 20), (256, 10)])
+def test_upsample_bwd_with_gating_gradient(c, h):
+    """upsample_bwd(gate=(dsa, wg)) == the upsample backward of dout + dsa (x) wg (the attention
+    gating gradient, models.py:116, folded into its consumer, models.py:89/92)."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(11)
+    n, ho = 3, 2 * h
+    x = torch.randn(n, c, h, h, generator=g).requires_grad_(True)
+    u = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
+    du = torch.randn(n, c, ho, ho, generator=g)
+    dsa = torch.randn(n, 1, ho, ho, generator=g)
+    wg = torch.randn(c, generator=g)
+    u.backward(du + dsa * wg.view(1, c, 1, 1))
+    dx = H.empty(n * h * h, c, device=DEV)
+    H.upsample_bwd(rows(du).to(DEV), dx, n, h, h, ho, ho, False,
+                   gate=(dsa.reshape(-1).contiguous().to(DEV), wg.to(DEV)))
+    torch.cuda.synchronize()
+    assert rel(unrows(dx, n, h, h), x.grad) < 1e-6
+
+
 @pytest.mark.parametrize("c,gc,h", [(256, 512, 10), (64, 128, 40)])
 def test_attention(c, gc, h):
     from superresolution_for_pdes_amd import hipops as H
