@@ -39,6 +39,17 @@ CONV3 = [("enc1.conv1", 3, 64, 40), ("enc1.conv2", 64, 64, 40), ("enc2.conv1", 6
          ("out_conv2", 32, 16, 40)]
 
 
+_JSON_OUT = None
+
+
+def emit(rec):
+    """The one JSON line, on the process's original stdout (see main: library banners such as
+    RCCL's version block are moved to stderr so stdout carries only this line)."""
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(rec) + "\n")
+    out.flush()
+
+
 def conv_flops(cin, cout, hw):
     return 2.0 * cout * cin * 9 * hw * hw
 
@@ -167,7 +178,7 @@ def run_poisson(args, world, rank, dev):
         rec["cpu_baseline"] = {"value": round(cb[80], 2), "unit": "solves/s", "cores": 1, "kind": "port",
                                "sample": "scipy spsolve(diag(theta) L, f) per problem (the reference's call), "
                                          + ", ".join(f"n={n}: {v:.1f}/s" for n, v in cb.items())}
-    print(json.dumps(rec), flush=True)
+    emit(rec)
 
 
 def cpu_baseline_cascade(st, data, seconds):
@@ -262,11 +273,16 @@ def run_cascade(args, world, rank, dev):
     if not args.no_cpu_baseline and world == 1:
         st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         rec["cpu_baseline"] = cpu_baseline_cascade(st, data, args.cpu_seconds)
-    print(json.dumps(rec), flush=True)
+    emit(rec)
 
 
 def main():
+    global _JSON_OUT
     args = parse()
+    # RCCL prints its version block on fd 1 at communicator creation: keep fd 1 for the JSON line
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -390,7 +406,7 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        print(json.dumps(rec), flush=True)
+        emit(rec)
     if use_pg:
         dist.destroy_process_group()
 
