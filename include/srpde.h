@@ -194,6 +194,13 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                   const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
                   int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
                   void* workspace, size_t ws_bytes, hipStream_t stream);
+/* The parameter-gradient half of srpde_att_bwd (dW1, db1, dW2, db2 of the channel MLP, dwg, dbg of
+ * the spatial gate: fixed-order reductions over samples / pixel blocks of the per-sample rows it
+ * left in `workspace`).  srpde_att_bwd with dw1 == NULL stops before it, so a caller can queue
+ * these reductions on another stream (nothing downstream in the backward reads them). */
+int srpde_att_bwd_params(const float* g, int ldg, int n, int hw, int c, int gc, const float* m, const float* hbuf,
+                         float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg, void* workspace,
+                         size_t ws_bytes, hipStream_t stream);
 
 /* ---- output head: final 1x1 conv + residual x[:,0:1] (models.py:61,74,98,101) ------- */
 int srpde_head_fwd(const float* z, int ldz, int c, const float* wf, const float* bf, const float* xin, int xin_c,

@@ -900,6 +900,30 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                        P, gc, dg_accumulate);
     SRPDE_LAUNCH_CHECK("srpde_att_bwd(gating)");
   }
+  if (dw1 == nullptr) return 0;   // parameter gradients later: srpde_att_bwd_params
+  return srpde_att_bwd_params(g, ldg, n, hw, c, gc, m, hbuf, dw1, db1, dw2, db2, dwg, dbg, workspace, ws_bytes,
+                              stream);
+}
+
+int srpde_att_bwd_params(const float* g, int ldg, int n, int hw, int c, int gc, const float* m, const float* hbuf,
+                         float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg, void* workspace,
+                         size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(g && m && hbuf && dw1 && db1 && dw2 && db2 && dwg && dbg && workspace,
+                  "srpde_att_bwd_params: null");
+  if (ws_bytes < srpde_att_bwd_workspace_size(n, hw, c, gc)) {
+    set_error("srpde_att_bwd_params: workspace too small");
+    return kErrWorkspace;
+  }
+  const long long P = (long long)n * hw;
+  const int cr = c / 8;
+  float* dsa = static_cast<float*>(workspace);
+  float* dm = dsa + P;
+  float* dw1r = dm + (size_t)n * c;
+  float* dw2r = dw1r + (size_t)n * cr * c;
+  float* db1r = dw2r + (size_t)n * cr * c;
+  float* db2r = db1r + (size_t)n * cr;
+  float2* part = reinterpret_cast<float2*>(db2r + (size_t)n * c + 2);
+  part = reinterpret_cast<float2*>((reinterpret_cast<uintptr_t>(part) + 15) & ~uintptr_t(15));
   // parameter grads: fixed-order sums over samples / pixel blocks
   (void)dw1r; (void)dw2r;
   // dW1[r][c] = sum_n dh[n][r] m[n][c];  dW2[c][r] = sum_n dpre[n][c] h[n][r]

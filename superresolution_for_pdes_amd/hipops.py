@@ -412,7 +412,12 @@ def att_fwd(x, g, n, hw, w1, b1, w2, b2, wg, bg, out=None):
     return out, (m, hb, ca, sa)
 
 
-def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg):
+def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg,
+            defer_params=False):
+    """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None) is the
+    gating gradient's per-pixel factor for upsample_bwd(gate=...); ``params`` (when
+    ``defer_params``) is a callable that launches the parameter-gradient reductions on the
+    current stream, to be queued after this call (reads ``ws``, ``g``, ``m``, ``hb``)."""
     m, hb, ca, sa = saved
     c, gc = x.shape[1], g.shape[1]
     ws_bytes = int(query("srpde_att_bwd_workspace_size", n, hw, c, gc))
@@ -422,13 +427,19 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
     pg, ldg = _pl(g)
     pdx, lddx = _pl(dx)
     pdg, lddg = _pl(dg) if dg is not None else (0, 0)
+    pgrads = (dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr())
     call("srpde_att_bwd", pdo, lddo, px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), w2.data_ptr(), wg.data_ptr(),
          m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(), pdx, lddx, int(dx_acc), pdg, lddg, int(dg_acc),
-         dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr(),
-         ws.data_ptr(), ws_bytes, stream_ptr())
-    if dg is None:   # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
-        return ws[:4 * x.shape[0]].view(torch.float32)
-    return None
+         *((0,) * 6 if defer_params else pgrads), ws.data_ptr(), ws_bytes, stream_ptr())
+    params = None
+    if defer_params:
+        def params():
+            call("srpde_att_bwd_params", pg, ldg, n, hw, c, gc, m.data_ptr(), hb.data_ptr(), *pgrads, ws.data_ptr(),
+                 ws_bytes, stream_ptr())
+        params.keep = (ws,)
+    # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
+    dsa = ws[:4 * x.shape[0]].view(torch.float32) if dg is None else None
+    return dsa, params
 
 
 # ------------------------------------- head ----------------------------------------

@@ -296,12 +296,15 @@ def _att_fwd(att, x, g, n, hw):
     return out, saved
 
 
-def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc):
-    """``dg=None``: the gating gradient is not applied; returns the gate for upsample_bwd."""
+def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None):
+    """``dg=None``: the gating gradient is not applied; returns the gate for upsample_bwd.
+    ``wq``: the parameter-gradient reductions go to the weight-gradient side stream."""
     c1, c3, s0 = _att_params(att)
-    dsa = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
-                    grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
-                    grads[s0.bias])
+    dsa, params = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
+                            grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
+                            grads[s0.bias], defer_params=wq is not None)
+    if params is not None:
+        wq.submit(params, params.keep)
     return None if dsa is None else (dsa, s0.weight)
 
 
@@ -386,7 +389,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
     # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below
-    gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, None, True)
+    gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, None, True, wq=wq)
     ready("att1")
     dd2 = H.empty(P2, 128, device=dev)
     H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate)
@@ -396,7 +399,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
     # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
-    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, None, True)
+    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, None, True, wq=wq)
     ready("att2")
     dd3 = H.empty(P3, 256, device=dev)
     H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate)
@@ -405,7 +408,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq)
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)
-    _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True)
+    _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True, wq=wq)
     ready("att3")
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
