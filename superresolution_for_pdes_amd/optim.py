@@ -32,6 +32,16 @@ def _flat_span(tensors):
     return torch.empty(0, dtype=t0.dtype, device=t0.device).set_(t0.untyped_storage(), start, (off,), (1,))
 
 
+# bumped by every FusedAdamW.step: the update runs in a HIP kernel, which torch's tensor
+# version counters do not see, so caches keyed on parameter values (unet_exec's eval-mode
+# weight split) key on this as well
+_STEPS = [0]
+
+
+def step_count() -> int:
+    return _STEPS[0]
+
+
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, max_grad_norm=None):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -102,6 +112,7 @@ class FusedAdamW(torch.optim.Optimizer):
             self.clip_grad_norm_(mgn, grad_scale)
         coef = self._coef if getattr(self, "_pending", False) else None
         self._pending = False
+        _STEPS[0] += 1
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:

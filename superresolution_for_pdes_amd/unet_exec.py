@@ -112,7 +112,16 @@ def prepare_h3_weights(m):
         cache = (sig, torch.tensor(desc, dtype=torch.int64, device=dev), len(desc), rows, keep)
         m._srpde_h3w = cache
     _, desc_t, nl, rows, _ = cache
+    # eval mode: the split stays valid until a weight changes (in place through torch: version
+    # counters; through FusedAdamW's kernel: its step count); train mode re-splits every forward
+    key = None
+    if not m.training:
+        from .optim import step_count
+        key = (sig, tuple(c.weight._version for c in convs), step_count())
+        if getattr(m, "_srpde_h3w_key", None) == key:
+            return
     H.prepare_weights_h3(desc_t, nl, rows)
+    m._srpde_h3w_key = key
 
 
 def _fwd_weights(conv, cin, c0, c1, w, dil):

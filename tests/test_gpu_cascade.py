@@ -57,3 +57,24 @@ def test_cascade_20_to_640_shapes_and_batching():
     out2 = ml_multi_level_upscale(m, data, 80, "cuda", start_resolution=20, max_batch=1)
     out3 = ml_multi_level_upscale(m, data, 80, "cuda", start_resolution=20)
     assert np.max(np.abs(out2 - out3)) <= 1e-6 * np.abs(out3).max()
+
+
+def test_cascade_graph_replay_is_bit_identical_and_tracks_weights():
+    """eval_forward's HIP-graph replay == the eager forward, bit for bit; after a weight change
+    the graph is re-captured (the eval weight split's cache key changes)."""
+    from superresolution_for_pdes_amd.models import UNet
+    from superresolution_for_pdes_amd.resolution_comparison import ml_multi_level_upscale, solve_multi_resolution
+    np.random.seed(2)
+    data = solve_multi_resolution(20, [40, 80, 160])
+    m = UNet()
+    m.load_state_dict(fixture_state_torch())
+    m = m.cuda().eval()
+    eager = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20, graphs=False)
+    g1 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
+    g2 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
+    assert np.array_equal(eager, g1) and np.array_equal(g1, g2)
+    with torch.no_grad():
+        m.final.weight.mul_(0.5)          # in place: bumps the version counter
+    eager2 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20, graphs=False)
+    g3 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
+    assert np.array_equal(eager2, g3) and not np.array_equal(g3, g1)
