@@ -159,7 +159,8 @@ def eval_forward(model, x: torch.Tensor, graphs: bool = True) -> torch.Tensor:
     cache = model.__dict__.setdefault("_srpde_graphs", {})
     ent = cache.get(key)
     if ent is None or key[2] is None:
-        cache.clear()
+        for k in [k for k in cache if k[2] != key[2]]:   # graphs of older weights
+            del cache[k]
         xs = x.clone()
         with torch.no_grad():
             model(xs)                        # warm-up: lazily created scratch exists before capture

@@ -73,6 +73,9 @@ def test_cascade_graph_replay_is_bit_identical_and_tracks_weights():
     g1 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
     g2 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
     assert np.array_equal(eager, g1) and np.array_equal(g1, g2)
+    graphs = dict(m._srpde_graphs)
+    ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
+    assert len(graphs) == 3 and all(m._srpde_graphs[k] is v for k, v in graphs.items()), "graphs re-captured"
     with torch.no_grad():
         m.final.weight.mul_(0.5)          # in place: bumps the version counter
     eager2 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20, graphs=False)
