@@ -47,12 +47,15 @@ def solve_multi_resolution(n_coarse: int = 40, resolutions: List[int] = (80, 160
 class GlobalNormalization:
     """resolution_comparison.py:160-181 (fp32 statistics, unbiased std)."""
 
-    def __init__(self, u_fine, u_coarse, f_fine, theta_fine, device="cuda"):
+    def __init__(self, u_fine, u_coarse, f_fine, theta_fine, device="cuda", theta_is_constant=None):
+        """``theta_is_constant``: the reference's std < 1e-6 test, if already known (the test is
+        a host sync; a graph-captured cascade takes it from its capture)."""
         t = lambda a: _field(a, device, torch.float32)  # noqa: E731
         u_fine, f_fine, theta_fine = t(u_fine), t(f_fine), t(theta_fine)
         self.u_mean, self.u_std = u_fine.mean(), u_fine.std()
         self.f_mean, self.f_std = f_fine.mean(), f_fine.std()
-        self.theta_is_constant = bool(theta_fine.std() < 1e-6)
+        self.theta_is_constant = (bool(theta_fine.std() < 1e-6) if theta_is_constant is None
+                                  else bool(theta_is_constant))
         if self.theta_is_constant:
             self.theta_mean, self.theta_std = 0, 1
         else:
@@ -189,6 +192,60 @@ def ml_multi_level_upscale(model, data: dict, target_resolution: int, device: st
     no other exchange.  ``shard`` = (rank, world); default: the torch.distributed world."""
     model.eval()
     rank, world = _shard(shard)
+    levels = []
+    r = start_resolution
+    while r < target_resolution:
+        r *= 2
+        levels.append(r)
+    if graphs and world == 1 and torch.device(device).type == "cuda" and all(
+            isinstance(data[k][r], torch.Tensor) and data[k][r].is_cuda
+            for k in ("u", "f", "theta") for r in levels + [start_resolution] if k == "u" or r != start_resolution):
+        out = _cascade_graphed(model, data, target_resolution, start_resolution, tile, max_batch, levels, device)
+    else:
+        out = _cascade(model, data, target_resolution, start_resolution, tile, max_batch, rank, world, device,
+                       graphs)
+    return out if return_tensor else out.cpu().numpy()
+
+
+def _cascade_graphed(model, data, target_resolution, start_resolution, tile, max_batch, levels, device):
+    """The whole cascade (statistics, tiling, five U-Net forwards, stitching) captured once into
+    one HIP graph per (data tensors, geometry, weights) and replayed; the theta-constant tests
+    (host syncs) run once, at capture.  Bit-identical to the eager cascade."""
+    from . import unet_exec as X
+    with torch.no_grad():
+        model.flatten_parameters_()
+        X.prepare_h3_weights(model)
+    wkey = getattr(model, "_srpde_h3w_key", None)
+    sig = tuple((k, r, data[k][r].data_ptr(), data[k][r]._version) for k in ("u", "f", "theta")
+                for r in sorted(data[k]) if r in levels or (k == "u" and r == start_resolution))
+    key = ("cascade", target_resolution, start_resolution, tile, max_batch, sig, wkey)
+    cache = model.__dict__.setdefault("_srpde_graphs", {})
+    ent = cache.get(key) if wkey is not None else None
+    if ent is None:
+        for k in [k for k in cache if k[0] == "cascade"]:   # one cascade graph at a time
+            del cache[k]
+        flags = {r: bool(_field(data["theta"][r], device, torch.float32).std() < 1e-6) for r in levels}
+
+        def run():
+            return _cascade(model, data, target_resolution, start_resolution, tile, max_batch, 0, 1, device,
+                            False, flags)
+        with torch.no_grad():
+            run()                               # warm-up (lazily created buffers exist before capture)
+            torch.cuda.current_stream(torch.device(device)).synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = run()
+        ent = (g, out)
+        if wkey is not None:
+            cache[key] = ent
+    g, out = ent
+    g.replay()
+    return out.clone()
+
+
+def _cascade(model, data, target_resolution, start_resolution, tile, max_batch, rank, world, device, graphs,
+             flags=None):
+    """The level loop of ml_multi_level_upscale (eager launches; per-level graphs if ``graphs``)."""
     cur_res = start_resolution
     cur = _field(data["u"][cur_res], device, torch.float64)[None]   # [nb, S, S] blocks
     roots, m_split = None, None     # owned root-tile indices, tiles per side at the split level
@@ -197,7 +254,8 @@ def ml_multi_level_upscale(model, data: dict, target_resolution: int, device: st
     norms, r = {}, cur_res
     while r < target_resolution:
         r *= 2
-        norms[r] = GlobalNormalization(data["u"][r], None, data["f"][r], data["theta"][r], device=device)
+        norms[r] = GlobalNormalization(data["u"][r], None, data["f"][r], data["theta"][r], device=device,
+                                       theta_is_constant=None if flags is None else flags[r])
     while cur_res < target_resolution:
         nxt = cur_res * 2
         if roots is None and world > 1 and (cur_res // tile) ** 2 >= world:
@@ -219,8 +277,7 @@ def ml_multi_level_upscale(model, data: dict, target_resolution: int, device: st
         cur_res = nxt
     if roots is not None:
         cur = _gather_blocks(cur, m_split, world)
-    out = cur[0] if cur.shape[0] == 1 else _tiles_to_blocks(cur, 1)[0]
-    return out if return_tensor else out.cpu().numpy()
+    return cur[0] if cur.shape[0] == 1 else _tiles_to_blocks(cur, 1)[0]
 
 
 def _gather_blocks(blocks: torch.Tensor, m_split: int, world: int) -> torch.Tensor:

@@ -81,3 +81,27 @@ def test_cascade_graph_replay_is_bit_identical_and_tracks_weights():
     eager2 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20, graphs=False)
     g3 = ml_multi_level_upscale(m, data, 160, "cuda", start_resolution=20)
     assert np.array_equal(eager2, g3) and not np.array_equal(g3, g1)
+
+
+def test_whole_cascade_graph_on_device_fields():
+    """Device-resident fields take the whole-cascade graph (one replay per call): equal bits to the
+    eager cascade, replays without re-capture, and re-capture after a weight change."""
+    from superresolution_for_pdes_amd.models import UNet
+    from superresolution_for_pdes_amd.resolution_comparison import ml_multi_level_upscale, solve_multi_resolution
+    np.random.seed(3)
+    data = solve_multi_resolution(20, [40, 80, 160])
+    dd = {k: {r: torch.as_tensor(v).cuda() for r, v in data[k].items()} for k in ("u", "f", "theta")}
+    m = UNet()
+    m.load_state_dict(fixture_state_torch())
+    m = m.cuda().eval()
+    eager = ml_multi_level_upscale(m, dd, 160, "cuda", start_resolution=20, graphs=False, return_tensor=True)
+    g1 = ml_multi_level_upscale(m, dd, 160, "cuda", start_resolution=20, return_tensor=True)
+    ent = [v for k, v in m._srpde_graphs.items() if k[0] == "cascade"]
+    g2 = ml_multi_level_upscale(m, dd, 160, "cuda", start_resolution=20, return_tensor=True)
+    assert len(ent) == 1 and [v for k, v in m._srpde_graphs.items() if k[0] == "cascade"][0] is ent[0]
+    assert torch.equal(eager, g1) and torch.equal(g1, g2)
+    with torch.no_grad():
+        m.final.weight.mul_(0.5)
+    eager2 = ml_multi_level_upscale(m, dd, 160, "cuda", start_resolution=20, graphs=False, return_tensor=True)
+    g3 = ml_multi_level_upscale(m, dd, 160, "cuda", start_resolution=20, return_tensor=True)
+    assert torch.equal(eager2, g3) and not torch.equal(g3, g1)
