@@ -18,6 +18,7 @@ reverse schedule.  Design points:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -218,6 +219,17 @@ class WgradStream:
 
 # weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
 _WGRAD_STREAM = os.environ.get("SRPDE_WGRAD_STREAM", "1") != "0"
+_BWD_PRIORITY = os.environ.get("SRPDE_BWD_PRIORITY", "0") != "0"
+_PRIO_STREAMS = {}
+
+
+def _priority_stream(dev):
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    st = _PRIO_STREAMS.get(key)
+    if st is None:
+        lo, hi = torch.cuda.Stream.priority_range()   # (lowest, highest): a smaller number is higher
+        st = _PRIO_STREAMS[key] = torch.cuda.Stream(device=dev, priority=hi)
+    return st
 
 
 def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False, part=None,
@@ -462,14 +474,24 @@ class UNetFunction(torch.autograd.Function):
         views = {p: flat[off:off + nn].view_as(p) for _, p, off, nn in layout}
         reducer = getattr(model, "_grad_reducer", None)
         ends = _group_end_offsets(layout)
-        wq = WgradStream(dout.device) if _WGRAD_STREAM and dout.is_cuda else None
-        hook = None
-        if reducer is not None:
-            reducer.begin(flat, wait_streams=() if wq is None else (wq.side,))
-            hook = lambda grp: reducer.ready(ends[grp])  # noqa: E731
-        unet_backward(model, ctx.saved, dout, views, hook, wq=wq)
-        if reducer is not None:
-            reducer.finish()
+        side = _WGRAD_STREAM and dout.is_cuda
+        # with the weight gradients on a side stream, the dgrad chain may run on a high-priority
+        # stream so the dispatcher hands it CUs first (SRPDE_BWD_PRIORITY=1)
+        hi = _priority_stream(dout.device) if side and _BWD_PRIORITY else None
+        cur = torch.cuda.current_stream(dout.device) if dout.is_cuda else None
+        if hi is not None:
+            hi.wait_stream(cur)
+        with torch.cuda.stream(hi) if hi is not None else contextlib.nullcontext():
+            wq = WgradStream(dout.device) if side else None
+            hook = None
+            if reducer is not None:
+                reducer.begin(flat, wait_streams=() if wq is None else (wq.side,))
+                hook = lambda grp: reducer.ready(ends[grp])  # noqa: E731
+            unet_backward(model, ctx.saved, dout, views, hook, wq=wq)
+            if reducer is not None:
+                reducer.finish()
+        if hi is not None:
+            cur.wait_stream(hi)
         ctx.saved = None
         grads = [views[p] for p in model._param_list()]
         return (None, None, *grads)

@@ -13,11 +13,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _train_step(x, state, wgrad_stream):
+def _train_step(x, state, wgrad_stream, priority=False):
     from superresolution_for_pdes_amd import unet_exec
     from superresolution_for_pdes_amd.models import UNet
-    saved = unet_exec._WGRAD_STREAM
-    unet_exec._WGRAD_STREAM = wgrad_stream
+    saved = unet_exec._WGRAD_STREAM, unet_exec._BWD_PRIORITY
+    unet_exec._WGRAD_STREAM, unet_exec._BWD_PRIORITY = wgrad_stream, priority
     try:
         m = UNet()
         m.load_state_dict(state)
@@ -28,7 +28,7 @@ def _train_step(x, state, wgrad_stream):
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         bufs = {n: b.detach().clone() for n, b in m.named_buffers()}
     finally:
-        unet_exec._WGRAD_STREAM = saved
+        unet_exec._WGRAD_STREAM, unet_exec._BWD_PRIORITY = saved
     return out.detach(), grads, bufs
 
 
@@ -41,12 +41,12 @@ def test_wgrad_side_stream_is_bit_identical():
     x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(5)).to(DEV)
     x[:, 1] = 1.0
     a = _train_step(x, state, False)
-    b = _train_step(x, state, True)
-    assert torch.equal(a[0], b[0])
-    for n in a[1]:
-        assert torch.equal(a[1][n], b[1][n]), n
-    for n in a[2]:
-        assert torch.equal(a[2][n], b[2][n]), n
+    for b in (_train_step(x, state, True), _train_step(x, state, True, priority=True)):
+        assert torch.equal(a[0], b[0])
+        for n in a[1]:
+            assert torch.equal(a[1][n], b[1][n]), n
+        for n in a[2]:
+            assert torch.equal(a[2][n], b[2][n]), n
 
 
 @pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (6, 256, 0, 512, 10, 2),
