@@ -509,6 +509,69 @@ __global__ __launch_bounds__(256) void att_bwd_channel_kernel(
   }
 }
 
+// backward, passes 1 and 2 in one read of dout and x (one block per sample, C / 4 in {16, 32, 64}):
+// dsa_pre[p] = sigmoid'(sa) * sum_c dout * (x * ca)   (the C / 4 lanes of a pixel reduce by shuffles)
+// and dca[c] = sum_hw dout * sa * x, then the channel-MLP backward exactly as att_bwd_channel_kernel.
+__global__ __launch_bounds__(256) void att_bwd_sample_kernel(
+    const float* __restrict__ dout, int lddo, const float* __restrict__ x, int ldx, const float* __restrict__ sa,
+    int HW, int C, int Cr, const float* __restrict__ w1, const float* __restrict__ w2, const float* __restrict__ m,
+    const float* __restrict__ h, const float* __restrict__ ca, float* __restrict__ dm, float* __restrict__ dw1_rows,
+    float* __restrict__ db1_rows, float* __restrict__ dw2_rows, float* __restrict__ db2_rows,
+    float* __restrict__ dsa_pre) {
+  extern __shared__ float sh[];
+  const int n = blockIdx.x, C4 = C >> 2;
+  const int c4 = threadIdx.x % C4, r0 = threadIdx.x / C4, rs = blockDim.x / C4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  {
+    const float4 a = *reinterpret_cast<const float4*>(ca + (long long)n * C + c4 * 4);
+    const long long pb = (long long)n * HW;
+    for (int p = r0; p < HW; p += rs) {   // every lane of a pixel's C / 4 group takes the same trips
+      const float4 d = *reinterpret_cast<const float4*>(dout + (pb + p) * lddo + c4 * 4);
+      const float4 v = *reinterpret_cast<const float4*>(x + (pb + p) * ldx + c4 * 4);
+      const float q = sa[pb + p];
+      s.x += (d.x * q) * v.x; s.y += (d.y * q) * v.y; s.z += (d.z * q) * v.z; s.w += (d.w * q) * v.w;
+      float dot = d.x * (v.x * a.x) + d.y * (v.y * a.y) + d.z * (v.z * a.z) + d.w * (v.w * a.w);
+      for (int o = C4 >> 1; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+      if (c4 == 0) dsa_pre[pb + p] = dot * (1.f - q) * q;
+    }
+  }
+  float4* red = reinterpret_cast<float4*>(sh);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  float* dpre = sh + 4 * 256;  // [C] grad of pre-sigmoid channel logits
+  float* dh = dpre + C;        // [Cr]
+  if ((int)threadIdx.x < C4) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red[r * C4 + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    const int c = threadIdx.x * 4;
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = ca[(long long)n * C + c + k];
+      dpre[c + k] = tv[k] * (1.f - a) * a;
+    }
+  }
+  __syncthreads();
+  // per-sample vectors only; the weight grads are batch reductions (outer_sum_kernel)
+  for (int c = threadIdx.x; c < C; c += blockDim.x) db2_rows[(long long)n * C + c] = dpre[c];
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float a = 0.f;
+    for (int c = 0; c < C; ++c) a += w2[c * Cr + r] * dpre[c];
+    a = h[(long long)n * Cr + r] > 0.f ? a : 0.f;
+    dh[r] = a;
+    db1_rows[(long long)n * Cr + r] = a;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f;
+    for (int r = 0; r < Cr; ++r) a += w1[r * C + c] * dh[r];
+    dm[(long long)n * C + c] = a / (float)HW;
+  }
+}
+
 // backward, pass 3 (elementwise): dx = (dout*sa)*ca + dm[n][c]  (write or accumulate)
 __global__ void att_bwd_dx_kernel(const float* __restrict__ dout, int lddo, const float* __restrict__ ca,
                                   const float* __restrict__ sa, const float* __restrict__ dm, float* __restrict__ dx,
@@ -885,13 +948,19 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
   float2* part = reinterpret_cast<float2*>(db2r + (size_t)n * c + 2);
   part = reinterpret_cast<float2*>((reinterpret_cast<uintptr_t>(part) + 15) & ~uintptr_t(15));
 
-  hipLaunchKernelGGL(att_bwd_pixel_kernel, dim3(grid_for(P * 8)), dim3(256), 0, stream, dout, lddo, x, ldx, ca, sa,
-                     P, hw, c, dsa);
-  SRPDE_LAUNCH_CHECK("srpde_att_bwd(pixel)");
   const size_t lds = (4 * 256 + c + cr) * sizeof(float);
-  hipLaunchKernelGGL(att_bwd_channel_kernel, dim3(n), dim3(256), lds, stream, dout, lddo, x, ldx, sa, hw, c, cr, w1,
-                     w2, m, hbuf, ca, dm, dw1r, db1r, dw2r, db2r);
-  SRPDE_LAUNCH_CHECK("srpde_att_bwd(channel)");
+  if (c == 64 || c == 128 || c == 256) {   // one pass over dout and x per sample
+    hipLaunchKernelGGL(att_bwd_sample_kernel, dim3(n), dim3(256), lds, stream, dout, lddo, x, ldx, sa, hw, c, cr, w1,
+                       w2, m, hbuf, ca, dm, dw1r, db1r, dw2r, db2r, dsa);
+    SRPDE_LAUNCH_CHECK("srpde_att_bwd(sample)");
+  } else {
+    hipLaunchKernelGGL(att_bwd_pixel_kernel, dim3(grid_for(P * 8)), dim3(256), 0, stream, dout, lddo, x, ldx, ca,
+                       sa, P, hw, c, dsa);
+    SRPDE_LAUNCH_CHECK("srpde_att_bwd(pixel)");
+    hipLaunchKernelGGL(att_bwd_channel_kernel, dim3(n), dim3(256), lds, stream, dout, lddo, x, ldx, sa, hw, c, cr,
+                       w1, w2, m, hbuf, ca, dm, dw1r, db1r, dw2r, db2r);
+    SRPDE_LAUNCH_CHECK("srpde_att_bwd(channel)");
+  }
   hipLaunchKernelGGL(att_bwd_dx_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, lddo, ca, sa, dm,
                      dx, lddx, P, hw, c, dx_accumulate);
   SRPDE_LAUNCH_CHECK("srpde_att_bwd(dx)");
