@@ -298,11 +298,13 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots):
     return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots)
 
 
-def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None):
+def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
+    """``part``: bn2's backward reduction, when the dgrad that wrote ``da`` produced it."""
     s1, s2 = saved
     P = n * h * w
     da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
-    part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, below=(blk.bn1, s1), wq=wq)
+    part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, part=part, below=(blk.bn1, s1),
+                    wq=wq)
     _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part, wq=wq)
 
 
@@ -402,11 +404,13 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
                     wq=wq)
     ready("out_bn2"); ready("out_conv2")
     dd1 = H.empty(P1, 64, device=dev)
-    _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part, wq=wq)
+    # out_conv1's dgrad writes dec1's output gradient: its epilogue also reduces dec1.bn2's backward
+    part = _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part,
+                    below=(m.dec1.bn2, S.dec1[1]), wq=wq)
     ready("out_bn1"); ready("out_conv1")
     # dec1: grad of cat[u2 (128), e1a (64)]
     dcat1 = H.empty(P1, 192, device=dev)
-    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1, wq=wq)
+    _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1, wq=wq, part=part)
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
     # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below
