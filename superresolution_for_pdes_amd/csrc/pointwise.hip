@@ -319,6 +319,11 @@ __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __res
   *reinterpret_cast<float4*>(o) = s;
 }
 
+// the gather's cap of 8 candidates per axis (gather_weights) holds for scale = (in-1)/(out-1) > 1/4:
+// input i's candidates are the outputs o with floor(o * scale) in {i-1, i}, at most
+// floor(2 / scale) + 1 of them
+static bool upsample_gather_ok(int in, int out) { return out <= 1 || in <= 1 || 2.0 * (out - 1) < 8.0 * (in - 1); }
+
 // launch geometry of the pixel-blocked kernels, or false when C/4 is not a power of two <= 256
 static bool px_geometry(long long npix, int c, dim3* grid, dim3* block) {
   const int c4 = c / 4;
@@ -868,6 +873,8 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
                                       hipStream_t stream) {
   SRPDE_CHECK_ARG(dout && dsa && wg && dx && c % 4 == 0 && lddo % 4 == 0 && lddx % 4 == 0 && ho >= h && wo >= w,
                   "srpde_upsample_bilinear_bwd_gated: bad args");
+  SRPDE_CHECK_ARG(upsample_gather_ok(h, ho) && upsample_gather_ok(w, wo),
+                  "srpde_upsample_bilinear_bwd_gated: upsampling ratio above 4 (%dx%d -> %dx%d)", h, w, ho, wo);
   dim3 g, b;
   SRPDE_CHECK_ARG(px_geometry((long long)n * h * w, c, &g, &b),
                   "srpde_upsample_bilinear_bwd_gated: needs c / 4 a power of two <= 256 (c=%d)", c);
@@ -880,6 +887,8 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
 int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
                                 int wo, int c, int accumulate, hipStream_t stream) {
   SRPDE_CHECK_ARG(dout && dx && c % 4 == 0 && ho >= h && wo >= w, "srpde_upsample_bilinear_bwd: bad args");
+  SRPDE_CHECK_ARG(upsample_gather_ok(h, ho) && upsample_gather_ok(w, wo),
+                  "srpde_upsample_bilinear_bwd: upsampling ratio above 4 (%dx%d -> %dx%d)", h, w, ho, wo);
   dim3 g, b;
   if (px_geometry((long long)n * h * w, c, &g, &b)) {
     hipLaunchKernelGGL(upsample_bwd_px_kernel, g, b, 0, stream, dout, lddo, dx, lddx, (unsigned)(n * h * w), h, w, ho,

@@ -161,11 +161,12 @@ def test_conv_cin_pad_and_accumulate():
     assert rel(dw, wg.grad) < 2e-6
 
 
-@pytest.mark.parametrize("c", [16, 64, 512])
-def test_bn_relu_fwd_bwd(c):
+@pytest.mark.parametrize("c,n,h", [(16, 3, 10), (64, 3, 10), (512, 3, 10),
+                                   # large enough that the kernels' four-rows-in-flight loops run
+                                   (64, 40, 40), (512, 100, 10)])
+def test_bn_relu_fwd_bwd(c, n, h):
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator().manual_seed(c)
-    n, h = 3, 10
     y = torch.randn(n, c, h, h, generator=g) * 2 + 0.5
     gamma = torch.rand(c, generator=g) + 0.5
     beta = torch.randn(c, generator=g) * 0.2
@@ -231,6 +232,30 @@ def test_pool_upsample():
     torch.cuda.synchronize()
     assert rel(unrows(u, n, 2 * h, 2 * h), u_ref) < 1e-6
     assert rel(unrows(dxu, n, h, h), uv.grad) < 1e-6
+
+
+@pytest.mark.parametrize("h,ho", [(20, 40), (10, 20), (7, 9), (2, 4), (5, 15), (4, 12)])
+def test_upsample_bwd_gather_slots(h, ho):
+    """The gather backward at the model's 2x ratios and at others up to the gather's cap (8
+    candidates per axis) against torch's bilinear (align_corners=True) backward."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(h * 100 + ho)
+    n, c = 2, 32
+    x = torch.randn(n, c, h, h, generator=g).requires_grad_(True)
+    u = F.interpolate(x, size=(ho, ho), mode="bilinear", align_corners=True)
+    du = torch.randn(n, c, ho, ho, generator=g)
+    u.backward(du)
+    dx = H.empty(n * h * h, c, device=DEV)
+    H.upsample_bwd(rows(du).to(DEV), dx, n, h, h, ho, ho, False)
+    torch.cuda.synchronize()
+    assert rel(unrows(dx, n, h, h), x.grad) < 1e-6
+
+
+def test_upsample_bwd_rejects_ratios_beyond_the_gather_cap():
+    from superresolution_for_pdes_amd import hipops as H
+    dx = H.empty(2 * 3 * 3, 32, device=DEV)
+    with pytest.raises(RuntimeError, match="ratio above 4"):
+        H.upsample_bwd(torch.zeros(2 * 16 * 16, 32, device=DEV), dx, 2, 3, 3, 16, 16, False)
 
 
 @pytest.mark.parametrize("c,h", [(128, 20), (256, 10)])

@@ -1,0 +1,14 @@
+# Quick check of a pointwise-kernel change: kernel + U-Net GPU tests, the bench line, and the
+# kernel-trace stats of the bench command.   usage: bash tools/gpu_s11.sh TAG
+set -o pipefail
+T=${1:-s11}
+R=$GRAFT_REPO_ROOT
+cd $R
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_unet.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_$T.log 2>&1 || { echo "pytest failed"; grep -v amdgpu gpurun_out/pytest_$T.log | tail -30; exit 1; }
+tail -1 gpurun_out/pytest_$T.log
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { echo "bench failed"; tail -20 gpurun_out/bench_$T.err; exit 1; }
+cat gpurun_out/bench_$T.json
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o bench -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$T.log 2>&1 || { echo "prof failed"; exit 1; }
+echo done
