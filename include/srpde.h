@@ -168,6 +168,18 @@ int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, in
 int srpde_maxpool2x2_bwd(const float* x, int ldx, const float* dout, int lddo, float* dx, int lddx, int n, int h,
                          int w, int c, int accumulate, hipStream_t stream);
 
+/* ---- PDEDataset assembly (src/models.py:132-207; replaces the per-field normalisation,
+ *      F.interpolate(size=fine, bilinear, align_corners=True) of the coarse field and the
+ *      torch.cat of models.py:155-203) -------------------------------------------------
+ * u_coarse [n][hc][wc], u_fine / theta_fine / f_fine [n][hf][wf] (contiguous fp32);
+ * stats = device {u_mean, u_std, f_mean, f_std, theta_mean, theta_std} (fp32, the split's
+ * statistics; theta's ignored when theta_constant != 0, theta then passes through unnormalised).
+ * Writes inputs [n][3][hf][wf] = (resize((u_coarse - u_mean) / u_std), theta_n, f_n) and
+ * targets [n][1][hf][wf] = (u_fine - u_mean) / u_std. */
+int srpde_pde_dataset_assemble(const float* u_coarse, const float* u_fine, const float* theta_fine,
+                               const float* f_fine, const float* stats, int theta_constant, int n, int hc, int wc,
+                               int hf, int wf, float* inputs, float* targets, hipStream_t stream);
+
 /* ---- bilinear, align_corners=True: nn.Upsample(2) (models.py:70, :89-93) and the
  *      F.interpolate(size=(40,40)) of PDEDataset (models.py:182-187) ------------------ */
 int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho, int wo,

@@ -149,6 +149,35 @@ __global__ void upsample_fwd_scalar_kernel(const float* __restrict__ x, int ldx,
   }
 }
 
+// PDEDataset assembly (models.py:155-203) in one pass, one thread per fine pixel: the coarse
+// field normalised with the FINE statistics tap by tap, then bilinearly resized to the fine grid
+// (align_corners=True, the same lerp as upsample_fwd_scalar_kernel), theta normalised unless
+// constant, f normalised, and the normalised target.  Each normalisation is (v - mean) / std with
+// a correctly rounded division, as the reference's tensor expressions compute it.
+// stats = {u_mean, u_std, f_mean, f_std, theta_mean, theta_std} (device, fp32).
+__global__ __launch_bounds__(256) void pde_dataset_kernel(const float* __restrict__ uc, const float* __restrict__ uf,
+                                                          const float* __restrict__ th, const float* __restrict__ fs,
+                                                          const float* __restrict__ stats, int theta_const, int N,
+                                                          int hc, int wc, int hf, int wf, float* __restrict__ inputs,
+                                                          float* __restrict__ targets) {
+  const long long plane = (long long)hf * wf, total = (long long)N * plane;
+  const float um = stats[0], us = stats[1], fm = stats[2], fsd = stats[3], tm = stats[4], ts = stats[5];
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < total;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long n = q / plane;
+    const int pix = (int)(q - n * plane), y = pix / wf, x = pix - y * wf;
+    const Lerp ly = lerp_index(y, hc, hf), lx = lerp_index(x, wc, wf);
+    const float* base = uc + n * hc * wc;
+    const float a = (base[ly.i0 * wc + lx.i0] - um) / us, b = (base[ly.i0 * wc + lx.i1] - um) / us;
+    const float d = (base[ly.i1 * wc + lx.i0] - um) / us, f = (base[ly.i1 * wc + lx.i1] - um) / us;
+    float* in = inputs + n * 3 * plane + pix;
+    in[0] = ly.l0 * (lx.l0 * a + lx.l1 * b) + ly.l1 * (lx.l0 * d + lx.l1 * f);
+    in[plane] = theta_const ? th[q] : (th[q] - tm) / ts;
+    in[2 * plane] = (fs[q] - fm) / fsd;
+    targets[q] = (uf[q] - um) / us;
+  }
+}
+
 // backward as a deterministic gather: every input pixel sums the output pixels whose
 // 4-tap stencil touches it (scale < 1 => at most ~5 candidates per axis).
 __device__ __forceinline__ int gather_weights(int i, int in, int out, int* idx, float* wt) {
@@ -844,6 +873,19 @@ int srpde_maxpool2x2_bwd(const float* x, int ldx, const float* dout, int lddo, f
   hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)n * (h / 2) * (w / 2) * (c / 4))), dim3(256), 0,
                      stream, x, ldx, dout, lddo, dx, lddx, n, h, w, c, accumulate);
   SRPDE_LAUNCH_CHECK("srpde_maxpool2x2_bwd");
+  return 0;
+}
+
+int srpde_pde_dataset_assemble(const float* u_coarse, const float* u_fine, const float* theta_fine,
+                               const float* f_fine, const float* stats, int theta_constant, int n, int hc, int wc,
+                               int hf, int wf, float* inputs, float* targets, hipStream_t stream) {
+  SRPDE_CHECK_ARG(u_coarse && u_fine && theta_fine && f_fine && stats && inputs && targets,
+                  "srpde_pde_dataset_assemble: null");
+  SRPDE_CHECK_ARG(n >= 0 && hc >= 1 && wc >= 1 && hf >= hc && wf >= wc, "srpde_pde_dataset_assemble: bad shape");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pde_dataset_kernel, dim3(grid_for((long long)n * hf * wf)), dim3(256), 0, stream, u_coarse,
+                     u_fine, theta_fine, f_fine, stats, theta_constant, n, hc, wc, hf, wf, inputs, targets);
+  SRPDE_LAUNCH_CHECK("srpde_pde_dataset_assemble");
   return 0;
 }
 

@@ -378,6 +378,23 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
 
 
+def pde_dataset_assemble(u_coarse, u_fine, theta_fine, f_fine, stats, theta_constant):
+    """srpde_pde_dataset_assemble: -> (inputs [N, 3, hf, wf], targets [N, 1, hf, wf])."""
+    n, hc, wc = u_coarse.shape
+    _, hf, wf = u_fine.shape
+    for t in (u_coarse, u_fine, theta_fine, f_fine, stats):
+        if not (t.is_cuda and t.dtype == F32 and t.is_contiguous()):
+            raise RuntimeError("pde_dataset_assemble: contiguous fp32 ROCm tensors only (no CPU fallback)")
+    if theta_fine.shape != u_fine.shape or f_fine.shape != u_fine.shape or stats.numel() != 6:
+        raise ValueError("pde_dataset_assemble: theta / f must match u_fine's shape, stats has 6 entries")
+    inputs = torch.empty(n, 3, hf, wf, dtype=F32, device=u_fine.device)
+    targets = torch.empty(n, 1, hf, wf, dtype=F32, device=u_fine.device)
+    call("srpde_pde_dataset_assemble", u_coarse.data_ptr(), u_fine.data_ptr(), theta_fine.data_ptr(),
+         f_fine.data_ptr(), stats.data_ptr(), int(theta_constant), n, hc, wc, hf, wf, inputs.data_ptr(),
+         targets.data_ptr(), stream_ptr())
+    return inputs, targets
+
+
 def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate, gate=None):
     """``gate = (dsa, wg)``: the upsampled tensor's gradient is dout + dsa (x) wg (the attention
     gating gradient left unapplied by att_bwd(dg=None))."""

@@ -237,9 +237,10 @@ class PDEDataset(torch.utils.data.Dataset):
 
         Statistics follow the reference exactly: fp32 mean / unbiased std over the whole
         split, theta passed through when std < 1e-6, coarse normalised with the FINE
-        statistics, then bilinear (align_corners=True) to the fine grid -- the resize runs
-        on the HIP upsample kernel.  Tensors live on ``device``; batches are gathered by
-        index on the device (``batch(idx)``), no DataLoader workers needed.
+        statistics, then bilinear (align_corners=True) to the fine grid -- normalisation,
+        resize and channel stack run as one HIP pass (srpde_pde_dataset_assemble).  Tensors
+        live on ``device``; batches are gathered by index on the device (``batch(idx)``), no
+        DataLoader workers needed.
         """
         self.device = device
         if not str(device).startswith("cuda"):
@@ -263,19 +264,36 @@ class PDEDataset(torch.utils.data.Dataset):
         else:
             self.theta_mean = self.theta_fine.mean()
             self.theta_std = self.theta_fine.std()
-        self.u_fine_norm = (self.u_fine - self.u_mean) / self.u_std
-        self.u_coarse_norm = (self.u_coarse - self.u_mean) / self.u_std
-        self.f_fine_norm = (self.f_fine - self.f_mean) / self.f_std
-        if self.theta_is_constant:
-            self.theta_fine_norm = self.theta_fine
-        else:
-            self.theta_fine_norm = (self.theta_fine - self.theta_mean) / self.theta_std
-        nf = self.u_fine.shape[-1]
-        self.u_coarse_upsampled = upsample_bilinear(self.u_coarse_norm.unsqueeze(1), nf, nf)
-        # model-ready inputs [N, 3, nf, nf] and targets [N, 1, nf, nf], built once on device
-        self.inputs = torch.cat([self.u_coarse_upsampled, self.theta_fine_norm.unsqueeze(1),
-                                 self.f_fine_norm.unsqueeze(1)], dim=1).contiguous()
-        self.targets = self.u_fine_norm.unsqueeze(1).contiguous()
+        # normalisation, the coarse field's resize to the fine grid and the channel stack in one
+        # HIP pass (srpde_pde_dataset_assemble); model-ready inputs [N, 3, nf, nf], targets [N, 1, nf, nf]
+        one, zero = torch.ones((), device=device), torch.zeros((), device=device)
+        tm = zero if self.theta_is_constant else self.theta_mean
+        ts = one if self.theta_is_constant else self.theta_std
+        stats = torch.stack([self.u_mean, self.u_std, self.f_mean, self.f_std, tm, ts]).float().contiguous()
+        self.inputs, self.targets = H.pde_dataset_assemble(self.u_coarse.contiguous(), self.u_fine.contiguous(),
+                                                           self.theta_fine.contiguous(), self.f_fine.contiguous(),
+                                                           stats, self.theta_is_constant)
+
+    # the reference's intermediate fields (models.py:170-187), as views of the assembled tensors
+    @property
+    def u_fine_norm(self):
+        return self.targets[:, 0]
+
+    @property
+    def u_coarse_norm(self):
+        return (self.u_coarse - self.u_mean) / self.u_std
+
+    @property
+    def f_fine_norm(self):
+        return self.inputs[:, 2]
+
+    @property
+    def theta_fine_norm(self):
+        return self.inputs[:, 1]
+
+    @property
+    def u_coarse_upsampled(self):
+        return self.inputs[:, 0:1]
 
     def __len__(self) -> int:
         return len(self.u_fine)
