@@ -348,10 +348,150 @@ __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __res
   *reinterpret_cast<float4*>(o) = s;
 }
 
+// Row-blocked upsample backward: one workgroup per (sample, input row iy), all channels.  Phase 1
+// reduces iy's candidate output rows with their y weights (and the attention gating gradient,
+// GATED) into an LDS row R[ox][c]: every gradient element is read once per workgroup, the
+// candidate rows' loads of a thread independent of each other.  Phase 2 applies the x weights
+// from LDS.  Needs at most ROWS_NS candidate rows (upsample_rows_ok) and C/4 dividing 256.
+// The pixel-blocked gather above re-read each gradient element ~4x through L2 with one load per
+// trip (2.35 TB/s isolated).
+constexpr int ROWS_NS = 6;
+// weight of output o in input i's gradient (gather_weights' per-candidate term); the candidates of
+// i form one contiguous range of o (i0 and i1 are monotone in o)
+__device__ __forceinline__ float cand_weight(int o, int i, int in, int out, bool* hit) {
+  const Lerp l = lerp_index(o, in, out);
+  *hit = l.i0 == i || l.i1 == i;
+  return (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+}
+__device__ __forceinline__ void cand_range(int i, int in, int out, int* lo, int* hi) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  *lo = 0;
+  *hi = out - 1;
+  if (scale > 0.f) {
+    *lo = max(0, (int)floorf((float)(i - 1) / scale) - 1);
+    *hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
+  }
+}
+
+// phase 1 of upsample_bwd_rows_kernel with NSL candidate-row slots (slots past the range re-read
+// the first row, branch-free, with weight 0)
+template <bool GATED, int NSL>
+__device__ __forceinline__ void upsample_rows_phase1(const float* __restrict__ dout, int lddo, int Ho, int Wo, int C4,
+                                                     int n, int iy, int H, int oy0, int hi,
+                                                     const float* __restrict__ gsa, const float* __restrict__ gw,
+                                                     float4* rrow) {
+  const int cq = threadIdx.x % C4, lx0 = threadIdx.x / C4, nlx = blockDim.x / C4;
+  float wy[NSL];
+#pragma unroll
+  for (int a = 0; a < NSL; ++a) {
+    bool hit = false;
+    const float w = oy0 + a <= hi ? cand_weight(oy0 + a, iy, H, Ho, &hit) : 0.f;
+    wy[a] = hit ? w : 0.f;
+  }
+  const float4 wv = GATED ? *reinterpret_cast<const float4*>(gw + cq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* base = dout + (size_t)n * Ho * Wo * lddo + cq * 4;
+  const float* sb = GATED ? gsa + (size_t)n * Ho * Wo : nullptr;
+  for (int ox = lx0; ox < Wo; ox += nlx) {
+    float4 g[NSL];
+    float sv[NSL];
+#pragma unroll
+    for (int a = 0; a < NSL; ++a) {
+      const int o = (oy0 + a <= hi ? oy0 + a : oy0) * Wo + ox;
+      g[a] = *reinterpret_cast<const float4*>(base + (size_t)o * lddo);
+      if constexpr (GATED) sv[a] = sb[o];
+    }
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int a = 0; a < NSL; ++a) {   // zero-weight slots add nothing (0 * finite)
+      float4 gg = g[a];
+      if constexpr (GATED) {
+        gg.x = sv[a] * wv.x + gg.x; gg.y = sv[a] * wv.y + gg.y; gg.z = sv[a] * wv.z + gg.z; gg.w = sv[a] * wv.w + gg.w;
+      }
+      r.x += wy[a] * gg.x; r.y += wy[a] * gg.y; r.z += wy[a] * gg.z; r.w += wy[a] * gg.w;
+    }
+    rrow[ox * C4 + cq] = r;
+  }
+}
+
+template <bool GATED>
+__global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __restrict__ dout, int lddo,
+                                                                float* __restrict__ dx, int lddx, int H, int W, int Ho,
+                                                                int Wo, int C, int accumulate,
+                                                                const float* __restrict__ gsa,
+                                                                const float* __restrict__ gw) {
+  extern __shared__ float4 rrow[];   // [Wo][C/4]
+  const int C4 = C >> 2;
+  const int cq = threadIdx.x % C4, lx0 = threadIdx.x / C4, nlx = blockDim.x / C4;
+  const int n = blockIdx.x / H, iy = blockIdx.x - n * H;
+  // iy's candidate output rows: [oy0, last], contiguous, at most ROWS_NS (upsample_rows_ok)
+  int lo, hi;
+  cand_range(iy, H, Ho, &lo, &hi);
+  int oy0 = hi + 1;
+  for (int o = lo; o <= hi && oy0 > hi; ++o) {
+    bool hit;
+    cand_weight(o, iy, H, Ho, &hit);
+    if (hit) oy0 = o;
+  }
+  if (oy0 > hi) oy0 = lo;   // no candidate (not reached for valid shapes): all weights 0, loads in range
+  int last = oy0;
+  for (int o = oy0 + 1; o <= hi && o < oy0 + ROWS_NS; ++o) {
+    bool hit;
+    cand_weight(o, iy, H, Ho, &hit);
+    if (hit) last = o;
+  }
+  // the row count is uniform over the workgroup: one instantiation per count, no wasted loads
+  const int nrow = last - oy0 + 1;
+  if (nrow <= 3) upsample_rows_phase1<GATED, 3>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
+  else if (nrow == 4) upsample_rows_phase1<GATED, 4>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
+  else if (nrow == 5) upsample_rows_phase1<GATED, 5>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
+  else upsample_rows_phase1<GATED, ROWS_NS>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
+  __syncthreads();
+  for (int ix = lx0; ix < W; ix += nlx) {
+    int xlo, xhi;
+    cand_range(ix, W, Wo, &xlo, &xhi);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int o = xlo; o <= xhi; ++o) {
+      bool hit;
+      const float w = cand_weight(o, ix, W, Wo, &hit);
+      if (hit) {
+        const float4 r = rrow[o * C4 + cq];
+        s.x += w * r.x; s.y += w * r.y; s.z += w * r.z; s.w += w * r.w;
+      }
+    }
+    float* o = dx + ((size_t)blockIdx.x * W + ix) * lddx + cq * 4;
+    if (accumulate) {
+      const float4 old = *reinterpret_cast<const float4*>(o);
+      s.x += old.x; s.y += old.y; s.z += old.z; s.w += old.w;
+    }
+    *reinterpret_cast<float4*>(o) = s;
+  }
+}
+
 // the gather's cap of 8 candidates per axis (gather_weights) holds for scale = (in-1)/(out-1) > 1/4:
 // input i's candidates are the outputs o with floor(o * scale) in {i-1, i}, at most
 // floor(2 / scale) + 1 of them
 static bool upsample_gather_ok(int in, int out) { return out <= 1 || in <= 1 || 2.0 * (out - 1) < 8.0 * (in - 1); }
+
+// the row-blocked kernel: input row i's candidate rows number at most floor(2/scale) + 1 (+1 for
+// rounding) <= ROWS_NS when 2/scale < 5; C/4 a power of two <= 256; one LDS row of Wo x C floats
+static bool upsample_rows_ok(int h, int w, int ho, int wo, int c, int lddo, int lddx) {
+  static const bool off = [] {
+    const char* e = getenv("SRPDE_UPSAMPLE_BWD");   // "px": the pixel-blocked gather (A/B)
+    return e != nullptr && strcmp(e, "px") == 0;
+  }();
+  const int c4 = c / 4;
+  return !off && c % 4 == 0 && c4 >= 1 && c4 <= 256 && (c4 & (c4 - 1)) == 0 && lddo % 4 == 0 && lddx % 4 == 0 &&
+         h > 1 && ho > 1 && 2.0 * (ho - 1) < 5.0 * (h - 1) && upsample_gather_ok(w, wo) &&
+         (size_t)wo * c * sizeof(float) <= 64 * 1024;
+}
+
+template <bool GATED>
+static void launch_upsample_bwd_rows(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
+                                     int wo, int c, int accumulate, const float* gsa, const float* gw,
+                                     hipStream_t stream) {
+  hipLaunchKernelGGL(upsample_bwd_rows_kernel<GATED>, dim3((unsigned)(n * h)), dim3(256), (size_t)wo * c * sizeof(float),
+                     stream, dout, lddo, dx, lddx, h, w, ho, wo, c, accumulate, gsa, gw);
+}
 
 // launch geometry of the pixel-blocked kernels, or false when C/4 is not a power of two <= 256
 static bool px_geometry(long long npix, int c, dim3* grid, dim3* block) {
@@ -917,6 +1057,11 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
                   "srpde_upsample_bilinear_bwd_gated: bad args");
   SRPDE_CHECK_ARG(upsample_gather_ok(h, ho) && upsample_gather_ok(w, wo),
                   "srpde_upsample_bilinear_bwd_gated: upsampling ratio above 4 (%dx%d -> %dx%d)", h, w, ho, wo);
+  if (upsample_rows_ok(h, w, ho, wo, c, lddo, lddx)) {
+    launch_upsample_bwd_rows<true>(dout, lddo, dx, lddx, n, h, w, ho, wo, c, accumulate, dsa, wg, stream);
+    SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd_gated");
+    return 0;
+  }
   dim3 g, b;
   SRPDE_CHECK_ARG(px_geometry((long long)n * h * w, c, &g, &b),
                   "srpde_upsample_bilinear_bwd_gated: needs c / 4 a power of two <= 256 (c=%d)", c);
@@ -931,6 +1076,11 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
   SRPDE_CHECK_ARG(dout && dx && c % 4 == 0 && ho >= h && wo >= w, "srpde_upsample_bilinear_bwd: bad args");
   SRPDE_CHECK_ARG(upsample_gather_ok(h, ho) && upsample_gather_ok(w, wo),
                   "srpde_upsample_bilinear_bwd: upsampling ratio above 4 (%dx%d -> %dx%d)", h, w, ho, wo);
+  if (upsample_rows_ok(h, w, ho, wo, c, lddo, lddx)) {
+    launch_upsample_bwd_rows<false>(dout, lddo, dx, lddx, n, h, w, ho, wo, c, accumulate, nullptr, nullptr, stream);
+    SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd");
+    return 0;
+  }
   dim3 g, b;
   if (px_geometry((long long)n * h * w, c, &g, &b)) {
     hipLaunchKernelGGL(upsample_bwd_px_kernel, g, b, 0, stream, dout, lddo, dx, lddx, (unsigned)(n * h * w), h, w, ho,
