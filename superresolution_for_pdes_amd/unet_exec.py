@@ -219,7 +219,12 @@ class WgradStream:
 
 # weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
 _WGRAD_STREAM = os.environ.get("SRPDE_WGRAD_STREAM", "1") != "0"
-_BWD_PRIORITY = os.environ.get("SRPDE_BWD_PRIORITY", "0") != "0"
+# the backward's dgrad chain on a high-priority stream: "1" always, "0" never, unset: only under
+# data parallelism.  A high-priority stream never shares a hardware queue with the normal-priority
+# weight-gradient stream; with RCCL's streams present the two normal-priority streams were seen
+# sharing one queue, which serialised wgrad behind dgrad (DataParallel step 37.9 ms -> 35.7 ms,
+# plain step 35.6 ms; without a process group the priority is neutral, 35.74 vs 35.64 ms)
+_BWD_PRIORITY = os.environ.get("SRPDE_BWD_PRIORITY", "auto")
 _PRIO_STREAMS = {}
 
 
@@ -480,8 +485,9 @@ class UNetFunction(torch.autograd.Function):
         ends = _group_end_offsets(layout)
         side = _WGRAD_STREAM and dout.is_cuda
         # with the weight gradients on a side stream, the dgrad chain may run on a high-priority
-        # stream so the dispatcher hands it CUs first (SRPDE_BWD_PRIORITY=1)
-        hi = _priority_stream(dout.device) if side and _BWD_PRIORITY else None
+        # stream (SRPDE_BWD_PRIORITY; on by default under data parallelism, see _BWD_PRIORITY)
+        prio = _BWD_PRIORITY == "1" or (_BWD_PRIORITY == "auto" and reducer is not None)
+        hi = _priority_stream(dout.device) if side and prio else None
         cur = torch.cuda.current_stream(dout.device) if dout.is_cuda else None
         if hi is not None:
             hi.wait_stream(cur)
