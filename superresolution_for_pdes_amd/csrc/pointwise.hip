@@ -356,6 +356,12 @@ __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __res
 // The pixel-blocked gather above re-read each gradient element ~4x through L2 with one load per
 // trip (2.35 TB/s isolated).
 constexpr int ROWS_NS = 6;
+// bijective block remap: XCD x (= bid % 8 in dispatch order) takes the x-th contiguous eighth
+__device__ __forceinline__ int xcd_rows_remap(int bid, int total) {
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
 // weight of output o in input i's gradient (gather_weights' per-candidate term); the candidates of
 // i form one contiguous range of o (i0 and i1 are monotone in o)
 __device__ __forceinline__ float cand_weight(int o, int i, int in, int out, bool* hit) {
@@ -422,7 +428,10 @@ __global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __r
   extern __shared__ float4 rrow[];   // [Wo][C/4]
   const int C4 = C >> 2;
   const int cq = threadIdx.x % C4, lx0 = threadIdx.x / C4, nlx = blockDim.x / C4;
-  const int n = blockIdx.x / H, iy = blockIdx.x - n * H;
+  // consecutive workgroups go to different XCDs (each with its own L2): remap so an XCD walks a
+  // contiguous run of rows and the output rows two neighbouring input rows share hit its L2
+  const int blk = xcd_rows_remap(blockIdx.x, gridDim.x);
+  const int n = blk / H, iy = blk - n * H;
   // iy's candidate output rows: [oy0, last], contiguous, at most ROWS_NS (upsample_rows_ok)
   int lo, hi;
   cand_range(iy, H, Ho, &lo, &hi);
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __r
         s.x += w * r.x; s.y += w * r.y; s.z += w * r.z; s.w += w * r.w;
       }
     }
-    float* o = dx + ((size_t)blockIdx.x * W + ix) * lddx + cq * 4;
+    float* o = dx + ((size_t)blk * W + ix) * lddx + cq * 4;
     if (accumulate) {
       const float4 old = *reinterpret_cast<const float4*>(o);
       s.x += old.x; s.y += old.y; s.z += old.z; s.w += old.w;
