@@ -148,6 +148,13 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
 int srpde_bn_affine(const float* mean, const float* invstd, const float* gamma, const float* beta, int C, long long P,
                     float* scale, float* shift, unsigned* amax_bound, hipStream_t stream);
 size_t srpde_bn_relu_bwd_workspace_size(long long P, int C);
+/* backward flags (the `relu` argument of the two calls below):
+ *   SRPDE_BN_RELU  the BN output went through ReLU (mask dz by the recomputed output > 0)
+ *   SRPDE_BN_EVAL  the forward normalised with the running statistics (eval mode): mean / invstd
+ *                  are constants, dy = gamma*invstd*dz without the batch-statistic terms
+ *                  (aten native_batch_norm_backward with training=False) */
+#define SRPDE_BN_RELU 1
+#define SRPDE_BN_EVAL 2
 /* srpde_bn_relu_bwd with the (sum dz, sum dz*xhat) reduction already done by the producer of da
  * (srpde_conv_fwd_h3's bn_part, nblk row blocks): skips the reduction pass over y and da */
 int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
@@ -161,6 +168,10 @@ int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const 
 
 /* ---- input staging: NCHW model input -> NHWC (channel-padded) ----------------------- */
 int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w, int cpad, hipStream_t stream);
+/* the way back for the gradient w.r.t. the model input: rows [P, ldx] -> NCHW [n, c, h, w] */
+int srpde_nhwc_to_nchw(const float* x, int ldx, float* out, int n, int c, int h, int w, hipStream_t stream);
+/* y[:, ch] += alpha * x for y NCHW [n, c, hw], x [n, hw] (the residual path of models.py:74,101) */
+int srpde_axpy_channel(float* y, const float* x, int n, int c, int hw, int ch, float alpha, hipStream_t stream);
 
 /* ---- nn.MaxPool2d(2)  (src/models.py:69, used :79-80) -------------------------------- */
 int srpde_maxpool2x2_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int c,

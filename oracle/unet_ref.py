@@ -130,23 +130,30 @@ def up2(x):
     return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
 
 
-def unet_forward(st, x, training: bool):
+def unet_forward(st, x, training: bool, taps=None):
     """UNet.forward, models.py:72-101.  ``st`` running stats are updated in place
-    (functionally: the dict entries are replaced) when ``training``."""
+    (functionally: the dict entries are replaced) when ``training``.  ``taps`` (a dict, for
+    diagnostics): receives the named intermediates with ``retain_grad()`` so their gradients
+    can be compared stage by stage (tools/diag_stages.py)."""
+    def tap(name, t):
+        if taps is not None and t.requires_grad:
+            t.retain_grad()
+            taps[name] = t
+        return t
     coarse = x[:, 0:1]
-    e1 = conv_block(st, "enc1", x, training)
-    e2 = conv_block(st, "enc2", F.max_pool2d(e1, 2), training)
-    e3 = conv_block(st, "enc3", F.max_pool2d(e2, 2), training)
-    b = F.relu(_bn_apply(st, "bridge.1", _conv_apply(st, "bridge.0", e3, 2, 2), training))
-    b = F.relu(_bn_apply(st, "bridge.4", _conv_apply(st, "bridge.3", b, 2, 2), training))
-    e3a = attention_gate(st, "att3", e3, b)
-    d3 = conv_block(st, "dec3", torch.cat([b, e3a], 1), training)
-    e2a = attention_gate(st, "att2", e2, up2(d3))
-    d2 = conv_block(st, "dec2", torch.cat([up2(d3), e2a], 1), training)
-    e1a = attention_gate(st, "att1", e1, up2(d2))
-    d1 = conv_block(st, "dec1", torch.cat([up2(d2), e1a], 1), training)
-    y = F.relu(_bn_apply(st, "out_bn1", _conv_apply(st, "out_conv1", d1, 1), training))
-    y = F.relu(_bn_apply(st, "out_bn2", _conv_apply(st, "out_conv2", y, 1), training))
+    e1 = tap("e1", conv_block(st, "enc1", x, training))
+    e2 = tap("e2", conv_block(st, "enc2", F.max_pool2d(e1, 2), training))
+    e3 = tap("e3", conv_block(st, "enc3", F.max_pool2d(e2, 2), training))
+    b = tap("b1", F.relu(_bn_apply(st, "bridge.1", _conv_apply(st, "bridge.0", e3, 2, 2), training)))
+    b = tap("b", F.relu(_bn_apply(st, "bridge.4", _conv_apply(st, "bridge.3", b, 2, 2), training)))
+    e3a = tap("e3a", attention_gate(st, "att3", e3, b))
+    d3 = tap("d3", conv_block(st, "dec3", torch.cat([b, e3a], 1), training))
+    e2a = tap("e2a", attention_gate(st, "att2", e2, tap("u3g", up2(d3))))
+    d2 = tap("d2", conv_block(st, "dec2", torch.cat([tap("u3c", up2(d3)), e2a], 1), training))
+    e1a = tap("e1a", attention_gate(st, "att1", e1, tap("u2g", up2(d2))))
+    d1 = tap("d1", conv_block(st, "dec1", torch.cat([tap("u2c", up2(d2)), e1a], 1), training))
+    y = tap("o1", F.relu(_bn_apply(st, "out_bn1", _conv_apply(st, "out_conv1", d1, 1), training)))
+    y = tap("o2", F.relu(_bn_apply(st, "out_bn2", _conv_apply(st, "out_conv2", y, 1), training)))
     y = _conv_apply(st, "final", y)
     return y + coarse
 

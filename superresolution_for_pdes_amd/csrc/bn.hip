@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
       float xh, dz;
 #define BN_ACC(X)                                              \
   xh = (v.X - mu.X) * is.X;                                    \
-  dz = (!relu || xh * g.X + b.X > 0.f) ? d.X : 0.f;            \
+  dz = (!(relu & 1) || xh * g.X + b.X > 0.f) ? d.X : 0.f;      \
   s1.X += dz;                                                  \
   s2.X += dz * xh;
       BN_ACC(x) BN_ACC(y) BN_ACC(z) BN_ACC(w)
@@ -229,7 +229,9 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float2* __restrict__
   }
 }
 
-// dy = gamma*invstd*(dz - sum(dz)/P - xhat*sum(dz*xhat)/P); partial column sums of dy (conv bias grad)
+// train mode: dy = gamma*invstd*(dz - sum(dz)/P - xhat*sum(dz*xhat)/P); eval mode (flags bit 1: the
+// normalisation used the running statistics, constants w.r.t. the input): dy = gamma*invstd*dz.
+// Partial column sums of dy (conv bias grad).  flags bit 0: ReLU after the BN.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ y, int ldy,
                                                            const float* __restrict__ da, int ldda,
                                                            const float* __restrict__ mean,
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     const float4 is = *reinterpret_cast<const float4*>(invstd + c);
     const float4 g = *reinterpret_cast<const float4*>(gamma + c);
     const float4 b = *reinterpret_cast<const float4*>(beta + c);
-    const double invP = 1.0 / (double)P;
+    const double invP = (relu & 2) ? 0.0 : 1.0 / (double)P;
     float4 m1, m2, k;
     m1.x = (float)(sdz[c] * invP); m1.y = (float)(sdz[c + 1] * invP);
     m1.z = (float)(sdz[c + 2] * invP); m1.w = (float)(sdz[c + 3] * invP);
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       float xh, dz;
 #define BN_APPLY(X)                                            \
   xh = (v.X - mu.X) * is.X;                                    \
-  dz = (!relu || xh * g.X + b.X > 0.f) ? d.X : 0.f;            \
+  dz = (!(relu & 1) || xh * g.X + b.X > 0.f) ? d.X : 0.f;      \
   o.X = (dz - m1.X - xh * m2.X) * k.X;                         \
   sb.X += o.X;
       BN_APPLY(x) BN_APPLY(y) BN_APPLY(z) BN_APPLY(w)

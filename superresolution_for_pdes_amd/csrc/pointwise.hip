@@ -22,6 +22,32 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, float* __restri
   }
 }
 
+// gradient w.r.t. the model input: NHWC rows [P, ldx] -> NCHW [N, C, HW] (first C channels)
+__global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int N, int C,
+                                    int HW) {
+  const long long total = (long long)N * C * HW;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long nc = e / HW;
+    const int p = (int)(e - nc * HW);
+    const long long n = nc / C;
+    const int c = (int)(nc - n * C);
+    out[e] = x[(n * HW + p) * ldx + c];
+  }
+}
+
+// y[n, ch, :] += alpha * x[n, :] for y [N, C, HW] (the residual x[:, 0:1] of models.py:74,101)
+__global__ void axpy_channel_kernel(float* __restrict__ y, const float* __restrict__ x, int N, int C, int HW, int ch,
+                                    float alpha) {
+  const long long total = (long long)N * HW;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long n = e / HW;
+    const int p = (int)(e - n * HW);
+    y[(n * C + ch) * HW + p] += alpha * x[e];
+  }
+}
+
 // --------------------------------- max pool ------------------------------------
 // nn.MaxPool2d(2): first maximum in (0,0),(0,1),(1,0),(1,1) order wins (strict >), as aten.
 __global__ void maxpool2_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int ldo, int N,
@@ -991,6 +1017,22 @@ int srpde_nchw_to_nhwc(const float* x, float* out, int n, int cin, int h, int w,
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)n * h * w)), dim3(256), 0, stream, x, out, n, cin,
                      h * w, cpad);
   SRPDE_LAUNCH_CHECK("srpde_nchw_to_nhwc");
+  return 0;
+}
+
+int srpde_nhwc_to_nchw(const float* x, int ldx, float* out, int n, int c, int h, int w, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && out && n > 0 && c > 0 && ldx >= c, "srpde_nhwc_to_nchw: bad args");
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for((long long)n * c * h * w)), dim3(256), 0, stream, x, ldx, out,
+                     n, c, h * w);
+  SRPDE_LAUNCH_CHECK("srpde_nhwc_to_nchw");
+  return 0;
+}
+
+int srpde_axpy_channel(float* y, const float* x, int n, int c, int hw, int ch, float alpha, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && x && n > 0 && ch >= 0 && ch < c && hw > 0, "srpde_axpy_channel: bad args");
+  hipLaunchKernelGGL(axpy_channel_kernel, dim3(grid_for((long long)n * hw)), dim3(256), 0, stream, y, x, n, c, hw, ch,
+                     alpha);
+  SRPDE_LAUNCH_CHECK("srpde_axpy_channel");
   return 0;
 }
 

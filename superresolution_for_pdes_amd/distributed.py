@@ -20,8 +20,12 @@ each step (``broadcast_buffers``), as torch DDP does by default.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
+
+_null = contextlib.nullcontext
 
 
 class GradReducer:
@@ -36,6 +40,7 @@ class GradReducer:
         self.works = []
         self.stream = None
         self.n_buckets = 0
+        self.buckets = []
         self.wait_streams = ()
 
     def _side_stream(self, dev):
@@ -52,11 +57,19 @@ class GradReducer:
         self.wait_streams = tuple(wait_streams)
         self.launched = 0
         self.works = []
+        self.buckets = []
         self.n_buckets = 0
+
+    def _collective(self, chunk):
+        """Issue the bucket's all-reduce on the current stream; returns the async work (or None
+        for a stream-ordered stand-in, see tests/test_gpu_schedule.py)."""
+        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        return dist.all_reduce(chunk, op=op, group=self.pg, async_op=True)
 
     def _launch(self, lo, hi):
         chunk = self.flat[lo:hi]
         st = self._side_stream(self.flat.device)
+        self.buckets.append((lo, hi))
         if st is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.device))
@@ -64,10 +77,9 @@ class GradReducer:
             for s in self.wait_streams:
                 st.wait_stream(s)
             with torch.cuda.stream(st):
-                op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
-                self.works.append((dist.all_reduce(chunk, op=op, group=self.pg, async_op=True), chunk))
+                self.works.append((self._collective(chunk), chunk))
         else:
-            self.works.append((dist.all_reduce(chunk, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), chunk))
+            self.works.append((self._collective(chunk), chunk))
         self.n_buckets += 1
 
     def ready(self, upto: int):
@@ -82,13 +94,13 @@ class GradReducer:
             self.launched = total
         cur = torch.cuda.current_stream(self.flat.device) if self.flat.is_cuda else None
         for work, chunk in self.works:
-            if cur is not None:
-                with torch.cuda.stream(self.stream):
+            # the SUM -> mean division runs on the stream the collective's result is ordered on
+            # (the side stream): on the compute stream it could overtake the copy-back
+            with torch.cuda.stream(self.stream) if cur is not None else _null():
+                if work is not None:
                     work.wait()
-            else:
-                work.wait()
-            if not self.use_avg:
-                chunk.div_(self.world)
+                if not self.use_avg:
+                    chunk.div_(self.world)
         if cur is not None:
             cur.wait_stream(self.stream)
         self.works = []

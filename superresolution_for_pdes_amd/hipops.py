@@ -328,8 +328,13 @@ def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True, amax=None):
     tag_amax(out, amax)
 
 
-def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True, amax=None, part=None):
-    """BN (+ReLU) backward; ``part`` = the reduction already produced by conv_fwd(bn_bwd=...)."""
+BN_RELU, BN_EVAL = 1, 2   # srpde_bn_relu_bwd flags (include/srpde.h)
+
+
+def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu=True, amax=None, part=None,
+                eval_mode=False):
+    """BN (+ReLU) backward; ``part`` = the reduction already produced by conv_fwd(bn_bwd=...).
+    ``eval_mode``: the forward used the running statistics (no batch-statistic terms)."""
     P, C = y.shape
     py, ldy = _pl(y)
     pda, ldda = _pl(da)
@@ -337,7 +342,7 @@ def bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias, relu
     ws_bytes = int(query("srpde_bn_relu_bwd_workspace_size", P, C))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
     args = (py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pdy, lddy,
-            _p(dgamma), _p(dbeta), _p(dbias), P, C, int(relu), _p(amax))
+            _p(dgamma), _p(dbeta), _p(dbias), P, C, (BN_RELU if relu else 0) | (BN_EVAL if eval_mode else 0), _p(amax))
     if part is None:
         call("srpde_bn_relu_bwd", *args, ws.data_ptr(), ws_bytes, stream_ptr())
     else:
@@ -351,6 +356,21 @@ def nchw_to_nhwc(x, cpad):
     out = empty(n * h * w, cpad, device=x.device)
     call("srpde_nchw_to_nhwc", x.data_ptr(), out.data_ptr(), n, c, h, w, cpad, stream_ptr())
     return out
+
+
+def nhwc_to_nchw(x, n, c, h, w):
+    """[P, >=c] rows -> contiguous [n, c, h, w] (srpde_nhwc_to_nchw)."""
+    px, ldx = _pl(x)
+    out = torch.empty(n, c, h, w, dtype=F32, device=x.device)
+    call("srpde_nhwc_to_nchw", px, ldx, out.data_ptr(), n, c, h, w, stream_ptr())
+    return out
+
+
+def axpy_(y, x, channel=0, channels=1, alpha=1.0):
+    """y[:, channel] += alpha * x for y [n, channels, h, w] and x [n * h * w] (srpde_axpy_channel)."""
+    n = y.shape[0]
+    hw = y[0, 0].numel()
+    call("srpde_axpy_channel", y.data_ptr(), x.data_ptr(), n, channels, hw, channel, float(alpha), stream_ptr())
 
 
 def maxpool_fwd(x, n, h, w):

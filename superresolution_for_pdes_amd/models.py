@@ -81,8 +81,7 @@ class _ConvBlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         blk = ctx.blk
         n, h, w = ctx.shape
-        if not blk.training:
-            raise NotImplementedError("HIP ConvBlock backward is implemented for train-mode BatchNorm")
+        # eval mode is handled inside (the BN backward drops its batch-statistic terms)
         da = _to_rows(dout)
         params = [blk.conv1.weight, blk.conv1.bias, blk.bn1.weight, blk.bn1.bias,
                   blk.conv2.weight, blk.conv2.bias, blk.bn2.weight, blk.bn2.bias]

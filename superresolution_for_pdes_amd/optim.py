@@ -85,6 +85,15 @@ class FusedAdamW(torch.optim.Optimizer):
             self._flat[key] = fb
         return fb
 
+    def state_dict(self):
+        """torch.optim.AdamW's layout: every parameter's state holds its OWN ``step`` tensor (the
+        fused path shares one counter internally; a shared tensor in a checkpoint would be
+        incremented once per parameter by torch's AdamW after loading)."""
+        sd = super().state_dict()
+        sd["state"] = {k: {kk: (vv.clone() if kk == "step" and torch.is_tensor(vv) else vv) for kk, vv in v.items()}
+                       for k, v in sd["state"].items()}
+        return sd
+
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm, grad_scale=1.0):
         """clip_grad_norm_(all params, max_norm) on device.  Like torch's, the NEXT step()

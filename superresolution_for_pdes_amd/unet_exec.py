@@ -56,6 +56,16 @@ class _Saved:
     pass
 
 
+# diagnostics hook (tools/diag_stages.py): when a dict, unet_backward stores a copy of each
+# named activation gradient as soon as it is final
+DEBUG_TAPS = None
+
+
+def _tap(name, t):
+    if DEBUG_TAPS is not None:
+        DEBUG_TAPS[name] = t.detach().clone()
+
+
 # bench/profiling hook: {conv module name: list} -> (start, end) HIP events recorded on the
 # compute stream around that layer's forward conv launch
 TIMED_LAYERS = {}
@@ -173,7 +183,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
     # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
     # the weight gradient reads the stored split
-    saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp)
+    saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
     if not activate:
         slot = slots.take()
         aff = H.bn_affine(mean, invstd, bn.weight, bn.bias, P, amax=slot)
@@ -246,11 +256,15 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     ``below = (bn, saved)``: the BN + ReLU whose output this layer reads; when the dgrad runs on
     h3 into a fresh ``dx`` it also produces that BN's reduction, returned for the next call.
     ``wq``: a WgradStream that takes the weight-gradient launch off the compute stream."""
-    x0, x1, y, mean, invstd, xp = saved
+    x0, x1, y, mean, invstd, xp, train = saved
     P, cout = y.shape
     dy = H.empty(P, cout, device=y.device)
+    # eval mode: the forward normalised with the running statistics (constants), so the BN
+    # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
     H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
-                  amax=slots.take(), part=part)
+                  amax=slots.take(), part=part, eval_mode=not train)
+    if DEBUG_TAPS is not None:
+        _tap("dy:" + getattr(conv, "_srpde_name", "?"), dy)
     dyp = None
     out_part = None
     cin = conv.in_channels if x0 is None else x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
@@ -387,8 +401,10 @@ def unet_forward(m, x, training, save=False):
     return out.view(n, 1, h, w), S
 
 
-def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
+def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     """Reverse schedule.  ``grads``: param -> writable view (every one is fully written).
+    ``want_dx``: also return the gradient w.r.t. the input x ([B, 3, H, W]; enc1.conv1's
+    dgrad plus the residual's identity path into channel 0, models.py:74,101).
     ``grad_ready(group)`` is called as soon as a module group's gradients are queued (with
     ``wq``, a WgradStream, the weight gradients run on its side stream: a consumer waits for
     that stream too; the compute stream joins it before this returns)."""
@@ -403,19 +419,24 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     # head
     do2 = H.empty(P1, 16, device=dev)
     H.head_bwd(dout, S.o2, m.final.weight, n, hw1, do2, grads[m.final.weight], grads[m.final.bias])
+    _tap("o2", do2)
     ready("final")
     do1 = H.empty(P1, m.out_conv1.out_channels, device=dev)
     part = _cbr_bwd(m.out_conv2, m.out_bn2, S.out2, do2, n, h, w, 1, grads, slots, do1, below=(m.out_bn1, S.out1),
                     wq=wq)
     ready("out_bn2"); ready("out_conv2")
+    _tap("o1", do1)
     dd1 = H.empty(P1, 64, device=dev)
     # out_conv1's dgrad writes dec1's output gradient: its epilogue also reduces dec1.bn2's backward
     part = _cbr_bwd(m.out_conv1, m.out_bn1, S.out1, do1, n, h, w, 1, grads, slots, dd1, part=part,
                     below=(m.dec1.bn2, S.dec1[1]), wq=wq)
     ready("out_bn1"); ready("out_conv1")
+    _tap("d1", dd1)
     # dec1: grad of cat[u2 (128), e1a (64)]
     dcat1 = H.empty(P1, 192, device=dev)
     _block_bwd(m.dec1, S.dec1, dd1, n, h, w, grads, slots, dcat1, wq=wq, part=part)
+    _tap("u2c", dcat1[:, :128])
+    _tap("e1a", dcat1[:, 128:])
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
     # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below
@@ -423,9 +444,12 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     ready("att1")
     dd2 = H.empty(P2, 128, device=dev)
     H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate)
+    _tap("d2", dd2)
     # dec2: grad of cat[u3 (256), e2a (128)]
     dcat2 = H.empty(P2, 384, device=dev)
     _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2, wq=wq)
+    _tap("u3c", dcat2[:, :256])
+    _tap("e2a", dcat2[:, 256:])
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
     # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
@@ -433,32 +457,46 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None):
     ready("att2")
     dd3 = H.empty(P3, 256, device=dev)
     H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate)
+    _tap("d3", dd3)
     # dec3: grad of cat[b (512), e3a (256)]
     dcat3 = H.empty(P3, 768, device=dev)
     _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq)
+    _tap("e3a", dcat3[:, 512:])
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)
     _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True, wq=wq)
+    _tap("b", dcat3[:, :512])
     ready("att3")
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
     part = _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1,
                     below=(m.bridge[1], S.br1), wq=wq)
+    _tap("b1", dab1)
     _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True, part=part, wq=wq)
+    _tap("e3", de3)
     ready("bridge")
     # encoder
     dp2 = H.empty(P3, 128, device=dev)
     _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, slots, dp2, wq=wq)
     ready("enc3")
     H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
+    _tap("e2", de2)
     dp1 = H.empty(P2, 64, device=dev)
     _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1, wq=wq)
     ready("enc2")
     H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
-    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, None, wq=wq)
+    _tap("e1", de1)
+    dx4 = H.empty(P1, S.x4.shape[1], device=dev) if want_dx else None
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, dx4, wq=wq)
     ready("enc1")
     if wq is not None:
         wq.join()
+    if dx4 is None:
+        return None
+    # NHWC [P, 4] -> NCHW [B, 3, H, W], and the residual x[:, 0:1] passes dout straight through
+    dx = H.nhwc_to_nchw(dx4, n, 3, h, w)
+    H.axpy_(dx, dout, channel=0, channels=3)
+    return dx
 
 
 class UNetFunction(torch.autograd.Function):
@@ -475,8 +513,6 @@ class UNetFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         model = ctx.model
-        if ctx.needs_input_grad[0]:
-            raise NotImplementedError("gradient w.r.t. the U-Net input is not provided by the HIP path")
         layout = model._flat_layout()
         total = layout[-1][2] + layout[-1][3]
         flat = torch.empty(total, dtype=torch.float32, device=dout.device)
@@ -497,11 +533,11 @@ class UNetFunction(torch.autograd.Function):
             if reducer is not None:
                 reducer.begin(flat, wait_streams=() if wq is None else (wq.side,))
                 hook = lambda grp: reducer.ready(ends[grp])  # noqa: E731
-            unet_backward(model, ctx.saved, dout, views, hook, wq=wq)
+            dx = unet_backward(model, ctx.saved, dout, views, hook, wq=wq, want_dx=ctx.needs_input_grad[0])
             if reducer is not None:
                 reducer.finish()
         if hi is not None:
             cur.wait_stream(hi)
         ctx.saved = None
         grads = [views[p] for p in model._param_list()]
-        return (None, None, *grads)
+        return (dx, None, *grads)

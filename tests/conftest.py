@@ -38,4 +38,5 @@ def golden():
     import numpy as np
 
     d = os.path.join(ROOT, "tests", "golden")
-    return {k: np.load(os.path.join(d, f"{k}_fixture.npz")) for k in ("unet", "poisson", "datagen", "cascade")}
+    return {k: np.load(os.path.join(d, f"{k}_fixture.npz")) for k in ("unet", "poisson", "datagen", "cascade",
+                                                                             "unet_b1024", "cascade640")}

@@ -18,6 +18,18 @@ Fixtures:
   datagen_fixture.npz  generate_dataset / generate_subdomain_dataset / combine_datasets
                        with seeded np.random, PDEDataset stats and items
   cascade_fixture.npz  solve_multi_resolution(40,[80,160]) + ml_multi_level_upscale to 160
+  unet_b1024_fixture.npz  the bench configuration (#2): B=1024 train-mode forward + MSE backward
+                       + clip + AdamW in fp64 and fp32 (output samples and per-sample sums, all
+                       16 BNs' running stats, per-parameter gradient norms and samples, one
+                       optimizer step).  The fp64 run wraps the reference's blocks in
+                       torch.utils.checkpoint (same ops, recomputed in backward) to fit in host
+                       memory; running stats are read before the recompute touches them.
+  cascade640_fixture.npz  solve_multi_resolution(40,[80..640]) + ml_multi_level_upscale to
+                       320 and 640, plus the bilinear / bicubic multi-level and direct baselines
+                       (resolution_comparison_enhanced.py:19-65, :355-408) and their metrics
+
+Usage: ``make_golden.py [name ...]`` (default: the four fast fixtures; ``unet_b1024`` and
+``cascade640`` take minutes and are generated on request).
 """
 from __future__ import annotations
 
@@ -189,10 +201,119 @@ def cascade_fixture():
     np.savez_compressed(os.path.join(HERE, "cascade_fixture.npz"), **out)
 
 
+B1024_SAMPLE_K = 256
+B1024_CKPT = ["enc1", "enc2", "enc3", "bridge", "att3", "dec3", "att2", "dec2", "att1", "dec1"]
+
+
+def _b1024_run(tag):
+    """One reference train step at B=1024 in fp64 ("64") or fp32 ("32"); returns a dict of arrays."""
+    import functools
+    from torch.utils.checkpoint import checkpoint
+    torch.set_num_threads(os.cpu_count())
+    dt = torch.float64 if tag == "64" else torch.float32
+    x, t = fixture_inputs(1024, seed=11)
+    m = ref_model(dt).train()
+    if tag == "64":
+        for name in B1024_CKPT:
+            mod = getattr(m, name)
+            mod.forward = functools.partial(checkpoint, mod.forward, use_reentrant=False)
+    xx = torch.from_numpy(x).to(dt)
+    y = m(xx)
+    loss = torch.nn.MSELoss()(y, torch.from_numpy(t).to(dt))
+    out = {}
+    # BN running stats after the forward, before a checkpoint recompute updates them again
+    for k, v in m.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            out[f"rs{tag}:{k}"] = v.double().numpy().copy()
+    yf = y.detach().reshape(-1)
+    idx = np.arange(0, yf.numel(), 97, dtype=np.int64)
+    out["out_idx"] = idx
+    out[f"out{tag}"] = yf[idx].double().numpy()
+    out[f"out_sum{tag}"] = y.detach().double().sum(dim=(1, 2, 3)).numpy()
+    out[f"out_sq{tag}"] = (y.detach().double() ** 2).sum(dim=(1, 2, 3)).numpy()
+    out[f"loss{tag}"] = np.array(loss.item())
+    loss.backward()
+    names = trainable_names()
+    params = dict(m.named_parameters())
+    gn = []
+    for i, n in enumerate(names):
+        g = params[n].grad.detach().reshape(-1)
+        gn.append(float(torch.linalg.vector_norm(g.double())))
+        gi = sample_indices(g.numel(), 5000 + i, k=B1024_SAMPLE_K)
+        out[f"gidx:{n}"] = gi
+        out[f"gval{tag}:{n}"] = g[gi].double().numpy()
+    out[f"gnorm{tag}"] = np.array(gn)
+    # one clip + AdamW step exactly as train_enhanced.py:74-75, 308
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    tot = torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+    out[f"clip_total{tag}"] = np.array(float(tot))
+    opt.step()
+    for n in names:
+        p = params[n].detach().reshape(-1)
+        out[f"pval{tag}:{n}"] = p[out[f"gidx:{n}"]].double().numpy()
+    return out
+
+
+def unet_b1024_fixture():
+    """Config #2 at full size (B=1024, train mode).  fp64 and fp32 run in separate child
+    processes (each needs ~20 GB of host memory)."""
+    import subprocess
+    import tempfile
+    merged = {"B": np.array(1024), "input_seed": np.array(11)}
+    with tempfile.TemporaryDirectory() as td:
+        for tag in ("64", "32"):
+            dst = os.path.join(td, f"b{tag}.npz")
+            subprocess.run([sys.executable, os.path.abspath(__file__), f"_b1024:{tag}:{dst}"], check=True)
+            with np.load(dst) as z:
+                merged.update({k: z[k] for k in z.files})
+    np.savez_compressed(os.path.join(HERE, "unet_b1024_fixture.npz"), **merged)
+
+
+def cascade640_fixture():
+    """Config #5's cascade pinned to 640^2, with the paired interpolation baselines."""
+    import resolution_comparison_enhanced as ref_rce
+    torch.set_num_threads(os.cpu_count())
+    np.random.seed(0)
+    data = ref_rc.solve_multi_resolution(40, [80, 160, 320, 640])
+    m = ref_model(torch.float32).eval()
+    out = {"k1": np.array(data["k1"]), "k2": np.array(data["k2"]), "u40": data["u"][40]}
+    sub = {80: (1, 1), 160: (1, 1), 320: (2, 3), 640: (3, 5)}   # stored grid strides (rows, cols)
+    for r in (40, 80, 160, 320, 640):
+        u = data["u"][r]
+        out[f"u{r}_stats"] = np.array([u.mean(), u.std(), np.linalg.norm(u), u.min(), u.max()])
+        out[f"u{r}_row"] = u[r // 3].copy()
+    for tgt in (80, 160, 320, 640):
+        ml = ref_rc.ml_multi_level_upscale(m, data, tgt, "cpu")
+        out[f"ml{tgt}"] = ml.astype(np.float32) if tgt >= 320 else ml
+        u40 = torch.from_numpy(data["u"][40]).float()[None, None]
+        sols = {
+            "blm": ref_rce.bilinear_multi_level_upscale(data, tgt),
+            "cbm": ref_rce.cubic_multi_level_upscale(data, tgt),
+            "bld": torch.nn.functional.interpolate(u40, size=(tgt, tgt), mode="bilinear",
+                                                   align_corners=True).squeeze().numpy(),
+            "cbd": torch.nn.functional.interpolate(u40, size=(tgt, tgt), mode="bicubic",
+                                                   align_corners=True).squeeze().numpy(),
+            "ml": ml,
+        }
+        sr, sc = sub[tgt]
+        for k, v in sols.items():
+            e = v - data["u"][tgt]
+            out[f"{k}{tgt}_metrics"] = np.array([np.mean(np.abs(e)), np.sqrt(np.mean(e ** 2))])
+            if k != "ml":
+                out[f"{k}{tgt}"] = v[::sr, ::sc].copy()
+    np.savez_compressed(os.path.join(HERE, "cascade640_fixture.npz"), **out)
+
+
+FIXTURES = {"unet": unet_fixture, "poisson": poisson_fixture, "datagen": datagen_fixture,
+            "cascade": cascade_fixture, "unet_b1024": unet_b1024_fixture, "cascade640": cascade640_fixture}
+
 if __name__ == "__main__":
-    unet_fixture()
-    poisson_fixture()
-    datagen_fixture()
-    cascade_fixture()
+    args = sys.argv[1:]
+    if args and args[0].startswith("_b1024:"):
+        _, tag, dst = args[0].split(":", 2)
+        np.savez(dst, **_b1024_run(tag))
+        sys.exit(0)
+    for name in args or ["unet", "poisson", "datagen", "cascade"]:
+        FIXTURES[name]()
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -78,3 +78,65 @@ def test_grad_reducer_and_buffer_broadcast_world2():
         assert ok_params and ok_buf
     shards = [set(r[5]) for r in res]
     assert not shards[0] & shards[1] and shards[0] | shards[1] == set(range(10))
+
+
+def _unet_layout_worker(rank, world, port, q):
+    """GradReducer over the U-Net's REAL flat layout, fed the executor's group-end prefix sequence
+    (unet_exec.FLAT_GROUPS order, _group_end_offsets), with different gradients per rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from superresolution_for_pdes_amd.distributed import GradReducer
+        from superresolution_for_pdes_amd.models import UNet
+        from superresolution_for_pdes_amd.unet_exec import FLAT_GROUPS, _group_end_offsets, flat_layout
+        m = UNet()
+        layout = flat_layout(m)
+        total = layout[-1][2] + layout[-1][3]
+        ends = _group_end_offsets(layout)
+        g = torch.Generator().manual_seed(100 + rank)
+        local = torch.randn(total, generator=g)
+        flat = local.clone()
+        bucket = 2 << 20                               # 2 MB = 524,288 floats
+        red = GradReducer(bucket_bytes=bucket)
+        red.begin(flat)
+        tail_ok = True
+        prev = 0
+        for grp in FLAT_GROUPS:                        # the order the backward finishes groups
+            assert ends[grp] >= prev                   # a growing prefix
+            prev = ends[grp]
+            red.ready(ends[grp])
+            # nothing beyond the launched prefix is touched before finish()
+            tail_ok &= torch.equal(flat[red.launched:], local[red.launched:])
+        launched_before_finish = red.launched
+        red.finish()
+        q.put((rank, total, flat, tail_ok, list(red.buckets), launched_before_finish, red.bucket))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_reducer_unet_layout_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_unet_layout_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = res[0][1]
+    assert total == 7_834_588
+    locals_ = [torch.randn(total, generator=torch.Generator().manual_seed(100 + r)) for r in range(world)]
+    want = (locals_[0] + locals_[1]) / 2              # AVG semantics
+    for rank, _, flat, tail_ok, buckets, launched, bsz in res:
+        assert tail_ok, rank
+        assert torch.allclose(flat, want, rtol=0, atol=1e-6), rank
+        # full buckets while the backward runs, in order, tiling [0, total) exactly; the tail at finish
+        assert buckets[0][0] == 0 and buckets[-1][1] == total
+        assert all(a[1] == b[0] for a, b in zip(buckets, buckets[1:]))
+        assert all(hi - lo == bsz for lo, hi in buckets[:-1]) and 0 < buckets[-1][1] - buckets[-1][0] <= bsz
+        assert launched == (total // bsz) * bsz
+    assert res[0][4] == res[1][4]                      # identical bucket boundaries on both ranks

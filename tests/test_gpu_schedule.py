@@ -86,6 +86,44 @@ def test_data_parallel_world1_is_bit_identical():
         dist.destroy_process_group()
 
 
+def test_reducer_buckets_wait_for_their_gradients():
+    """World-1 stand-in for the data-parallel reducer whose "collective" scales its bucket by 3 on
+    the reducer stream.  A bucket launched before every kernel writing into it finished (dgrad-chain
+    BN / head gradients on the high-priority stream, wgrad and attention parameter gradients on the
+    side stream) would be overwritten unscaled: the gradients must equal exactly 3x the plain ones."""
+    from superresolution_for_pdes_amd.distributed import GradReducer
+    from superresolution_for_pdes_amd.models import UNet, init_weights
+
+    class ScaleReducer(GradReducer):
+        def __init__(self, bucket_bytes):   # no process group
+            self.pg, self.bucket, self.world, self.backend, self.use_avg = None, bucket_bytes // 4, 1, "fake", True
+            self.flat, self.launched, self.works, self.stream = None, 0, [], None
+            self.n_buckets, self.buckets, self.wait_streams = 0, [], ()
+
+        def _collective(self, chunk):
+            chunk.mul_(3.0)
+            return None
+
+    torch.manual_seed(2)
+    ref = UNet()
+    ref.apply(init_weights)
+    state = {k: v.clone() for k, v in ref.state_dict().items()}
+    x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(7)).to(DEV)
+    x[:, 1] = 1.0
+    a = _train_step(x, state, True)
+    m = UNet()
+    m.load_state_dict(state)
+    m = m.to(DEV).train()
+    m._grad_reducer = ScaleReducer(1 << 20)
+    out = m(x)
+    (out ** 2).mean().backward()
+    torch.cuda.synchronize()
+    assert m._grad_reducer.n_buckets >= 8
+    assert torch.equal(a[0], out.detach())
+    for n, p in m.named_parameters():
+        assert torch.equal(a[1][n] * 3.0, p.grad), n
+
+
 @pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (6, 256, 0, 512, 10, 2),
                                                  (4, 256, 128, 128, 20, 1), (3, 64, 0, 32, 40, 1),
                                                  (5, 128, 64, 64, 40, 1)])

@@ -160,3 +160,107 @@ def test_fused_bn_backward_reduction_matches_separate_pass():
             continue   # true gradient 0 (bias feeding BatchNorm): noise only
         e = float((g - r).norm() / max(float(r.norm()), 1e-30))
         assert e < 1e-4, (n, e)
+
+
+def _grad_errors(m, ref_grads):
+    params = dict(m.named_parameters())
+    out = {}
+    for n, r in ref_grads.items():
+        g = params[n].grad.detach().double().cpu()
+        out[n] = float((g - r).norm() / max(float(r.norm()), 1e-30))
+    return out
+
+
+def test_eval_mode_backward_matches_oracle():
+    """model.eval(); loss.backward(): BatchNorm normalised with the running statistics, so its
+    backward has no batch-statistic terms.  Every parameter gradient and the input
+    gradient against the fp64 oracle (autograd through the reference op sequence).  A wrong
+    (train-mode) BN backward is off by O(1); the bar is max(1e-4, 3x the oracle's own fp32 error)."""
+    from oracle.unet_ref import clone_state, forward_with_grads, unet_forward as ref_fwd
+    st = fixture_state_torch(torch.float64)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(8, 3, 40, 40, generator=g)
+    x[:, 1] = 1.0
+    t = torch.randn(8, 1, 40, 40, generator=g)
+    m = make_model(False)
+    xd = x.to(DEV).requires_grad_(True)
+    out = m(xd)
+    loss = torch.nn.functional.mse_loss(out, t.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_out, ref_loss, ref_grads, _ = forward_with_grads(st, x.double(), t.double(), training=False)
+    _, _, g32, _ = forward_with_grads(clone_state(st, torch.float32), x, t, training=False)
+    assert rmse(out.detach().cpu(), ref_out) <= 2e-5
+    errs = _grad_errors(m, ref_grads)
+    bad = {}
+    for n, e in errs.items():
+        r = ref_grads[n]
+        e32 = float((g32[n].double() - r).norm() / max(float(r.norm()), 1e-30))
+        if e > max(1e-4, 3 * e32):
+            bad[n] = (e, e32)
+    assert not bad, bad
+    # input gradient (enc1.conv1's dgrad + the residual x[:, 0:1] path)
+    gx_ref = {}
+    for dt in (torch.float64, torch.float32):
+        xr = x.to(dt).requires_grad_(True)
+        lr_ = torch.nn.functional.mse_loss(ref_fwd(clone_state(st, dt), xr, False), t.to(dt))
+        (gx_ref[dt],) = torch.autograd.grad(lr_, xr)
+    gx = xd.grad.detach().double().cpu()
+    ref = gx_ref[torch.float64]
+    e = float((gx - ref).norm() / ref.norm())
+    e32 = float((gx_ref[torch.float32].double() - ref).norm() / ref.norm())
+    assert e <= max(1e-4, 3 * e32), (e, e32)
+    # running statistics untouched by an eval-mode forward
+    assert int(m.state_dict()["enc1.bn1.num_batches_tracked"]) == 0
+
+
+def test_train_mode_input_gradient_matches_oracle():
+    """Gradient w.r.t. the U-Net input in train mode (previously NotImplementedError)."""
+    from oracle.unet_ref import clone_state, unet_forward as ref_fwd
+    st = fixture_state_torch(torch.float64)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(32, 3, 40, 40, generator=g)
+    x[:, 1] = 1.0
+    t = torch.randn(32, 1, 40, 40, generator=g)
+    m = make_model(True)
+    xd = x.to(DEV).requires_grad_(True)
+    torch.nn.functional.mse_loss(m(xd), t.to(DEV)).backward()
+    gx_ref = {}
+    for dt in (torch.float64, torch.float32):
+        xr = x.to(dt).requires_grad_(True)
+        lr_ = torch.nn.functional.mse_loss(ref_fwd(clone_state(st, dt), xr, True), t.to(dt))
+        (gx_ref[dt],) = torch.autograd.grad(lr_, xr)
+    gx = xd.grad.detach().double().cpu()
+    assert gx.shape == x.shape
+    ref = gx_ref[torch.float64]
+    e = float((gx - ref).norm() / ref.norm())
+    e32 = float((gx_ref[torch.float32].double() - ref).norm() / ref.norm())
+    # train-mode BN backward cancellation: the reference's own fp32 input gradient is the floor
+    assert e <= max(1e-4, 3 * e32), (e, e32)
+
+
+def test_convblock_eval_backward_matches_torch():
+    """ConvBlock in eval mode supports backward (previously NotImplementedError)."""
+    from superresolution_for_pdes_amd.models import ConvBlock
+    torch.manual_seed(0)
+    blk = ConvBlock(64, 64)
+    ref = torch.nn.Sequential(blk.conv1, blk.bn1, torch.nn.ReLU(), blk.conv2, blk.bn2, torch.nn.ReLU())
+    with torch.no_grad():
+        for bn in (blk.bn1, blk.bn2):
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 1.5)
+    ref64 = __import__("copy").deepcopy(ref).double().eval()
+    blk = blk.to(DEV).eval()
+    x = torch.randn(4, 64, 20, 20)
+    xd = x.to(DEV).requires_grad_(True)
+    y = blk(xd)
+    (y ** 2).mean().backward()
+    xr = x.double().requires_grad_(True)
+    yr = ref64(xr)
+    (yr ** 2).mean().backward()
+    assert rmse(y.detach().cpu(), yr.detach()) <= 1e-5 * float(yr.std())
+    e = float((xd.grad.cpu().double() - xr.grad).norm() / xr.grad.norm())
+    assert e <= 1e-4, e
+    for (n, p), (_, q) in zip(blk.named_parameters(), ref64.named_parameters()):
+        e = float((p.grad.cpu().double() - q.grad).norm() / max(float(q.grad.norm()), 1e-30))
+        assert e <= 1e-4, (n, e)
