@@ -75,29 +75,71 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads():
+    """All host cores this process may use: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    pool) -- os.cpu_count() there reports the whole machine."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(n, int(env))) if env and env.isdigit() else n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds):
-    """Oracle (torch-CPU restatement of UNet + MSE + backward + clip + AdamW) on host cores."""
+    """Oracle (torch-CPU restatement of UNet + MSE + backward + clip + AdamW) on the host cores,
+    as BASELINE.md section 3 / SURVEY 8(d) prescribe: all cores, 2 warm-ups, then the median of
+    >= 5 timed steps (time.perf_counter) at the reference's batch 32.  Also config #1 as the
+    reference runs it: train_model for one epoch on 64 samples (80/20 split, batch 32: two train
+    steps on 51 samples, one eval batch of 13), median of 3 epochs."""
+    import statistics
     from oracle import unet_ref as U
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     st = U.kaiming_init_state(0)
     b = 32
     g = torch.Generator().manual_seed(1)
-    x = torch.randn(b, 3, 40, 40, generator=g)
+    x = torch.randn(64, 3, 40, 40, generator=g)
     x[:, 1] = 1.0
-    t = torch.randn(b, 1, 40, 40, generator=g)
-    opt = None
-    U.train_step(st, x, t, opt_state=opt)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    step = 1
-    while time.perf_counter() - t0 < seconds or n < 2:
+    t = torch.randn(64, 1, 40, 40, generator=g)
+    opt, step = None, 0
+    for _ in range(2):   # warm-ups
         step += 1
-        _, st, _, opt, _ = U.train_step(st, x, t, opt_state=opt, step=step)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * b / dt, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle train steps (fwd+MSE+bwd+clip+AdamW) at batch {b} on host CPU, "
-                      f"{dt:.1f}s, torch {torch.__version__} threads={threads}"}
+        _, st, _, opt, _ = U.train_step(st, x[:b], t[:b], opt_state=opt, step=step)
+    times, t_all = [], time.perf_counter()
+    while len(times) < 5 or (time.perf_counter() - t_all < 0.6 * seconds and len(times) < 200):
+        step += 1
+        t0 = time.perf_counter()
+        _, st, _, opt, _ = U.train_step(st, x[:b], t[:b], opt_state=opt, step=step)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    # config #1: one train_model epoch on 64 samples (train_enhanced.py:60-92 with the oracle step)
+    tr, va = slice(0, 51), slice(51, 64)
+    epochs = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        for lo in range(0, 51, b):
+            step += 1
+            sl = slice(lo, min(lo + b, 51))
+            _, st, _, opt, _ = U.train_step(st, x[tr][sl], t[tr][sl], opt_state=opt, step=step)
+        with torch.no_grad():
+            torch.nn.functional.mse_loss(U.unet_forward(st, x[va], False), t[va])
+        epochs.append(time.perf_counter() - t0)
+    ep = statistics.median(epochs[1:])
+    return {"value": round(b / med, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"median of {len(times)} oracle train steps (fwd+MSE+bwd+clip+AdamW) at batch {b} after 2 "
+                      f"warm-ups: {1e3 * med:.1f} ms/step; config #1 (train_model epoch, 64 samples, batch 32, "
+                      f"+ val): {ep:.3f} s/epoch = {51 / ep:.1f} train samples/s (median of 3 after 1 warm-up); "
+                      f"torch {torch.__version__}, {threads} threads",
+            "config1_epoch_s": round(ep, 4)}
 
 
 def cpu_baseline_poisson(seconds, sizes=(40, 80)):
@@ -380,6 +422,11 @@ def main():
             except (ValueError, OSError):
                 traffic = None
         samples = world * B * args.steps
+        # whole-step fraction: algorithmic FLOP of every 3x3 conv pass the step runs (forward,
+        # dgrad except enc1.conv1's, whose input needs no gradient, and wgrad) at batch B, over the
+        # step time, against the same roof -- BN / attention / pooling / optimizer time included
+        step_flop = sum(conv_flops(c, o, h) * B * (3 if n != "enc1.conv1" else 2) for n, c, o, h in CONV3)
+        step_ach = step_flop / (elapsed / args.steps) / 1e12
         rec = {
             "metric": "20->40 SR training samples/sec at batch 1024 per GPU (fwd+MSE bwd+clip+AdamW)",
             "value": round(samples / elapsed, 2),
@@ -402,7 +449,9 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(kern_avg, 4),
-                         "algorithmic_flop_per_launch": flops_launch},
+                         "algorithmic_flop_per_launch": flops_launch,
+                         "step": {"algorithmic_flop": step_flop, "achieved": round(step_ach, 2),
+                                  "frac": round(step_ach / peak, 4)}},
         }
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -191,6 +191,12 @@ int srpde_pde_dataset_assemble(const float* u_coarse, const float* u_fine, const
                                const float* f_fine, const float* stats, int theta_constant, int n, int hc, int wc,
                                int hf, int wf, float* inputs, float* targets, hipStream_t stream);
 
+/* ---- bicubic, align_corners=True, single-channel fields [planes][h][w] -> [planes][ho][wo]:
+ *      F.interpolate(mode='bicubic') of the cascade's interpolation baselines
+ *      (src/resolution_comparison_enhanced.py:43-65 multi-level, :386-392 direct) --------- */
+int srpde_resize_bicubic_ac(const float* x, float* out, int planes, int h, int w, int ho, int wo,
+                            hipStream_t stream);
+
 /* ---- bilinear, align_corners=True: nn.Upsample(2) (models.py:70, :89-93) and the
  *      F.interpolate(size=(40,40)) of PDEDataset (models.py:182-187) ------------------ */
 int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho, int wo,

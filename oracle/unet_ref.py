@@ -106,17 +106,37 @@ def _conv_apply(st, name, x, padding=0, dilation=1):
     return F.conv2d(x, st[f"{name}.weight"], st[f"{name}.bias"], padding=padding, dilation=dilation)
 
 
-def conv_block(st, name, x, training):
+def _relu(z, decisions, key):
+    """F.relu / nn.ReLU; with ``decisions`` (see unet_forward) the ReLU takes the given branch
+    mask instead of deciding from its own (fp64) input: relu(z) := z * mask."""
+    if decisions is None:
+        return F.relu(z)
+    return z * decisions[key].to(device=z.device, dtype=z.dtype)
+
+
+def _maxpool(x, decisions, key):
+    """F.max_pool2d(x, 2); with ``decisions`` the window maxima are taken at the given argmax
+    indices (max_pool2d_with_indices layout: flat h*W+w per channel plane)."""
+    if decisions is None:
+        return F.max_pool2d(x, 2)
+    idx = decisions[key].to(x.device)
+    n, c, h2, w2 = idx.shape
+    return x.flatten(2).gather(2, idx.flatten(2)).view(n, c, h2, w2)
+
+
+def conv_block(st, name, x, training, decisions=None):
     """ConvBlock.forward, models.py:21-24."""
-    x = F.relu(_bn_apply(st, f"{name}.bn1", _conv_apply(st, f"{name}.conv1", x, 1), training))
-    x = F.relu(_bn_apply(st, f"{name}.bn2", _conv_apply(st, f"{name}.conv2", x, 1), training))
+    x = _relu(_bn_apply(st, f"{name}.bn1", _conv_apply(st, f"{name}.conv1", x, 1), training), decisions,
+              f"{name}.bn1")
+    x = _relu(_bn_apply(st, f"{name}.bn2", _conv_apply(st, f"{name}.conv2", x, 1), training), decisions,
+              f"{name}.bn2")
     return x
 
 
-def attention_gate(st, name, x, gating):
+def attention_gate(st, name, x, gating, decisions=None):
     """AttentionGate.forward, models.py:119-130."""
     m = x.mean(dim=(2, 3), keepdim=True)                                  # AdaptiveAvgPool2d(1)
-    h = F.relu(_conv_apply(st, f"{name}.channel_attention.1", m))
+    h = _relu(_conv_apply(st, f"{name}.channel_attention.1", m), decisions, f"{name}.channel_attention.2")
     ca = torch.sigmoid(_conv_apply(st, f"{name}.channel_attention.3", h))
     x = x * ca
     if gating.shape[-2:] != x.shape[-2:]:                                  # models.py:125-126
@@ -130,30 +150,40 @@ def up2(x):
     return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
 
 
-def unet_forward(st, x, training: bool, taps=None):
+def unet_forward(st, x, training: bool, taps=None, decisions=None):
     """UNet.forward, models.py:72-101.  ``st`` running stats are updated in place
     (functionally: the dict entries are replaced) when ``training``.  ``taps`` (a dict, for
     diagnostics): receives the named intermediates with ``retain_grad()`` so their gradients
-    can be compared stage by stage (tools/diag_stages.py)."""
+    can be compared stage by stage (tools/diag_stages.py).
+
+    ``decisions`` (optional): the discrete choices of another implementation's forward -- the
+    ReLU masks after every BatchNorm (key: the BN's name) and in the channel attention (key
+    ``att*.channel_attention.2``), and the max-pool argmax indices (``pool1``, ``pool2``).  The
+    oracle then evaluates the SAME branch of the piecewise-smooth network in its own precision:
+    an fp32 implementation and fp64 disagree on a ReLU whose input is within rounding of 0,
+    and a single such flip moves an activation gradient by ~1/sqrt(numel) in relative L2 (it
+    is what limits the reference's own fp32-vs-fp64 agreement); on a shared branch the
+    remaining difference is arithmetic error only."""
     def tap(name, t):
         if taps is not None and t.requires_grad:
             t.retain_grad()
             taps[name] = t
         return t
     coarse = x[:, 0:1]
-    e1 = tap("e1", conv_block(st, "enc1", x, training))
-    e2 = tap("e2", conv_block(st, "enc2", F.max_pool2d(e1, 2), training))
-    e3 = tap("e3", conv_block(st, "enc3", F.max_pool2d(e2, 2), training))
-    b = tap("b1", F.relu(_bn_apply(st, "bridge.1", _conv_apply(st, "bridge.0", e3, 2, 2), training)))
-    b = tap("b", F.relu(_bn_apply(st, "bridge.4", _conv_apply(st, "bridge.3", b, 2, 2), training)))
-    e3a = tap("e3a", attention_gate(st, "att3", e3, b))
-    d3 = tap("d3", conv_block(st, "dec3", torch.cat([b, e3a], 1), training))
-    e2a = tap("e2a", attention_gate(st, "att2", e2, tap("u3g", up2(d3))))
-    d2 = tap("d2", conv_block(st, "dec2", torch.cat([tap("u3c", up2(d3)), e2a], 1), training))
-    e1a = tap("e1a", attention_gate(st, "att1", e1, tap("u2g", up2(d2))))
-    d1 = tap("d1", conv_block(st, "dec1", torch.cat([tap("u2c", up2(d2)), e1a], 1), training))
-    y = tap("o1", F.relu(_bn_apply(st, "out_bn1", _conv_apply(st, "out_conv1", d1, 1), training)))
-    y = tap("o2", F.relu(_bn_apply(st, "out_bn2", _conv_apply(st, "out_conv2", y, 1), training)))
+    D = decisions
+    e1 = tap("e1", conv_block(st, "enc1", x, training, D))
+    e2 = tap("e2", conv_block(st, "enc2", _maxpool(e1, D, "pool1"), training, D))
+    e3 = tap("e3", conv_block(st, "enc3", _maxpool(e2, D, "pool2"), training, D))
+    b = tap("b1", _relu(_bn_apply(st, "bridge.1", _conv_apply(st, "bridge.0", e3, 2, 2), training), D, "bridge.1"))
+    b = tap("b", _relu(_bn_apply(st, "bridge.4", _conv_apply(st, "bridge.3", b, 2, 2), training), D, "bridge.4"))
+    e3a = tap("e3a", attention_gate(st, "att3", e3, b, D))
+    d3 = tap("d3", conv_block(st, "dec3", torch.cat([b, e3a], 1), training, D))
+    e2a = tap("e2a", attention_gate(st, "att2", e2, tap("u3g", up2(d3)), D))
+    d2 = tap("d2", conv_block(st, "dec2", torch.cat([tap("u3c", up2(d3)), e2a], 1), training, D))
+    e1a = tap("e1a", attention_gate(st, "att1", e1, tap("u2g", up2(d2)), D))
+    d1 = tap("d1", conv_block(st, "dec1", torch.cat([tap("u2c", up2(d2)), e1a], 1), training, D))
+    y = tap("o1", _relu(_bn_apply(st, "out_bn1", _conv_apply(st, "out_conv1", d1, 1), training), D, "out_bn1"))
+    y = tap("o2", _relu(_bn_apply(st, "out_bn2", _conv_apply(st, "out_conv2", y, 1), training), D, "out_bn2"))
     y = _conv_apply(st, "final", y)
     return y + coarse
 
@@ -168,13 +198,13 @@ def clone_state(st, dtype=None):
     return out
 
 
-def forward_with_grads(st, x, target, training=True):
+def forward_with_grads(st, x, target, training=True, decisions=None):
     """One MSE forward/backward (train_enhanced.py:69-72).  Returns (out, loss, grads, st')."""
     st = clone_state(st)
     names = [n for n in trainable_names() if n in st]
     for n in names:
         st[n].requires_grad_(True)
-    out = unet_forward(st, x, training)
+    out = unet_forward(st, x, training, decisions=decisions)
     loss = F.mse_loss(out, target)                           # nn.MSELoss(), train_enhanced.py:307
     grads = torch.autograd.grad(loss, [st[n] for n in names])
     return out.detach(), loss.detach(), OrderedDict(zip(names, [g.detach() for g in grads])), st

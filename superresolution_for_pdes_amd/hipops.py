@@ -398,6 +398,17 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
 
 
+def resize_bicubic(x, ho, wo):
+    """F.interpolate(mode='bicubic', align_corners=True) of single-channel fields: x [planes, h, w]
+    contiguous fp32 -> [planes, ho, wo] (srpde_resize_bicubic_ac)."""
+    if not (x.is_cuda and x.dtype == F32 and x.is_contiguous() and x.dim() == 3):
+        raise RuntimeError("resize_bicubic: contiguous fp32 [planes, h, w] ROCm tensor (no CPU fallback)")
+    pl, h, w = x.shape
+    out = torch.empty(pl, ho, wo, dtype=F32, device=x.device)
+    call("srpde_resize_bicubic_ac", x.data_ptr(), out.data_ptr(), pl, h, w, ho, wo, stream_ptr())
+    return out
+
+
 def pde_dataset_assemble(u_coarse, u_fine, theta_fine, f_fine, stats, theta_constant):
     """srpde_pde_dataset_assemble: -> (inputs [N, 3, hf, wf], targets [N, 1, hf, wf])."""
     n, hc, wc = u_coarse.shape

@@ -1,0 +1,66 @@
+"""Branch-matched comparison helpers (test infrastructure).
+
+The U-Net is piecewise smooth: ReLU masks and max-pool argmaxes are discrete decisions taken on
+rounded values.  Where a ReLU input lies within rounding error of 0, fp32 and fp64 take different
+branches, and one flipped element moves an activation gradient by ~1/sqrt(numel) in relative L2
+(tools/diag_bnbwd.py shows a single flip out of 204,800 giving 3.6e-3).  That -- not arithmetic
+error -- is what bounds any fp32 implementation's agreement with fp64 (the reference's own fp32
+path included).  To measure the HIP path's ARITHMETIC error, these helpers read the decisions its
+forward took (from the executor's saved tensors, with the kernels' own rounding: x_hat =
+fp32((y - mean) * invstd), mask = sign of the fused multiply-add x_hat * gamma + beta) and hand
+them to the fp64 oracle (oracle.unet_ref.unet_forward(decisions=...)), which then evaluates the
+same branch exactly.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from superresolution_for_pdes_amd import unet_exec as X
+
+_BLOCKS = ["enc1", "enc2", "enc3", "dec3", "dec2", "dec1"]
+
+
+def hip_step(model, x, t, want_dx=True):
+    """One forward (save=True) + MSE backward through the executor, weight gradients on the side
+    stream as in training.  Returns (out, {param name: grad}, dx or None, S)."""
+    out, S = X.unet_forward(model, x, model.training, save=True)
+    dout = (2.0 / out.numel()) * (out - t)
+    layout = model._flat_layout()
+    flat = torch.empty(layout[-1][2] + layout[-1][3], device=x.device)
+    views = {p: flat[o:o + n].view_as(p) for _, p, o, n in layout}
+    wq = X.WgradStream(x.device)
+    dx = X.unet_backward(model, S, dout.reshape(-1), views, wq=wq, want_dx=want_dx)
+    torch.cuda.synchronize()
+    names = {p: n for n, p in model.named_parameters()}
+    return out, {names[p]: g for p, g in views.items()}, dx, S
+
+
+def _relu_mask(saved, bn, n, h, w):
+    y, mean, invstd = saved[2], saved[3], saved[4]
+    xh = (y - mean) * invstd                                     # fp32, the kernels' two roundings
+    z = xh.double() * bn.weight.detach().double() + bn.bias.detach().double()   # exact sign of the fma
+    return (z > 0).view(n, h, w, y.shape[1]).permute(0, 3, 1, 2).cpu()
+
+
+def hip_decisions(model, S):
+    n, h, w = S.shape
+    dims = {"enc1": (h, w), "enc2": (h // 2, w // 2), "enc3": (h // 4, w // 4), "dec3": (h // 4, w // 4),
+            "dec2": (h // 2, w // 2), "dec1": (h, w)}
+    dec = {}
+    for blk in _BLOCKS:
+        s1, s2 = getattr(S, blk)
+        mod = getattr(model, blk)
+        dec[f"{blk}.bn1"] = _relu_mask(s1, mod.bn1, n, *dims[blk])
+        dec[f"{blk}.bn2"] = _relu_mask(s2, mod.bn2, n, *dims[blk])
+    dec["bridge.1"] = _relu_mask(S.br1, model.bridge[1], n, h // 4, w // 4)
+    dec["bridge.4"] = _relu_mask(S.br2, model.bridge[4], n, h // 4, w // 4)
+    dec["out_bn1"] = _relu_mask(S.out1, model.out_bn1, n, h, w)
+    dec["out_bn2"] = _relu_mask(S.out2, model.out_bn2, n, h, w)
+    for key, t, hh, ww in (("pool1", S.e1, h, w), ("pool2", S.e2, h // 2, w // 2)):
+        nchw = t.view(n, hh, ww, t.shape[1]).permute(0, 3, 1, 2).contiguous()
+        dec[key] = F.max_pool2d(nchw, 2, return_indices=True)[1].cpu()   # first-max ties, as the kernel
+    for att in ("att3", "att2", "att1"):
+        hb = getattr(S, att)[1]
+        dec[f"{att}.channel_attention.2"] = (hb > 0).view(n, hb.shape[1], 1, 1).cpu()
+    return dec

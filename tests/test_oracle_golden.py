@@ -83,3 +83,16 @@ def test_cascade_fixture_self_consistent(golden):
     for r in (40, 80, 160):
         assert np.array_equal(d["theta"][r], z[f"theta{r}"])
         assert np.max(np.abs(d["u"][r] - z[f"u{r}"])) < 1e-15
+
+
+def test_interpolation_fixture_is_torch_interpolate(golden):
+    """The cascade640 fixture's bilinear / bicubic baselines are aten's F.interpolate
+    (align_corners=True) of the fp32 40^2 ground truth -- the semantics the HIP resize kernels
+    restate (resolution_comparison_enhanced.py:19-65)."""
+    import torch.nn.functional as F
+    z = golden["cascade640"]
+    u = torch.from_numpy(z["u40"]).float()[None, None]
+    for mode, k in (("bilinear", "bld"), ("bicubic", "cbd")):
+        for tgt, (sr, sc) in ((80, (1, 1)), (160, (1, 1)), (640, (3, 5))):
+            v = F.interpolate(u, size=(tgt, tgt), mode=mode, align_corners=True)[0, 0].numpy()
+            assert np.array_equal(v[::sr, ::sc], z[f"{k}{tgt}"])
