@@ -19,6 +19,50 @@ import torch
 from . import poisson as P
 
 
+def resolve_shard(shard):
+    """(rank, world): the given pair, else the torch.distributed world, else (0, 1)."""
+    if shard is not None:
+        return shard
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous, balanced slice [lo, hi) of n samples for ``rank``."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def gather_fields(local: dict, n: int, world: int, host_keys=(), host_values=None) -> dict:
+    """All-gather every per-sample device field of a sharded dataset (rank slices from
+    shard_range) into the full [n, ...] tensors on every rank; ``host_keys`` are replaced by the
+    full host arrays every rank already holds (``host_values``)."""
+    out = dict(local)
+    for key in host_keys:
+        out[key] = host_values[key]
+    if world == 1:
+        return out
+    import torch.distributed as dist
+    counts = [shard_range(n, r, world) for r in range(world)]
+    cmax = max(hi - lo for lo, hi in counts)
+    for key, v in local.items():
+        if key in host_keys or not isinstance(v, torch.Tensor):
+            continue
+        pad = v.new_zeros((cmax,) + tuple(v.shape[1:]))
+        pad[:v.shape[0]] = v
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad.contiguous())
+        out[key] = torch.cat([parts[r][:hi - lo] for r, (lo, hi) in enumerate(counts)])
+    return out
+
+
+def to_numpy(d: dict) -> dict:
+    return {k: (v.contiguous().cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in d.items()}
+
+
 class PoissonSolver:
     def __init__(self, n_coarse: int = 20, n_fine: int = 40, device: str = "cuda"):
         self.n_coarse = n_coarse
@@ -70,14 +114,25 @@ class PoissonSolver:
         """Batched on-device solve: f, theta [B, n, n] (numpy or tensors) -> u [B, n, n] float64 tensor."""
         return P.solve_batched(f, theta, device=self.device)
 
-    def generate_dataset(self, n_samples: int, k_range: Tuple[float, float] = (1, 5)) -> dict:
-        """data_generation.py:106-159; theta = 1, independent solves on the coarse and fine grids."""
+    def generate_dataset(self, n_samples: int, k_range: Tuple[float, float] = (1, 5), keep_on_device: bool = False,
+                         shard=None) -> dict:
+        """data_generation.py:106-159; theta = 1, independent solves on the coarse and fine grids.
+
+        ``keep_on_device``: the fields stay float64 device tensors (to feed ``PDEDataset``
+        without a host round trip); default numpy, as the reference returns.
+        ``shard=(rank, world)`` (default: the torch.distributed world): every rank draws the whole
+        k sequence from the global np.random (so the RNG stream, and the dataset, equal the
+        single-process run), solves only its contiguous slice of the samples, and one all-gather
+        per field assembles the full set on every rank (SURVEY 8(e) data-gen row)."""
         k = np.empty((n_samples, 2))
         for s in range(n_samples):          # same draw order as the reference loop
             k[s, 0] = np.random.uniform(*k_range)
             k[s, 1] = np.random.uniform(*k_range)
-        out = self._dataset_from_k(k)
-        return {kk: v.cpu().numpy() if isinstance(v, torch.Tensor) else v for kk, v in out.items()}
+        rank, world = resolve_shard(shard)
+        lo, hi = shard_range(n_samples, rank, world)
+        out = self._dataset_from_k(k[lo:hi])
+        out = gather_fields(out, n_samples, world, ("k1", "k2"), {"k1": k[:, 0].copy(), "k2": k[:, 1].copy()})
+        return out if keep_on_device else to_numpy(out)
 
     def _dataset_from_k(self, k: np.ndarray) -> dict:
         nf, nc = self.n_fine, self.n_coarse

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import poisson as P
-from .data_generation import PoissonSolver
+from .data_generation import PoissonSolver, gather_fields, resolve_shard, shard_range, to_numpy
 
 
 class EnhancedPoissonSolver(PoissonSolver):
@@ -43,17 +43,22 @@ class EnhancedPoissonSolver(PoissonSolver):
     def downsample(self, field, factor: int = 2):
         return field[::factor, ::factor]
 
-    def generate_subdomain_dataset(self, n_samples: int, k_range: Tuple[float, float] = (0.5, 12.0)) -> dict:
-        """enhanced_data_generation.py:98-165 with one batched 80^2 solve."""
-        ns, nf, nsf = n_samples, self.n_fine, self.n_superfine
-        k = np.empty((ns, 2))
-        starts = np.empty((ns, 2), dtype=np.int64)
+    def generate_subdomain_dataset(self, n_samples: int, k_range: Tuple[float, float] = (0.5, 12.0),
+                                   keep_on_device: bool = False, shard=None) -> dict:
+        """enhanced_data_generation.py:98-165 with one batched 80^2 solve.  ``keep_on_device`` /
+        ``shard``: as PoissonSolver.generate_dataset (draws stay global, solves are sharded)."""
+        n_all, nf, nsf = n_samples, self.n_fine, self.n_superfine
+        k_all = np.empty((n_all, 2))
+        starts_all = np.empty((n_all, 2), dtype=np.int64)
         max_start = nsf - nf
-        for s in range(ns):  # reference draw order: k1, k2, start_x, start_y
-            k[s, 0] = np.random.uniform(*k_range)
-            k[s, 1] = np.random.uniform(*k_range)
-            starts[s, 0] = np.random.randint(0, max_start)
-            starts[s, 1] = np.random.randint(0, max_start)
+        for s in range(n_all):  # reference draw order: k1, k2, start_x, start_y
+            k_all[s, 0] = np.random.uniform(*k_range)
+            k_all[s, 1] = np.random.uniform(*k_range)
+            starts_all[s, 0] = np.random.randint(0, max_start)
+            starts_all[s, 1] = np.random.randint(0, max_start)
+        rank, world = resolve_shard(shard)
+        lo, hi = shard_range(n_all, rank, world)
+        k, starts, ns = k_all[lo:hi], starts_all[lo:hi], hi - lo
         f_sf = P.forcing_batched(k, nsf, self.device)
         th_sf = torch.ones(ns, nsf, nsf, dtype=torch.float64, device=self.device)
         u_sf = P.solve_batched(f_sf, th_sf, device=self.device)
@@ -73,19 +78,28 @@ class EnhancedPoissonSolver(PoissonSolver):
             "f_fine": f_fine,
             "theta_coarse": th_fine[:, ::2, ::2],
             "theta_fine": th_fine,
-            "k1": k[:, 0].copy(),
-            "k2": k[:, 1].copy(),
-            "is_subdomain": np.ones(ns, dtype=bool),
         }
-        return {kk: (v.contiguous().cpu().numpy() if isinstance(v, torch.Tensor) else v) for kk, v in out.items()}
+        out = {kk: v.contiguous() for kk, v in out.items()}
+        host = {"k1": k_all[:, 0].copy(), "k2": k_all[:, 1].copy(), "is_subdomain": np.ones(n_all, dtype=bool)}
+        out = gather_fields(out, n_all, world, tuple(host), host)
+        return out if keep_on_device else to_numpy(out)
 
     def combine_datasets(self, dataset1: Dict, dataset2: Dict) -> Dict:
-        """enhanced_data_generation.py:167-191."""
+        """enhanced_data_generation.py:167-191.  Device tensors are concatenated on the device
+        (torch.cat), host arrays with np.concatenate: the fields of keep_on_device datasets never
+        leave HBM on their way to PDEDataset."""
         if "is_subdomain" not in dataset1:
             dataset1["is_subdomain"] = np.zeros(len(dataset1["u_fine"]), dtype=bool)
         out = {}
         for key in dataset1:
-            out[key] = np.concatenate([dataset1[key], dataset2[key]]) if key in dataset2 else dataset1[key]
+            if key not in dataset2:
+                out[key] = dataset1[key]
+            elif isinstance(dataset1[key], torch.Tensor) or isinstance(dataset2[key], torch.Tensor):
+                a, b = dataset1[key], dataset2[key]
+                dev = a.device if isinstance(a, torch.Tensor) else b.device
+                out[key] = torch.cat([torch.as_tensor(a, device=dev), torch.as_tensor(b, device=dev)])
+            else:
+                out[key] = np.concatenate([dataset1[key], dataset2[key]])
         return out
 
 

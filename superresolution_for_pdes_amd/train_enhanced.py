@@ -12,7 +12,11 @@ checkpoint on improvement; early stopping.  Differences that do not change resul
   DataLoader workers (:286-300) cannot touch device tensors anyway;
 * ``main`` accepts overrides (``--epochs``, ``--batch-size``, ``--data``, ``--generate``
   for on-device data generation, config #3) and runs data-parallel over RCCL when
-  launched with torchrun (one process per GPU, distributed.DataParallel).
+  launched with torchrun (one process per GPU, distributed.DataParallel): the generated
+  dataset's solves are sharded over the ranks and all-gathered, the batch size is per rank
+  (global batch = world x batch), and validation deals the single-process batches to the
+  ranks so the reduced val loss (which drives the scheduler, checkpoints and early stopping)
+  equals the single-process value.
 """
 from __future__ import annotations
 
@@ -64,34 +68,43 @@ class DeviceBatchLoader:
     """Index-gathered batches from a device-resident PDEDataset (DataLoader replacement).
 
     shuffle: a seeded permutation per epoch; with world > 1 each rank takes a disjoint
-    strided shard of it (DistributedSampler semantics)."""
+    strided shard of it (DistributedSampler semantics: ``batch_size`` is per rank, the global
+    batch is world x batch_size, as under torch DDP).  ``shard_batches`` (evaluation): the
+    single-process batches themselves are dealt round-robin to the ranks, unpadded, so the
+    all-reduced (sum of batch losses, batch count) gives exactly the single-process mean."""
 
-    def __init__(self, dataset, batch_size, shuffle=False, seed=0, rank=0, world=1, drop_last=False):
+    def __init__(self, dataset, batch_size, shuffle=False, seed=0, rank=0, world=1, drop_last=False,
+                 shard_batches=False):
         self.ds, self.bs, self.shuffle = dataset, batch_size, shuffle
         self.seed, self.rank, self.world, self.drop_last = seed, rank, world, drop_last
+        self.shard_batches = shard_batches
         self.epoch = 0
 
     def _indices(self):
         from .distributed import shard_indices
         n = len(self.ds)
-        if self.world > 1:
+        if self.world > 1 and not self.shard_batches:
             return shard_indices(n, self.rank, self.world, self.seed, self.epoch, self.shuffle)
         if self.shuffle:
             g = torch.Generator().manual_seed(self.seed + self.epoch)
             return torch.randperm(n, generator=g)
         return torch.arange(n)
 
+    def _batches(self, idx):
+        out = [idx[s:s + self.bs] for s in range(0, len(idx), self.bs)]
+        if self.drop_last and out and len(out[-1]) < self.bs:
+            out = out[:-1]
+        if self.shard_batches and self.world > 1:
+            out = out[self.rank::self.world]
+        return out
+
     def __len__(self):
-        n = len(self._indices())
-        return n // self.bs if self.drop_last else (n + self.bs - 1) // self.bs
+        return len(self._batches(self._indices()))
 
     def __iter__(self):
         idx = self._indices().to(self.ds.inputs.device)
         self.epoch += 1
-        for s in range(0, len(idx), self.bs):
-            b = idx[s:s + self.bs]
-            if self.drop_last and len(b) < self.bs:
-                break
+        for b in self._batches(idx):
             yield self.ds.batch(b)
 
 
@@ -99,12 +112,13 @@ def _is_main():
     return not dist.is_initialized() or dist.get_rank() == 0
 
 
-def _mean_over_ranks(t):
+def _global_mean(total, count, device):
+    """(sum of batch losses, number of batches) summed over ranks -> the mean batch loss, the
+    reference's ``loss_sum / len(loader)`` (train_enhanced.py:79, :92) over all ranks' batches."""
+    t = torch.stack([total.to(torch.float64), torch.tensor(float(count), dtype=torch.float64, device=device)])
     if dist.is_initialized() and dist.get_world_size() > 1:
-        t = t.clone()
         dist.all_reduce(t)
-        t /= dist.get_world_size()
-    return t
+    return float(t[0] / torch.clamp(t[1], min=1.0))
 
 
 def train_model(model: nn.Module, train_loader, val_loader, criterion: nn.Module, optimizer: optim.Optimizer,
@@ -133,7 +147,7 @@ def train_model(model: nn.Module, train_loader, val_loader, criterion: nn.Module
                 optimizer.step()
             acc += loss.detach()
             nb += 1
-        train_loss = float(_mean_over_ranks(acc / max(nb, 1)))
+        train_loss = _global_mean(acc, nb, device)
 
         model.eval()
         vacc = torch.zeros((), dtype=torch.float64, device=device)
@@ -143,7 +157,7 @@ def train_model(model: nn.Module, train_loader, val_loader, criterion: nn.Module
                 inputs, targets = inputs.to(device), targets.to(device)
                 vacc += criterion(model(inputs), targets).detach()
                 vb += 1
-        val_loss = float(_mean_over_ranks(vacc / max(vb, 1)))
+        val_loss = _global_mean(vacc, vb, device)
 
         scheduler.step(val_loss)
         current_lr = optimizer.param_groups[0]["lr"]
@@ -234,13 +248,30 @@ def default_config():
     }
 
 
-def generate_on_device(n_standard=1000, n_subdomain=1000):
-    """Config #3: the enhanced_data_generation.py __main__ dataset built by the HIP solver."""
+def generate_on_device(n_standard=1000, n_subdomain=1000, keep_on_device=True, shard=None):
+    """Config #3: the enhanced_data_generation.py __main__ dataset built by the HIP solver.
+    The fields stay device tensors from the batched CG to PDEDataset; under
+    torchrun the solves are sharded over the ranks and all-gathered (8(e)), the draws global."""
     from .enhanced_data_generation import EnhancedPoissonSolver
     s = EnhancedPoissonSolver(20, 40, 80)
-    d1 = s.generate_dataset(n_samples=n_standard, k_range=(0.5, 5.0))
-    d2 = s.generate_subdomain_dataset(n_samples=n_subdomain, k_range=(0.5, 12.0))
+    d1 = s.generate_dataset(n_samples=n_standard, k_range=(0.5, 5.0), keep_on_device=keep_on_device, shard=shard)
+    d2 = s.generate_subdomain_dataset(n_samples=n_subdomain, k_range=(0.5, 12.0), keep_on_device=keep_on_device,
+                                      shard=shard)
     return s.combine_datasets(d1, d2)
+
+
+def _per_sample(v):
+    return (v.ndim if hasattr(v, "ndim") else np.ndim(v)) > 0
+
+
+def select(data: dict, idx) -> dict:
+    """Rows ``idx`` of every per-sample field (device tensors indexed on the device)."""
+    out = {}
+    for k, v in data.items():
+        if not _per_sample(v):
+            continue
+        out[k] = v[torch.as_tensor(idx, device=v.device)] if isinstance(v, torch.Tensor) else v[idx]
+    return out
 
 
 def main(argv=None):
@@ -249,7 +280,8 @@ def main(argv=None):
     ap.add_argument("--generate", type=int, nargs=2, metavar=("N_STD", "N_SUB"), default=None,
                     help="generate the dataset on device instead of loading --data")
     ap.add_argument("--epochs", type=int, default=None)
-    ap.add_argument("--batch-size", type=int, default=None)
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per-rank batch (under torchrun the global batch is world x batch-size, as torch DDP)")
     ap.add_argument("--results", default="results")
     args = ap.parse_args(argv)
 
@@ -282,12 +314,11 @@ def main(argv=None):
     else:
         data = dict(np.load(args.data))
     train_idx, val_idx = stratified_split(data, config["val_split"], config["stratify_by_subdomain"])
-    train_data = {k: v[train_idx] for k, v in data.items() if np.ndim(v) > 0}
-    val_data = {k: v[val_idx] for k, v in data.items() if np.ndim(v) > 0}
-    train_ds = PDEDataset(train_data, device=device)
-    val_ds = PDEDataset(val_data, device=device)
+    train_ds = PDEDataset(select(data, train_idx), device=device)
+    val_ds = PDEDataset(select(data, val_idx), device=device)
     train_loader = DeviceBatchLoader(train_ds, config["batch_size"], shuffle=True, seed=42, rank=rank, world=world)
-    val_loader = DeviceBatchLoader(val_ds, config["batch_size"], shuffle=False, rank=rank, world=world)
+    val_loader = DeviceBatchLoader(val_ds, config["batch_size"], shuffle=False, rank=rank, world=world,
+                                   shard_batches=True)
 
     model = UNet().to(device)
     model.apply(init_weights)

@@ -49,13 +49,14 @@ def test_train_model_short_run(tmp_path):
     from superresolution_for_pdes_amd.models import PDEDataset, UNet, init_weights
     from superresolution_for_pdes_amd.optim import FusedAdamW
     from superresolution_for_pdes_amd.train_enhanced import (DeviceBatchLoader, ScalarWriter, generate_on_device,
-                                                             stratified_split, train_model)
+                                                             select, stratified_split, train_model)
     np.random.seed(42)
     torch.manual_seed(42)
     data = generate_on_device(24, 24)
     tr, va = stratified_split(data)
-    trd = PDEDataset({k: v[tr] for k, v in data.items() if np.ndim(v) > 0}, device="cuda")
-    vad = PDEDataset({k: v[va] for k, v in data.items() if np.ndim(v) > 0}, device="cuda")
+    assert isinstance(data["u_fine"], torch.Tensor) and data["u_fine"].is_cuda   # CG output stays in HBM
+    trd = PDEDataset(select(data, tr), device="cuda")
+    vad = PDEDataset(select(data, va), device="cuda")
     model = UNet().cuda()
     model.apply(init_weights)
     opt = FusedAdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
@@ -77,3 +78,47 @@ def test_train_model_short_run(tmp_path):
         model.eval()
         assert torch.allclose(m2(x), model(x), atol=0, rtol=0)
     assert os.path.exists(tmp_path / "tb" / "scalars.jsonl")
+
+
+def test_generated_dataset_device_equals_host():
+    """keep_on_device=True (the training feed) and the reference's numpy return are the same data."""
+    from superresolution_for_pdes_amd.train_enhanced import generate_on_device
+    np.random.seed(9)
+    dev = generate_on_device(6, 5, keep_on_device=True)
+    np.random.seed(9)
+    host = generate_on_device(6, 5, keep_on_device=False)
+    assert set(dev) == set(host)
+    for k, v in host.items():
+        d = dev[k].cpu().numpy() if isinstance(dev[k], torch.Tensor) else dev[k]
+        assert np.array_equal(d, v), k
+
+
+def test_main_end_to_end(tmp_path, monkeypatch):
+    """train_enhanced.main (reference train_enhanced.py:185-360) on device-generated data: the
+    config.json keys (:192-205), best_model.pth / final_model.pth key sets (:117-125, :341-351),
+    the three scalar tags (:99-101), and a checkpoint that load_model restores."""
+    import json
+    from superresolution_for_pdes_amd.compare_methods import load_model
+    from superresolution_for_pdes_amd.train_enhanced import default_config, main
+    monkeypatch.chdir(tmp_path)
+    hist = main(["--generate", "16", "16", "--epochs", "2", "--results", str(tmp_path / "results")])
+    runs = list((tmp_path / "results").glob("enhanced_run_*"))
+    assert len(runs) == 1
+    run = runs[0]
+    cfg = json.load(open(run / "config.json"))
+    assert set(cfg) == set(default_config()) and cfg["num_epochs"] == 2 and cfg["batch_size"] == 32
+    best = torch.load(run / "best_model.pth", weights_only=True)
+    assert set(best) == {"epoch", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "train_loss",
+                         "val_loss"}
+    final = torch.load(run / "final_model.pth", weights_only=True)
+    assert set(final) == {"epoch", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "train_loss",
+                          "val_loss", "best_val_loss", "best_epoch"}
+    assert final["best_val_loss"] == hist["best_val_loss"] and final["best_epoch"] == hist["best_epoch"]
+    assert final["epoch"] == hist["num_epochs"] - 1 == 1
+    # AdamW state layout of torch.optim.AdamW: an independent step tensor per parameter (ADVICE r1)
+    steps = [s["step"] for s in final["optimizer_state_dict"]["state"].values()]
+    assert len(steps) == 84 and len({id(s) for s in steps}) == 84
+    tags = {json.loads(line)["tag"] for line in open(run / "tensorboard" / "scalars.jsonl")}
+    assert tags == {"Loss/train", "Loss/val", "Learning_rate"}
+    m = load_model(run / "final_model.pth", "cuda")
+    assert len(m.state_dict()) == 132
