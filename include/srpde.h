@@ -259,6 +259,14 @@ int srpde_poisson_lds_max_n(void);
  * (PoissonSolver.generate_forcing_term, src/data_generation.py:60-77) */
 int srpde_forcing_batched(const double* k12, int B, int n, double* out, hipStream_t stream);
 size_t srpde_poisson_workspace_size(int B, int n);
+/* The batched solve in one call (replaces spsolve(diag(theta) @ L, f), data_generation.py:79-104,
+ * for B problems at once): f, theta, u are [B][n][n] fp64 device arrays, iters_out [B] int32
+ * (nullable).  n <= srpde_poisson_lds_max_n(): one stream-ordered launch, no workspace.  Larger n:
+ * grid CG with workspace (srpde_poisson_workspace_size bytes); the call polls convergence every
+ * 128 iterations and therefore synchronises `stream` -- the one entry of this library that blocks
+ * the host.  The split entry points below are the same solve, for callers that poll themselves. */
+int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
+                             int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream);
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream);
 int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,

@@ -17,6 +17,8 @@
 //               A sticky per-problem `done` flag makes extra launches no-ops.
 #include "common.h"
 
+#include <vector>
+
 namespace srpde {
 
 constexpr int CG_MAXT = 1024;
@@ -373,6 +375,37 @@ int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit,
   hipLaunchKernelGGL(gcg_finish_kernel, dim3(nbx, B), dim3(256), 0, stream, g, u, iters, maxit);
   SRPDE_LAUNCH_CHECK("srpde_poisson_cg_grid_finish");
   return 0;
+}
+
+// One entry for any n (SURVEY 8(b)'s srpde_poisson_cg_batched): n <= 128 is one stream-ordered
+// launch (LDS-resident CG); n > 128 runs the grid CG from the host in chunks of kCheckEvery
+// iterations and polls the device done flags after each chunk -- the only call of the library that
+// synchronises `stream` (it must know when to stop issuing iterations).  ws: srpde_poisson_workspace_size.
+int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
+                             int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(f && theta && u && B > 0 && n >= 2 && maxit >= 0, "srpde_poisson_cg_batched: bad args");
+  if (n <= srpde_poisson_lds_max_n())
+    return srpde_poisson_cg_lds(f, theta, u, B, n, rtol, maxit, iters_out, nullptr, stream);
+  constexpr int kCheckEvery = 128;
+  int rc = srpde_poisson_cg_grid_init(f, theta, B, n, workspace, ws_bytes, stream);
+  if (rc != 0) return rc;
+  const int* done_dev = reinterpret_cast<const int*>(static_cast<const char*>(workspace) +
+                                                     srpde_poisson_cg_grid_done_offset(B, n));
+  std::vector<int> done(B);
+  for (int k = 0; k < maxit + 1;) {
+    const int cnt = std::min(kCheckEvery, maxit + 1 - k);
+    rc = srpde_poisson_cg_grid_iterate(B, n, rtol, k, cnt, maxit, workspace, ws_bytes, stream);
+    if (rc != 0) return rc;
+    k += cnt;
+    hipError_t e = hipMemcpyAsync(done.data(), done_dev, sizeof(int) * B, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) {
+      set_error("srpde_poisson_cg_batched: convergence poll failed: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    if (std::all_of(done.begin(), done.end(), [](int d) { return d != 0; })) break;
+  }
+  return srpde_poisson_cg_grid_finish(u, iters_out, B, n, maxit, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

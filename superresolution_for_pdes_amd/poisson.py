@@ -6,7 +6,9 @@ operator (reference src/data_generation.py:35-104, src/enhanced_data_generation.
 reference) as the SPD system (-L) u = -f/theta by matrix-free CG in fp64:
   * n <= 128 : one workgroup per problem, direction vector in LDS (one launch);
   * n  > 128 : grid CG, two launches per iteration; the host polls a device `done` flag
-               every ``check_every`` iterations (the only host sync of the path).
+               every 128 iterations (the only host sync of the path).
+Both go through the single C entry ``srpde_poisson_cg_batched`` (include/srpde.h), which a
+non-Python caller binds the same way.
 """
 from __future__ import annotations
 
@@ -33,7 +35,7 @@ def forcing_batched(k12, n: int, device="cuda"):
 
 
 def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, device="cuda",
-                  return_iters: bool = False, check_every: int = 128):
+                  return_iters: bool = False):
     """u[B, n, n] (float64, on device) with theta*Lap(u) = f per problem."""
     f = _dev_f64(f, device)
     theta = _dev_f64(theta, device)
@@ -48,24 +50,8 @@ def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, devic
         maxit = 20 * n * n
     u = torch.empty_like(f)
     iters = torch.empty(B, dtype=torch.int32, device=device)
-    if n <= int(query("srpde_poisson_lds_max_n")):
-        call("srpde_poisson_cg_lds", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),
-             iters.data_ptr(), 0, stream_ptr())
-    else:
-        ws_bytes = int(query("srpde_poisson_workspace_size", B, n))
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
-        call("srpde_poisson_cg_grid_init", f.data_ptr(), theta.data_ptr(), B, n, ws.data_ptr(), ws_bytes,
-             stream_ptr())
-        done_off = int(query("srpde_poisson_cg_grid_done_offset", B, n))
-        done = ws[done_off:done_off + 4 * B].view(torch.int32)
-        k = 0
-        while k < maxit + 1:
-            cnt = min(check_every, maxit + 1 - k)
-            call("srpde_poisson_cg_grid_iterate", B, n, float(rtol), k, cnt, int(maxit), ws.data_ptr(), ws_bytes,
-                 stream_ptr())
-            k += cnt
-            if bool((done != 0).all()):  # host poll (one small D2H copy per chunk)
-                break
-        call("srpde_poisson_cg_grid_finish", u.data_ptr(), iters.data_ptr(), B, n, int(maxit), ws.data_ptr(),
-             ws_bytes, stream_ptr())
+    ws_bytes = int(query("srpde_poisson_workspace_size", B, n))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
+    call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),
+         iters.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
     return (u, iters) if return_iters else u
