@@ -20,7 +20,9 @@ LAYERS = [("enc1.conv2", 64, 0, 64, 40, 1), ("enc2.conv1", 64, 0, 128, 20, 1), (
           ("dec1.conv2", 64, 0, 64, 40, 1), ("out_conv1", 64, 0, 32, 40, 1), ("out_conv2", 32, 0, 16, 40, 1)]
 
 
-def timeit(fn, iters):
+def timeit(fn, iters, seq=None, tag=None):
+    if seq is not None:
+        seq.extend([tag] * (iters + 2))
     for _ in range(2):
         fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -39,7 +41,11 @@ def main():
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
     ap.add_argument("--math", default=None, choices=("h3", "x6", "f32", "x6p"), help="default: the package default (h3)")
+    ap.add_argument("--json-out", default=None, help="per (layer, pass): ms, TF, algorithmic bytes")
+    ap.add_argument("--sequence-out", default=None,
+                    help="launch order of every conv call [(layer, pass)] (maps rocprofv3 dispatches to layers)")
     args = ap.parse_args()
+    seq, rows = [], []
     if args.math:
         H.set_conv_math("x6" if args.math == "x6p" else args.math)
     dev = "cuda"
@@ -72,26 +78,40 @@ def main():
         if h3p:
             H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
             H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
+            seq.extend([(name, "setup"), (name, "setup")])
         for kind in args.only.split(","):
+            tag = (name, kind)
             if kind == "fwd" and args.math == "x6p":   # inputs pre-split outside the timed call
                 p0, p1 = H.split_planes(x0), (H.split_planes(x1) if x1 is not None else None)
                 ms = timeit(lambda: H.conv_fwd_x6p(p0, p1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats),
-                            args.iters)
+                            args.iters, seq, tag)
             elif kind == "dgrad" and args.math == "x6p":
                 pdy = H.split_planes(dy)
                 ms = timeit(lambda: H.conv_fwd_x6p(pdy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
-                            args.iters)
+                            args.iters, seq, tag)
             elif kind == "fwd":
                 ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp),
-                            args.iters)
+                            args.iters, seq, tag)
             elif kind == "dgrad":
                 ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp),
-                            args.iters)
+                            args.iters, seq, tag)
             elif h3p:
-                ms = timeit(lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, hw, hw, 3, dil), args.iters)
+                ms = timeit(lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, hw, hw, 3, dil), args.iters, seq, tag)
             else:
-                ms = timeit(lambda: H.conv_wgrad(dy, x0, x1, dw, n, hw, hw, 3, dil), args.iters)
+                ms = timeit(lambda: H.conv_wgrad(dy, x0, x1, dw, n, hw, hw, 3, dil), args.iters, seq, tag)
             tf = flops / ms / 1e9
+            # algorithmic HBM bytes of one call (fp32 4 B/elem; stored h3 splits 2x2 B/elem):
+            # fwd x + w + y (+ the input split it stores); dgrad dy + w + dx (+ dy's split);
+            # wgrad: both stored splits (else both fp32 operands) + dw
+            wb = 4 * cout * cin * 9
+            if kind == "fwd":
+                ab = 4 * P * cin + wb + 4 * P * cout + (4 * P * cin if h3p else 0)
+            elif kind == "dgrad":
+                ab = 4 * P * cout + wb + 4 * P * cin + (4 * P * cout if h3p else 0)
+            else:
+                ab = 4 * P * (cin + cout) + wb
+            rows.append({"layer": name, "pass": kind, "ms": round(ms, 4), "tflops": round(tf, 1), "flop": flops,
+                         "algorithmic_bytes": ab, "h3p": h3p})
             t = tot.setdefault(kind, [0.0, 0.0])
             t[0] += flops
             t[1] += ms
@@ -99,6 +119,13 @@ def main():
         print(line, flush=True)
     for k, (f, ms) in tot.items():
         print(f"TOTAL {k}: {ms:.2f} ms  {f / ms / 1e9:.1f} TF/s")
+    import json
+    if args.json_out:
+        json.dump({"batch": n, "math": H.conv_math(), "rows": rows,
+                   "totals": {k: {"ms": round(ms, 3), "tflops": round(f / ms / 1e9, 1)} for k, (f, ms) in tot.items()}},
+                  open(args.json_out, "w"), indent=1)
+    if args.sequence_out:
+        json.dump(seq, open(args.sequence_out, "w"))
 
 
 if __name__ == "__main__":
