@@ -15,7 +15,8 @@ import torch  # noqa: F401  -- load torch's HIP runtime first: the .so binds to 
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libsrpde_hip.so")
+# SRPDE_LIB: an alternate build of the same ABI (same-box A/B timing of kernel changes, tools/gpu/conv_ab.sh)
+LIB_PATH = os.environ.get("SRPDE_LIB") or os.path.join(PKG, "lib", "libsrpde_hip.so")
 HEADER = os.path.join(ROOT, "include", "srpde.h")
 
 _CTYPES = {

@@ -19,6 +19,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libsrpde_hip.so")
+# SRPDE_BUILD_OUT: build to another path (an A/B baseline for tools/gpu/conv_ab.sh)
+if os.environ.get("SRPDE_BUILD_OUT"):
+    LIB = os.path.abspath(os.environ["SRPDE_BUILD_OUT"])
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SRPDE_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
@@ -42,7 +45,7 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    objdir = os.path.join(LIBDIR, "obj")
+    objdir = os.path.join(os.path.dirname(LIB), "obj" if LIB.startswith(LIBDIR) else "obj_" + os.path.basename(LIB))
     os.makedirs(objdir, exist_ok=True)
 
     def compile_one(src):

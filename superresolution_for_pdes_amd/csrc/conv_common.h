@@ -233,35 +233,19 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
 // partial statistics per SRB rows.  `stage` (nullable): 2 KiB of LDS per wave, past the
 // reduction scratch, through which the output leaves as 16-B row stores (needs ldy % 4 == 0 and
 // a 16-B aligned y): 4 dwordx4 stores per lane and 32x32 block instead of 16 dword stores.
-template <int BM, int BN, int WM, int WN, int SRB>
-__device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32], bool tail,
-                                          int wg, int nfull, int piece, int m0, int n0, int wmi, int wni, int lane,
-                                          float* smem, float* stage = nullptr) {
+// `colscale` (nullable): per accumulator column block j, an exact power-of-two scale still to be
+// applied (h3: the operand scales); it is fused with the bias into one FMA (bit-identical to the
+// separate multiply and add, the multiply being exact).  A tile whose rows all lie inside the
+// tensor (every tile but the last row tile) takes a path without per-row bounds checks.
+template <int BM, int BN, int WM, int WN, int SRB, bool FULL>
+__device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32],
+                                               int m0, int n0, int wmi, int wni, int lane, float* smem,
+                                               float* stage, const float (&bcol)[BN / WN / 32]) {
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int NSB = BM / SRB, WPS = WM / NSB;
   const int lr = lane & 31, lh = lane >> 5;
   const int wm0 = wmi * TM, wn0 = wni * TN;
-  if (tail) {
-    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r];
-        }
-    return;
-  }
-
-  // ---------------- epilogue: bias, store, BN partial statistics per SRB rows --------
-  float bcol[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn0 + j * 32 + lr;
-    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
-  }
+  auto row_ok = [&](int row) { return FULL || row < p.P; };
   // fused BN-backward reduction: issue every load of the BN input up front (clamped addresses,
   // masked in the sums) so they overlap each other and the stores instead of serialising
   float byv[TI][TJ][16];
@@ -273,17 +257,12 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
         const int col = min(n0 + wn0 + j * 32 + lr, p.Cout - 1);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = min(m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, p.P - 1);
+          const int row0 = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int row = FULL ? row0 : min(row0, p.P - 1);
           byv[i][j][r] = __builtin_nontemporal_load(p.bn_y + (size_t)row * p.bn_ldy + col);
         }
       }
   }
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] += bcol[j];
   if (stage != nullptr) {
     // each 16-row half of a wave's 32x32 block goes through the wave's LDS stage as [16][32]
     // floats and comes back as one float4 of a row per lane (8 lanes per 128-B row)
@@ -294,6 +273,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int col = n0 + wn0 + j * 32 + c4;
+        const bool cok = col < p.Cout;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
@@ -305,7 +285,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
           for (int k = 0; k < 2; ++k) {
             const float4 v = *reinterpret_cast<const float4*>(st + (8 * k + rr) * 32 + c4);
             const int row = m0 + wm0 + i * 32 + 16 * hf + 8 * k + rr;
-            if (row < p.P && col < p.Cout) {
+            if (row_ok(row) && cok) {
               float4* dst = reinterpret_cast<float4*>(p.y + (size_t)row * p.ldy + col);
               if (p.accumulate) {
                 const float4 o = *dst;
@@ -327,7 +307,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < p.P && col < p.Cout) {
+          if (row_ok(row) && col < p.Cout) {
             float* dst = p.y + (size_t)row * p.ldy + col;
             *dst = p.accumulate ? *dst + acc[i][j][r] : acc[i][j][r];
           }
@@ -350,7 +330,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (row < p.P && cok) {
+          if (row_ok(row) && cok) {
             const float xh = (byv[i][j][r] - mu) * is;
             const float dz = xh * ga + be > 0.f ? acc[i][j][r] : 0.f;
             s1 += dz;
@@ -384,7 +364,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
   float* red = smem;                  // [WM][BN] per-wave-row column partials
   const int sb = wmi / WPS;           // this wave's statistics sub-block
   const int rb0 = m0 + sb * SRB;
-  const int cnt = min(SRB, p.P - rb0);
+  const int cnt = FULL ? SRB : min(SRB, p.P - rb0);
   float mean[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
@@ -394,7 +374,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        s += (row < p.P) ? acc[i][j][r] : 0.f;
+        s += row_ok(row) ? acc[i][j][r] : 0.f;
       }
     s += __shfl_xor(s, 32, 64);
     if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
@@ -417,7 +397,7 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const float d = acc[i][j][r] - mean[j];
-        s += (row < p.P) ? d * d : 0.f;
+        s = row_ok(row) ? __builtin_fmaf(d, d, s) : s;   // the same FMA on both paths (bit-equal tiles)
       }
     s += __shfl_xor(s, 32, 64);
     if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
@@ -433,6 +413,50 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
       if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
     }
   }
+}
+
+template <int BM, int BN, int WM, int WN, int SRB>
+__device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[BM / WM / 32][BN / WN / 32], bool tail,
+                                          int wg, int nfull, int piece, int m0, int n0, int wmi, int wni, int lane,
+                                          float* smem, float* stage = nullptr, const float* colscale = nullptr) {
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wm0 = wmi * TM, wn0 = wni * TN;
+  if (tail) {
+    float* dst = p.part + ((size_t)(wg - nfull) * p.tsplit + piece) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const float cs = colscale ? colscale[j] : 1.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          dst[rl * BN + wn0 + j * 32 + lr] = acc[i][j][r] * cs;
+        }
+      }
+    return;
+  }
+
+  // ---------------- epilogue: bias (fused with the operand scale), store, BN statistics --------
+  float bcol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const float cs = colscale ? colscale[j] : 1.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_fmaf(acc[i][j][r], cs, bcol[j]);
+    }
+  if (m0 + BM <= p.P)
+    x6_finish_body<BM, BN, WM, WN, SRB, true>(p, acc, m0, n0, wmi, wni, lane, smem, stage, bcol);
+  else
+    x6_finish_body<BM, BN, WM, WN, SRB, false>(p, acc, m0, n0, wmi, wni, lane, smem, stage, bcol);
 }
 
 // ------------------------------ weight gradient --------------------------------

@@ -358,29 +358,39 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
       __syncthreads();
     }
   }
-  // undo the scales: acc * 2^-ea * 2^-wexp[col] (exact)
+  // the scales to undo: acc * 2^-(ea + wexp[col]), exact; applied by the epilogue in the same FMA
+  // as the bias.  A combined exponent outside the normal range (operands of extreme magnitude)
+  // takes the activation scale here first, so no intermediate under- or overflows.
+  float colscale[TJ];
   const float ia = exp2i(-ea);
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int col = n0 + wn0 + j * 32 + lr;
-    const float iw = col < p.Cout ? exp2i(-h.wexp[col]) : 0.f;
+    const int we = col < p.Cout ? h.wexp[col] : 0;
+    const int e = ea + we;
+    if (e > 126 || e < -126) {
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = (acc[i][j][r] * ia) * iw;
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= ia;
+      colscale[j] = exp2i(-we);
+    } else {
+      colscale[j] = exp2i(-e);
+    }
+    if (col >= p.Cout) colscale[j] = 0.f;
   }
   if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] + acc[i][j][15];
+      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] * colscale[j] + acc[i][j][15];
     if (t == 123.f) p.y[tid] = t;
     return;
   }
   // the halo buffer F is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
   x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
-                                 h.wide ? smem + 2 * WM * BN : nullptr);
+                                 h.wide ? smem + 2 * WM * BN : nullptr, colscale);
 }
 
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
