@@ -212,7 +212,9 @@ class WgradStream:
         key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
         side = WgradStream._streams.get(key)
         if side is None:
-            side = WgradStream._streams[key] = torch.cuda.Stream(device=dev)
+            frac = float(os.environ.get("SRPDE_WGRAD_CU_FRACTION", "1"))
+            side = _cu_masked_stream(dev, frac) if frac < 1 else torch.cuda.Stream(device=dev)
+            WgradStream._streams[key] = side
         self.side = side
 
     def submit(self, fn, keep=()):
@@ -225,6 +227,28 @@ class WgradStream:
 
     def join(self):
         self.main.wait_stream(self.side)
+
+
+def _cu_masked_stream(dev, frac):
+    """A HIP stream whose kernels may only use ``frac`` of the CUs (hipExtStreamCreateWithCUMask;
+    every CU index i with i % 8 < round(8 frac) kept), wrapped for torch.  Tuning knob
+    SRPDE_WGRAD_CU_FRACTION: bounds the weight-gradient side stream's CU footprint so the compute
+    stream's kernels always find free CUs."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    keep = max(1, min(8, round(8 * frac)))
+    for i in range(ncu):
+        if i % 8 < keep:
+            mask[i // 32] |= 1 << (i % 32)
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    return torch.cuda.ExternalStream(handle.value, device=dev)
 
 
 # weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
