@@ -97,13 +97,34 @@ int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hi
  * weights: desc = device int64 [nlayers][9] = {w, cout, cin_real, cin_pad, planes_f, exp_f,
  * planes_d, exp_d, first row}; a layer owns cout forward rows then cin_pad dgrad rows */
 int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows, hipStream_t stream);
+/* dgrad (conv^T) with the BatchNorm (+ReLU) backward apply of the layer fused into the operand
+ * transform: dy = gamma*invstd*(dz - m1 - xhat*m2) is formed per halo element from da (the BN
+ * output gradient) and bn_y_in (the BN input), never stored in fp32; m1, m2 and the dy scale bound
+ * from srpde_bn_bwd_prepare.  dysplit_out [2][P][cout_dy] fp16: dy's split for
+ * srpde_conv_wgrad_h3p.  bn_* / bn_part (nullable): the next BN's backward reduction as in
+ * srpde_conv_fwd_h3; dx_max (nullable): per output tile max|dx| (ceil(P/256)*ceil(cin_dx/BN)
+ * slots) for the next srpde_bn_bwd_prepare.  Replaces srpde_bn_relu_bwd + srpde_conv_fwd_h3(sign -1). */
+int srpde_conv_h3_bnb_supported(int cout_dy, int cin_dx, int w, int dil);
+int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, const float* bn_y_in, int bn_ldy_in,
+                            const float* mean, const float* invstd, const float* gamma, const float* beta,
+                            const float* m1, const float* m2, int flags, const void* wsplit, const int* wexp,
+                            float* dx, int lddx, int n, int h, int w, int cout_dy, int cin_dx, int dil,
+                            void* dysplit_out, const float* bn_y, int bn_ldy, const float* bn_mean,
+                            const float* bn_invstd, const float* bn_gamma, const float* bn_beta, void* bn_part,
+                            float* dx_max, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* Output tiles (= out_max slots) of srpde_conv_fwd_h3 for P rows, cin -> cout; 0 if unsupported. */
+long long srpde_conv_h3_tiles(long long P, int cin, int cout, int w, int dil);
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
                       const unsigned* amax1, const void* wsplit, const int* wexp, const float* bias, float* y, int ldy,
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
                       void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                      const float* bn_beta, void* bn_part, void* workspace, size_t ws_bytes, hipStream_t stream);
-/* in_scale / in_shift (nullable, c1 == 0 only): the input is relu(x0 * in_scale[c] + in_shift[c])
+                      const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
+                      hipStream_t stream);
+/* out_max (nullable): every output tile writes max|y| of its elements to out_max[tile]
+ * (ceil(P/rows) x ceil(cout/cols) slots, the h3 tile of the call) -- the scale bound that
+ * srpde_bn_bwd_prepare needs when y is the gradient of a BN output.
+ * in_scale / in_shift (nullable, c1 == 0 only): the input is relu(x0 * in_scale[c] + in_shift[c])
  * -- the producing BatchNorm + ReLU applied on the fly (srpde_bn_affine); padding stays zero.
  * bn_part (nullable; dgrad of a conv whose input was a BN + ReLU output, accumulate == 0): the
  * output is that activation's gradient, and the epilogue also writes the BN backward's
@@ -161,6 +182,17 @@ int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, c
                            const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
                            float* dbias, long long P, int C, int relu, unsigned* amax, const void* part, int nblk,
                            void* workspace, size_t ws_bytes, hipStream_t stream);
+/* The BN backward prepared for a consumer that applies it on the fly (srpde_conv_dgrad_h3_bnb):
+ * dgamma, dbeta, dbias, the float vectors m1 = sum(dz)/P and m2 = sum(dz*xhat)/P, and a rigorous
+ * bound on max|dy| (float bits) for the consumer's operand scale.  part (nullable): the
+ * (sum dz, sum dz*xhat) partials of the dgrad that produced da, with that dgrad's per-tile
+ * max|da| slots (da_max[n_da_max]); null: a reduction pass over y and da here. */
+size_t srpde_bn_bwd_prepare_workspace_size(long long P, int C);
+int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, long long P, int C, int flags, const void* part,
+                         int nblk_part, const float* da_max, int n_da_max, float* m1, float* m2, float* dgamma,
+                         float* dbeta, float* dbias, unsigned* dy_amax, void* workspace, size_t ws_bytes,
+                         hipStream_t stream);
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
                       float* dbias, long long P, int C, int relu, unsigned* amax, void* workspace,

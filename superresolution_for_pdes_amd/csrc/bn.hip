@@ -162,13 +162,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, long long P, int C,
                                                             int rows_per_blk, int relu,
-                                                            float2* __restrict__ part) {
+                                                            float2* __restrict__ part,
+                                                            float* __restrict__ da_max = nullptr) {
   extern __shared__ float4 red4[];  // [2][256]
   int c4, r0, rs;
   thread_rc(C, &c4, &r0, &rs);
   const int active = (C >> 2) * rs;
   const int c = c4 * 4;
   float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  float dmax = 0.f;
   if ((int)threadIdx.x < active) {
     const float4 mu = *reinterpret_cast<const float4*>(mean + c);
     const float4 is = *reinterpret_cast<const float4*>(invstd + c);
@@ -179,6 +181,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     for (long long p = pb + r0; p < pe; p += rs) {
       const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
       const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+      dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
       float xh, dz;
 #define BN_ACC(X)                                              \
   xh = (v.X - mu.X) * is.X;                                    \
@@ -202,6 +205,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     float2* o = part + (size_t)blockIdx.x * C + c;
     o[0] = make_float2(t1.x, t2.x); o[1] = make_float2(t1.y, t2.y);
     o[2] = make_float2(t1.z, t2.z); o[3] = make_float2(t1.w, t2.w);
+  }
+  if (da_max != nullptr) {   // this block's max|da| -> its slot (block-uniform branch)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+    __syncthreads();
+    float* wmx = reinterpret_cast<float*>(red4);
+    if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = dmax;
+    __syncthreads();
+    if (threadIdx.x == 0) da_max[blockIdx.x] = fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]));
   }
 }
 
@@ -293,6 +305,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     o[0] = make_float2(t.x, 0.f); o[1] = make_float2(t.y, 0.f);
     o[2] = make_float2(t.z, 0.f); o[3] = make_float2(t.w, 0.f);
   }
+}
+
+// The BN (+ReLU) backward's per-channel apply coefficients for a consumer that computes dy on the
+// fly (srpde_conv_dgrad_h3_bnb): m1 = sum(dz)/P, m2 = sum(dz*xhat)/P as float, exactly as
+// bn_bwd_apply_kernel forms them (0 in eval mode); the conv-bias gradient sum(dy) in fp64
+// (= gamma*invstd*(sum dz - P*m1 - m2*sum xhat), sum xhat = 0 for train-mode batch statistics:
+// 0 up to rounding, as the reference's autograd value); and a rigorous bound on max|dy| for the
+// consumer's operand scale: |dy_c| <= |gamma_c invstd_c| (max|da| + |m1_c| + max|xhat| |m2_c|),
+// max|xhat| <= sqrt(P-1) (Samuelson) in train mode.  One block.
+__global__ __launch_bounds__(256) void bn_bwd_coef_kernel(const double* __restrict__ sdz, const double* __restrict__ sdzx,
+                                                         long long P, int C, const float* __restrict__ invstd,
+                                                         const float* __restrict__ gamma, int eval,
+                                                         const float* __restrict__ da_max, int n_da_max,
+                                                         float* __restrict__ m1, float* __restrict__ m2,
+                                                         float* __restrict__ dbias, unsigned* dy_amax) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int k = threadIdx.x; k < n_da_max; k += 256) a = fmaxf(a, da_max[k]);
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  const float amax_da = red[0];
+  __syncthreads();
+  const double invP = eval ? 0.0 : 1.0 / (double)P;
+  const float xmax = eval ? 0.f : sqrtf((float)(P > 1 ? P - 1 : 1));
+  float b = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float k = gamma[c] * invstd[c];
+    const float a1 = (float)(sdz[c] * invP), a2 = (float)(sdzx[c] * invP);
+    m1[c] = a1;
+    m2[c] = a2;
+    if (dbias) dbias[c] = (float)((double)k * (sdz[c] - (double)P * (double)a1 * (eval ? 0.0 : 1.0)));
+    b = fmaxf(b, fabsf(k) * (amax_da + fabsf(a1) + xmax * fabsf(a2)));
+  }
+  red[threadIdx.x] = b;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *dy_amax = __float_as_uint(red[0] * 1.0001f);   // covers the float rounding of the sum
 }
 
 static int bwd_blocks(long long P, int C, int* rows_per_blk) {
@@ -429,6 +485,57 @@ int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, c
                        (double*)nullptr, (double*)nullptr);
     SRPDE_LAUNCH_CHECK("srpde_bn_relu_bwd_part(bias)");
   }
+  return 0;
+}
+
+// Everything the fused dgrad (srpde_conv_dgrad_h3_bnb) needs to apply this BN's backward on the
+// fly: dgamma, dbeta, dbias, the float m1 / m2 vectors and the dy operand-scale bound word.  `part`:
+// the (sum dz, sum dz*xhat) partials already produced by the dgrad that wrote da (nblk row blocks,
+// with that dgrad's per-tile max|da| in da_max[n_da_max]); null: one reduction pass over y and da
+// here (which also takes max|da|).  flags: SRPDE_BN_RELU | SRPDE_BN_EVAL.
+size_t srpde_bn_bwd_prepare_workspace_size(long long P, int C) {
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  return (size_t)nblk * C * sizeof(float2) + (size_t)C * sizeof(double) * 2 + (size_t)nblk * sizeof(float) + 64;
+}
+
+int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, long long P, int C, int flags, const void* part,
+                         int nblk_part, const float* da_max, int n_da_max, float* m1, float* m2, float* dgamma,
+                         float* dbeta, float* dbias, unsigned* dy_amax, void* workspace, size_t ws_bytes,
+                         hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && m1 && m2 && dy_amax && workspace && P > 0,
+                  "srpde_bn_bwd_prepare: null argument");
+  SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0, "srpde_bn_bwd_prepare: C / ld");
+  SRPDE_CHECK_ARG(part == nullptr || (da_max && n_da_max > 0 && nblk_part > 0),
+                  "srpde_bn_bwd_prepare: fused partials need the producer's max|da| slots");
+  if (ws_bytes < srpde_bn_bwd_prepare_workspace_size(P, C)) {
+    set_error("srpde_bn_bwd_prepare: workspace too small");
+    return kErrWorkspace;
+  }
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  float2* wpart = static_cast<float2*>(workspace);
+  double* sdz = reinterpret_cast<double*>(wpart + (size_t)nblk * C);
+  double* sdzx = sdz + C;
+  float* wmax = reinterpret_cast<float*>(sdzx + C);
+  const float2* use_part = static_cast<const float2*>(part);
+  int np = nblk_part;
+  if (part == nullptr) {
+    const size_t lds = 2 * 256 * sizeof(float4);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd,
+                       gamma, beta, P, C, rpb, flags & SRPDE_BN_RELU, wpart, wmax);
+    SRPDE_LAUNCH_CHECK("srpde_bn_bwd_prepare(reduce)");
+    use_part = wpart;
+    np = nblk;
+    da_max = wmax;
+    n_da_max = nblk;
+  }
+  hipLaunchKernelGGL(colsum2_kernel, dim3(C), dim3(256), 0, stream, use_part, np, C, dbeta, dgamma, sdz, sdzx);
+  SRPDE_LAUNCH_CHECK("srpde_bn_bwd_prepare(colsum)");
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(1), dim3(256), 0, stream, sdz, sdzx, P, C, invstd, gamma,
+                     (flags & SRPDE_BN_EVAL) ? 1 : 0, da_max, n_da_max, m1, m2, dbias, dy_amax);
+  SRPDE_LAUNCH_CHECK("srpde_bn_bwd_prepare(coef)");
   return 0;
 }
 

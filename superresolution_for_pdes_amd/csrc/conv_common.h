@@ -37,6 +37,10 @@ struct ConvParams {
   const float* bn_gamma = nullptr;
   const float* bn_beta = nullptr;
   float2* bn_part = nullptr;
+  // optional: every output tile writes max|out| of its own elements to out_max[tile] (no atomics;
+  // the consumer reduces the [ntiles] slots) -- the operand-scale bound of the BN backward that
+  // reads this output next (srpde_bn_bwd_prepare)
+  float* out_max = nullptr;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int total) {
@@ -135,6 +139,22 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
     }
   }
   constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
+  if (p.out_max != nullptr) {         // max|out| of this tile -> its slot
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+      if (m0 + g + i * G < p.P && cok)
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+    red[g][cq] = make_float4(mx, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int k = 0; k < G; ++k)
+        for (int c = 0; c < CQ; ++c) t = fmaxf(t, red[k][c].x);
+      p.out_max[wg] = t;
+    }
+    __syncthreads();
+  }
   if (p.bn_part != nullptr) {         // fused BN-backward reduction (as x6_finish)
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 mu = cok ? *reinterpret_cast<const float4*>(p.bn_mean + col) : z4;
@@ -313,6 +333,32 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
           }
         }
       }
+  }
+  if (p.out_max != nullptr) {         // max|out| of this tile -> out_max[tile] (one store per workgroup)
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const bool cok = n0 + wn0 + j * 32 + lr < p.Cout;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row_ok(row) && cok) mx = fmaxf(mx, fabsf(acc[i][j][r]));
+        }
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    __syncthreads();                  // smem may still hold the store stage's last reads
+    if (lane == 0) smem[wni * WM + wmi] = mx;
+    __syncthreads();
+    if (wmi == 0 && wni == 0 && lane == 0) {
+      float t = 0.f;
+      for (int k = 0; k < WM * WN; ++k) t = fmaxf(t, smem[k]);
+      const int nbn = (p.Cout + BN - 1) / BN;
+      p.out_max[(m0 / BM) * nbn + n0 / BN] = t;
+    }
+    __syncthreads();
   }
   if (p.bn_part != nullptr) {         // fused BN-backward reduction of the layer below (see ConvParams)
     float* red = smem;                // [2][WM][BN]

@@ -69,12 +69,20 @@ struct H3Args {
   const float* in_scale;   // optional per-channel affine + ReLU applied to x0 in the split
   const float* in_shift;   // (the producing BatchNorm, fused; c1 == 0)
   int wide;                // 1: the epilogue stores 16-B rows through LDS (ldy % 4 == 0, y 16-B aligned)
+  // BNB kernels (dgrad with the BatchNorm(+ReLU) backward apply fused into the operand transform):
+  // x0 is the gradient da of the BN + ReLU output; the operand is
+  //   dy = gamma*invstd * (dz - m1 - xhat*m2),  xhat = (y - mean)*invstd,  dz = da * [xhat*gamma + beta > 0]
+  // (m1 = m2 = 0 in eval mode), computed per halo element from a second fp32 halo tile of y
+  const float* bnb_y; int bnb_ldy;
+  const float* bnb_mean; const float* bnb_invstd; const float* bnb_gamma; const float* bnb_beta;
+  const float* bnb_m1; const float* bnb_m2;
+  int bnb_relu;
 };
 
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
 // TPS: taps per stage (one barrier per stage; the weight stage holds TPS taps).
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false>
 __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -85,6 +93,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   constexpr int B_STAGE = TPS * B_TAP;
   constexpr int NS = (9 + TPS - 1) / TPS;  // stages per channel chunk
   constexpr int AQ = (8 + NS - 2) / (NS - 1);   // halo-slice DMAs per wave in stages 0..NS-2 (8 per wave per chunk)
+  constexpr int AD = BNB ? 2 : 1;               // DMAs per halo slice (BNB: the gradient and the BN input)
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
   static_assert(TPS >= 1 && TPS <= 3, "taps per stage");
   // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its hi / lo fp16 planes (64-B rows)
@@ -93,7 +102,8 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   char* lds = reinterpret_cast<char*>(smem);
   const int arows = h.arows;
   char* const fbuf = lds;
-  char* const shi = fbuf + arows * ROW2;
+  char* const fbuf2 = fbuf + arows * ROW2;      // BNB: fp32 halo tile of the BN input y
+  char* const shi = fbuf + (BNB ? 2 : 1) * arows * ROW2;
   char* const slo = shi + arows * 64;
   char* const bbuf0 = slo + arows * 64;
   char* const zrow = bbuf0 + 2 * B_STAGE;
@@ -123,6 +133,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const size_t plane = (size_t)p.Cout * p.K;   // fp16 elements per weight plane
   const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
+  const int32x4 rsy = BNB ? make_rsrc(h.bnb_y, (unsigned)((size_t)p.P * h.bnb_ldy * 4)) : rs0;
   const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
 
   // activation scale (shared by both inputs of a virtual concat)
@@ -182,6 +193,11 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     const bool real = q < na;
     const unsigned off = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
     dma16(rs, off, lds_addr_of(real ? fbuf + q * 1024 : sink));
+    if constexpr (BNB) {
+      const unsigned offy = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * h.bnb_ldy + cb + swz(r, lane & 7) * 4) * 4)
+                                                            : OOB;
+      dma16(rsy, offy, lds_addr_of(real ? fbuf2 + q * 1024 : sink));
+    }
   };
   auto issue_b = [&](int ch, int st, int buf) {   // the TPS taps of stage `st` of chunk `ch`
 #pragma unroll
@@ -205,11 +221,39 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   // (the N-tile-0 workgroup of each row tile also stores its own rows' pieces to h.xsplit)
   const bool wsplit = h.xsplit != nullptr && nt == 0;
   const size_t xplane = (size_t)p.P * p.Cin;
+  struct BnbCoef { float mu[8], is[8], ga[8], be[8], m1[8], m2[8]; };
   auto convert = [&](int ch) {
+    BnbCoef bq;
+    if constexpr (BNB) {   // this thread's 8 channels (sg & 3 == tid & 3 for every task of the loop below)
+      const int cc = ch * BK2 + (tid & 3) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bq.mu[k] = h.bnb_mean[cc + k]; bq.is[k] = h.bnb_invstd[cc + k];
+        bq.ga[k] = h.bnb_gamma[cc + k]; bq.be[k] = h.bnb_beta[cc + k];
+        bq.m1[k] = h.bnb_m1[cc + k]; bq.m2[k] = h.bnb_m2[cc + k];
+      }
+    }
+    (void)bq;
     for (int sg = tid; sg < arows * 4; sg += NT) {
       const int r = sg >> 2, c8 = sg & 3;
       float4 v0 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8) * 16);
       float4 v1 = *reinterpret_cast<const float4*>(fbuf + r * ROW2 + swz(r, 2 * c8 + 1) * 16);
+      if constexpr (BNB) {   // fused BN (+ReLU) backward: da (F) and y (F2) -> dy; rows outside the tensor stay 0
+        const bool inside = pix0 + r >= 0 && pix0 + r < p.P;
+        const float4 y0 = *reinterpret_cast<const float4*>(fbuf2 + r * ROW2 + swz(r, 2 * c8) * 16);
+        const float4 y1 = *reinterpret_cast<const float4*>(fbuf2 + r * ROW2 + swz(r, 2 * c8 + 1) * 16);
+        float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const float yy8[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          // the same expressions as bn_bwd_apply_kernel (bn.hip)
+          const float xh = (yy8[k] - bq.mu[k]) * bq.is[k];
+          const float dz = (!h.bnb_relu || xh * bq.ga[k] + bq.be[k] > 0.f) ? vv[k] : 0.f;
+          vv[k] = inside ? (dz - bq.m1[k] - xh * bq.m2[k]) * (bq.ga[k] * bq.is[k]) : 0.f;
+        }
+        v0 = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        v1 = make_float4(vv[4], vv[5], vv[6], vv[7]);
+      }
       if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
         const int cc = ch * BK2 + c8 * 8, pix = pix0 + r;
         const bool inside = pix >= 0 && pix < p.P;
@@ -331,7 +375,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     // the next stage's weights must have landed; the halo slices issued after them may still be
     // in flight (they are waited for by the next stage's count, long before the chunk ends)
     if (ST < NS - 1 && more && h.relax)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ * AD) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!(p.dbg & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
@@ -976,8 +1020,8 @@ static int h3_half_max() {
   return v;
 }
 
-static size_t h3_lds(int bn, int arows, int tps = 1) {
-  return (size_t)arows * (ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
+static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false) {
+  return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
 }
 // taps per stage: the most (<= SRPDE_H3_TPS, default 2) whose weight double-buffer fits in LDS
 static int h3_tps(int bn, int arows) {
@@ -990,12 +1034,12 @@ static int h3_tps(int bn, int arows) {
   return t;
 }
 
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false>
 static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int NT = WM * WN * 64;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
   const int T = nbm * nbn;
-  const size_t lds = h3_lds(BN, h.arows, TPS);
+  const size_t lds = h3_lds(BN, h.arows, TPS, BNB);
   if ((size_t)h.arows * ROW2 < (size_t)(2 * WM * BN + WM * WN * 512) * 4) h.wide = 0;   // F too small to stage
   static int slots = [&] {
     int dev = 0, cus = 0;
@@ -1010,7 +1054,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS>), dim3(grid), dim3(NT), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, BNB>), dim3(grid), dim3(NT), lds, st, p,
+                     h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -1170,7 +1215,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
                       void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                      const float* bn_beta, void* bn_part, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                      const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
+                      hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
@@ -1193,7 +1239,7 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   const long long maxld = std::max(ldx0, c1 ? ldx1 : 0);
   SRPDE_CHECK_ARG((long long)p.P * maxld * 4 < (1LL << 31) && 2LL * cout * p.K * 2 < (1LL << 31),
                   "srpde_conv_fwd_h3: tensor too large");
-  H3Args a;
+  H3Args a{};
   a.wsp = static_cast<const _Float16*>(wsplit);
   a.wexp = wexp;
   a.amax0 = amax0;
@@ -1220,6 +1266,7 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "srpde_conv_fwd_h3: the fused BN reduction needs bn_y/mean/invstd/gamma/beta and no accumulate");
   p.bn_y = bn_y; p.bn_ldy = bn_ldy; p.bn_mean = bn_mean; p.bn_invstd = bn_invstd;
   p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
+  p.out_max = out_max;
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
   if (p.Cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) {   // shallow K: 128-row tiles, 2 per CU
     a.arows = h3_arows(w, dil, 128);
@@ -1240,6 +1287,80 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
     default: return H3_LAUNCH(32);
   }
 #undef H3_LAUNCH
+}
+
+// dgrad with the BatchNorm (+ReLU) backward apply fused into the operand transform (BNB kernels):
+// dx = conv^T(dy) with dy = gamma*invstd*(dz - m1 - xhat*m2) computed per halo element from the
+// BN output gradient da and the BN input y (no dy tensor in HBM).  m1 / m2 / the dy operand-scale
+// bound come from srpde_bn_bwd_prepare.  Stores dy's split (dysplit_out) for srpde_conv_wgrad_h3p,
+// optionally the next BN-backward reduction (bn_* / bn_part) and per-tile max|dx| (dx_max).
+int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, const float* bn_y_in, int bn_ldy_in,
+                            const float* mean, const float* invstd, const float* gamma, const float* beta,
+                            const float* m1, const float* m2, int flags, const void* wsplit, const int* wexp,
+                            float* dx, int lddx, int n, int h, int w, int cout_dy, int cin_dx, int dil,
+                            void* dysplit_out, const float* bn_y, int bn_ldy, const float* bn_mean,
+                            const float* bn_invstd, const float* bn_gamma, const float* bn_beta, void* bn_part,
+                            float* dx_max, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(da && dy_amax && bn_y_in && mean && invstd && gamma && beta && m1 && m2 && wsplit && wexp && dx &&
+                  dysplit_out, "srpde_conv_dgrad_h3_bnb: null pointer");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout_dy > 0 && cin_dx > 0, "srpde_conv_dgrad_h3_bnb: bad shape");
+  SRPDE_CHECK_ARG(srpde_conv_h3_supported(cout_dy, 0, cin_dx, w, dil, 3),
+                  "srpde_conv_dgrad_h3_bnb: unsupported shape (cout_dy=%d cin_dx=%d w=%d dil=%d)", cout_dy, cin_dx, w,
+                  dil);
+  SRPDE_CHECK_ARG(ldda % 4 == 0 && bn_ldy_in % 4 == 0 && aligned16(da) && aligned16(bn_y_in) && aligned16(wsplit) &&
+                  aligned16(dysplit_out), "srpde_conv_dgrad_h3_bnb: 16-byte alignment / ld % 4");
+  ConvParams p;
+  p.x0 = da; p.c0 = cout_dy; p.ldx0 = ldda;
+  p.x1 = nullptr; p.c1 = 0; p.ldx1 = 4;
+  p.x0p = nullptr; p.x1p = nullptr;
+  p.w = nullptr; p.bias = nullptr; p.y = dx; p.ldy = lddx;
+  p.stats = nullptr;
+  p.N = n; p.H = h; p.W = w; p.Cout = cin_dx; p.ksize = 3; p.dil = dil; p.sign = -1; p.accumulate = 0;
+  p.P = n * h * w; p.Cin = cout_dy; p.K = 9 * p.Cin;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  SRPDE_CHECK_ARG((long long)p.P * std::max(ldda, bn_ldy_in) * 4 < (1LL << 31) && 2LL * cin_dx * p.K * 2 < (1LL << 31),
+                  "srpde_conv_dgrad_h3_bnb: tensor too large");
+  SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && bn_ldy % 4 == 0 &&
+                                          cin_dx % 4 == 0), "srpde_conv_dgrad_h3_bnb: bad fused-reduction arguments");
+  p.bn_y = bn_y; p.bn_ldy = bn_ldy; p.bn_mean = bn_mean; p.bn_invstd = bn_invstd;
+  p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
+  p.out_max = dx_max;
+  H3Args a{};
+  a.wsp = static_cast<const _Float16*>(wsplit);
+  a.wexp = wexp;
+  a.amax0 = dy_amax;
+  a.amax1 = nullptr;
+  a.halo = (w + 1) * dil;
+  a.arows = h3_arows(w, dil);
+  a.relax = 1;
+  a.xsplit = static_cast<_Float16*>(dysplit_out);
+  a.in_scale = nullptr; a.in_shift = nullptr;
+  a.wide = lddx % 4 == 0 && aligned16(dx);
+  a.bnb_y = bn_y_in; a.bnb_ldy = bn_ldy_in;
+  a.bnb_mean = mean; a.bnb_invstd = invstd; a.bnb_gamma = gamma; a.bnb_beta = beta;
+  a.bnb_m1 = m1; a.bnb_m2 = m2;
+  a.bnb_relu = flags & 1;
+  const int bn = h3_bn(h3_cfg(cin_dx));
+  SRPDE_CHECK_ARG(h3_lds(bn, a.arows, 1, true) <= 160 * 1024, "srpde_conv_dgrad_h3_bnb: LDS (w=%d dil=%d)", w, dil);
+  SRPDE_CHECK_ARG(h3_cfg(cin_dx) != 1, "srpde_conv_dgrad_h3_bnb: 128-column tiles not provided (cin_dx=%d)", cin_dx);
+  // one tap per stage: the second fp32 halo tile takes the second weight stage's LDS.  (The
+  // 128-column tile does not fit its registers with the fused transform -- 46 VGPRs of scratch --
+  // so outputs with a multiple of 128 channels keep srpde_bn_relu_bwd + srpde_conv_fwd_h3.)
+  if (h3_cfg(cin_dx) == 2) return launch_fwd_h3<256, 64, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
+  return launch_fwd_h3<256, 32, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
+}
+
+// Number of output tiles (= out_max slots) srpde_conv_fwd_h3 uses for this shape; 0 if unsupported.
+long long srpde_conv_h3_tiles(long long P, int cin, int cout, int w, int dil) {
+  if (P <= 0 || !srpde_conv_h3_supported(cin, 0, cout, w, dil, 3)) return 0;
+  const int bm = (cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) ? 128 : 256;
+  const int bn = h3_bn(h3_cfg(cout));
+  return ((P + bm - 1) / bm) * ((cout + bn - 1) / bn);
+}
+
+int srpde_conv_h3_bnb_supported(int cout_dy, int cin_dx, int w, int dil) {
+  if (!srpde_conv_h3_supported(cout_dy, 0, cin_dx, w, dil, 3) || h3_cfg(cin_dx) == 1) return 0;
+  return h3_lds(h3_bn(h3_cfg(cin_dx)), h3_arows(w, dil), 1, true) <= 160 * 1024 ? 1 : 0;
 }
 
 }  // extern "C"

@@ -115,7 +115,7 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
 
 
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
-             planes_out=None, in_affine=None, bn_bwd=None):
+             planes_out=None, in_affine=None, bn_bwd=None, out_max=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
     ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad;
     ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly;
@@ -140,13 +140,13 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
-             *_bn_bwd_args(bn_bwd), ws.data_ptr(), ws.numel(), stream_ptr())
+             *_bn_bwd_args(bn_bwd), _p(out_max), ws.data_ptr(), ws.numel(), stream_ptr())
         if planes_out is not None:
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert planes_out is None and in_affine is None and bn_bwd is None, \
-        "planes_out / in_affine / bn_bwd need the h3 kernels"
+    assert planes_out is None and in_affine is None and bn_bwd is None and out_max is None, \
+        "planes_out / in_affine / bn_bwd / out_max need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
     if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
@@ -166,6 +166,65 @@ def _bn_bwd_args(bn_bwd):
     by, mean, invstd, gamma, beta, part = bn_bwd
     pby, ldby = _pl(by)
     return (pby, ldby, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), part.data_ptr())
+
+
+def bnb_capable(cout_dy, cin_dx, w, dil):
+    """The fused BN-backward dgrad (srpde_conv_dgrad_h3_bnb) covers this layer."""
+    return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_bnb_supported", cout_dy, cin_dx, w, dil))
+
+
+def bn_bwd_prepare(y, da, mean, invstd, gamma, beta, dgamma, dbeta, dbias, relu=True, eval_mode=False, part=None,
+                   da_max=None):
+    """srpde_bn_bwd_prepare -> (m1, m2, dy_amax word): the BN backward's per-channel terms for
+    conv_dgrad_bnb, and its parameter gradients.  ``part`` / ``da_max``: the partials and max|da|
+    slots of the dgrad that produced ``da`` (else a reduction pass over y and da)."""
+    P, C = y.shape
+    py, ldy = _pl(y)
+    pda, ldda = _pl(da)
+    m1, m2 = empty(C, device=y.device), empty(C, device=y.device)
+    word = torch.zeros(1, dtype=torch.int32, device=y.device)
+    ws_bytes = int(query("srpde_bn_bwd_prepare_workspace_size", P, C))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
+    if part is not None and da_max is None:
+        da_max = amax_of(da).view(torch.float32)     # max|da| as a one-slot float array
+    flags = (BN_RELU if relu else 0) | (BN_EVAL if eval_mode else 0)
+    call("srpde_bn_bwd_prepare", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), P, C, flags, _p(part), part.shape[0] if part is not None else 0, _p(da_max),
+         da_max.numel() if (part is not None) else 0, m1.data_ptr(), m2.data_ptr(), _p(dgamma), _p(dbeta), _p(dbias),
+         word.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
+    return m1, m2, word
+
+
+def dx_max_slots(n, h, w, cin_dx, device):
+    """Per-tile max|dx| slots written by conv_dgrad_bnb (256-row tiles x 64/32-column tiles)."""
+    bn = 64 if cin_dx % 64 == 0 else 32
+    return empty(-(-(n * h * w) // 256) * -(-cin_dx // bn), device=device)
+
+
+def out_max_slots(n, h, w, cin, cout, dil, device):
+    """Per-tile max|y| slots written by conv_fwd(out_max=...) (srpde_conv_h3_tiles: its tile choice)."""
+    t = query("srpde_conv_h3_tiles", n * h * w, cin, cout, w, dil)
+    assert t > 0, "out_max_slots: shape not on the h3 kernels"
+    return empty(t, device=device)
+
+
+def conv_dgrad_bnb(da, y, mean, invstd, gamma, beta, m1, m2, dy_amax, wpack, dx, n, h, w, cout_dy, cin_dx, dil,
+                   dysplit, relu=True, bn_bwd=None, dx_max=None):
+    """srpde_conv_dgrad_h3_bnb: dx = conv^T(dy) with the BN (+ReLU) backward applied on the fly
+    (dy = gamma*invstd*(dz - m1 - xhat*m2) from da and y); dy's split goes to ``dysplit``."""
+    planes, wexp = wpack.h3
+    pda, ldda = _pl(da)
+    py, ldy = _pl(y)
+    pdx, lddx = _pl(dx)
+    for buf in (bn_bwd[5] if bn_bwd is not None else None,):
+        if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
+            raise ValueError("statistics buffer not laid out for the h3 kernel (bn_bwd_partials)")
+    ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cin_dx)), dx.device)
+    call("srpde_conv_dgrad_h3_bnb", pda, ldda, dy_amax.data_ptr(), py, ldy, mean.data_ptr(), invstd.data_ptr(),
+         gamma.data_ptr(), beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), BN_RELU if relu else 0, planes.data_ptr(),
+         wexp.data_ptr(), pdx, lddx, n, h, w, cout_dy, cin_dx, dil, dysplit.data_ptr(), *_bn_bwd_args(bn_bwd),
+         _p(dx_max), ws.data_ptr(), ws.numel(), stream_ptr())
+    dysplit._srpde_amax = dy_amax
 
 
 def bn_bwd_partials(n, h, w, c, device):

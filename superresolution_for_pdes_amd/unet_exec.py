@@ -276,32 +276,65 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     """dgrad first: its h3 kernel stores dy's split, which the weight gradient then reads together
     with the input's split stored by the forward (h3p); otherwise the splitting wgrad kernels.
 
-    ``part``: this BN's backward reduction, already produced by the dgrad that wrote ``da``.
+    ``part``: this BN's backward reduction, already produced by the dgrad that wrote ``da`` -- a
+    (partials, max|da| slots or None) pair.
     ``below = (bn, saved)``: the BN + ReLU whose output this layer reads; when the dgrad runs on
     h3 into a fresh ``dx`` it also produces that BN's reduction, returned for the next call.
-    ``wq``: a WgradStream that takes the weight-gradient launch off the compute stream."""
+    ``wq``: a WgradStream that takes the weight-gradient launch off the compute stream.
+
+    Train mode with an h3 dgrad into ``dx`` of at most 64 channels (one output-column tile) from a
+    dy of at least 64 (two 32-channel chunks): the BN (+ReLU) backward is applied inside the
+    dgrad's operand transform (srpde_conv_dgrad_h3_bnb), so dy is never written or read in fp32 --
+    srpde_bn_bwd_prepare forms the per-channel terms first.  Per layer in the step (same box):
+    enc1.conv2 -84 us, dec1.conv2 -44 us, enc2.conv1 ~-120 us; with several output-column tiles
+    (dec1.conv1: +108 us, each tile repeats the transform) or a single input chunk (out_conv1:
+    +45 us) the separate elementwise pass is cheaper, so those keep it."""
     x0, x1, y, mean, invstd, xp, train = saved
     P, cout = y.shape
+    part_t, da_max = part if part is not None else (None, None)
+    cin = conv.in_channels if x0 is None else x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    dyp = None
+    out_part = None
+    if (_FUSE_BN_APPLY and train and dx is not None and xp is not None and not dx_accumulate
+            and cin <= 64 and cout >= 64 and H.bnb_capable(cout, cin, w, dil)):
+        m1, m2, dyw = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
+                                       grads[conv.bias], part=part_t, da_max=da_max)
+        wd = _dgrad_weights(conv, cin, w, dil)
+        dyp = H.split_planes_buffer(P, cout, y.device)
+        bn_bwd, dx_max = None, None
+        if below is not None and _FUSE_BN_BWD:
+            bnb, sb = below
+            out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
+            bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
+            dx_max = H.dx_max_slots(n, h, w, cin, y.device)
+        H.conv_dgrad_bnb(da, y, mean, invstd, bn.weight, bn.bias, m1, m2, dyw, wd, dx, n, h, w, cout, cin, dil, dyp,
+                         bn_bwd=bn_bwd, dx_max=dx_max)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
+        if wq is None:
+            fn()
+        else:
+            wq.submit(fn, keep)
+        return None if out_part is None else (out_part, dx_max)
     dy = H.empty(P, cout, device=y.device)
     # eval mode: the forward normalised with the running statistics (constants), so the BN
     # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
     H.bn_relu_bwd(y, da, mean, invstd, bn.weight, bn.bias, dy, grads[bn.weight], grads[bn.bias], grads[conv.bias],
-                  amax=slots.take(), part=part, eval_mode=not train)
+                  amax=slots.take(), part=part_t, eval_mode=not train)
     if DEBUG_TAPS is not None:
         _tap("dy:" + getattr(conv, "_srpde_name", "?"), dy)
-    dyp = None
-    out_part = None
-    cin = conv.in_channels if x0 is None else x0.shape[1] + (x1.shape[1] if x1 is not None else 0)
     if dx is not None:
         wd = _dgrad_weights(conv, cin, w, dil)
         if xp is not None:
             dyp = H.split_planes_buffer(P, cout, y.device)
-        bn_bwd = None
+        bn_bwd, dx_max = None, None
         if below is not None and not dx_accumulate and _FUSE_BN_BWD and H.h3_capable(cout, 0, cin, w, dil):
             bnb, sb = below
             out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
             bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
-        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp, bn_bwd=bn_bwd)
+            if _FUSE_BN_APPLY:   # max|dx| slots for a fused BN apply in the layer below
+                dx_max = H.out_max_slots(n, h, w, cout, cin, dil, y.device)
+        H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp, bn_bwd=bn_bwd,
+                   out_max=dx_max)
     dw = grads[conv.weight]
     if xp is not None and dyp is not None:
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax)
@@ -312,7 +345,12 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         fn()
     else:
         wq.submit(fn, keep)
-    return out_part
+    return None if out_part is None else (out_part, dx_max)
+
+
+# the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
+# (srpde_conv_dgrad_h3_bnb; SRPDE_FUSE_BN_APPLY=0: off)
+_FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
 
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)

@@ -293,3 +293,33 @@ def test_branch_matched_gradients_match_fp64(training, B):
 
 def _bn_fed_conv_bias(n):
     return n.endswith(".bias") and ("conv" in n or n.startswith("bridge.0") or n.startswith("bridge.3"))
+
+
+def test_fused_bn_apply_matches_separate_pass():
+    """The BN (+ReLU) backward applied inside the dgrad's operand transform
+    (srpde_conv_dgrad_h3_bnb: dy never materialised, its scale from srpde_bn_bwd_prepare's bound)
+    gives the same gradients as bn_relu_bwd + the plain dgrad (unet_exec._FUSE_BN_APPLY=False): the
+    same dy values up to the operand split's scale, so agreement to fp32 accuracy, not bits."""
+    from superresolution_for_pdes_amd import unet_exec
+    x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(9)).to(DEV)
+    x[:, 1] = 1.0
+    res = []
+    saved = unet_exec._FUSE_BN_APPLY
+    try:
+        for fuse in (True, False):
+            unet_exec._FUSE_BN_APPLY = fuse
+            m = make_model(True)
+            xd = x.clone().requires_grad_(True)
+            (m(xd) ** 2).mean().backward()
+            g = {n: p.grad.detach().double().clone() for n, p in m.named_parameters()}
+            g["input"] = xd.grad.detach().double().clone()
+            res.append(g)
+    finally:
+        unet_exec._FUSE_BN_APPLY = saved
+    for n, g in res[0].items():
+        r = res[1][n]
+        if n.endswith(".bias") and ("conv" in n or n.startswith("bridge.0") or n.startswith("bridge.3")):
+            assert float(g.norm()) <= 1e-4 and float(r.norm()) <= 1e-4, n   # true gradient 0
+            continue
+        e = float((g - r).norm() / max(float(r.norm()), 1e-30))
+        assert e < 1e-4, (n, e)
