@@ -91,13 +91,6 @@ int srpde_conv_h3_stats_rows(void);
  * on 128-row tiles, two workgroups per CU (0: never).  Returns the previous value.  Tuning and
  * tests; the default comes from SRPDE_H3_HALF. */
 int srpde_conv_h3_set_half(int max_chunks);
-/* srpde_conv_fwd_h3's persistent, streamed walk (one workgroup per CU over its row tiles, the next
- * channel chunk's halo split between the current chunk's MFMA stages; same results): 1 = taken
- * for eligible shapes (at least 4 tile rounds per CU, <= 64 output columns per tile, halo fits),
- * 0 = never.  Returns the previous value.  Tuning and tests; the default comes from SRPDE_H3S. */
-int srpde_conv_h3_set_streamed(int mode);
-/* 1 if srpde_conv_fwd_h3 takes the streamed walk for P output rows of cout channels (width w). */
-int srpde_conv_h3_streamed_taken(long long P, int cout, int w, int dil);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]

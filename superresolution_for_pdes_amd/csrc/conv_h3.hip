@@ -440,343 +440,6 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
                                  h.wide ? smem + 2 * WM * BN : nullptr, colscale);
 }
 
-// ------------- "h3s": persistent, streamed variant of the forward / dgrad kernel -------------
-// One workgroup per CU walks its row tiles (b, b + G, b + 2G, ...), so the per-tile setup is
-// paid once and nothing is exposed between tiles.  The halo tile of the NEXT channel chunk
-// (the same tile's, or chunk 0 of the next tile) is DMA'd slice by slice into F during the
-// current chunk's tap stages, and every slice is split into the second S buffer two stages
-// after its DMA by the wave that issued it (its own vmcnt covers the landing), between that
-// wave's MFMA stages: the split no longer stops the MFMAs, and no tile starts with an exposed
-// load.  One tap per stage; two S buffers; the B (weight) stages double-buffered.  Same
-// arithmetic, in the same order, as conv_fwd_h3_kernel: bit-identical outputs.
-// LDS: F [arows][128 B] | S0 hi, lo [arows][64 B] | S1 hi, lo | B [2][BN x 64 B x 2] | zero row | sink
-template <int BN, int SRB>
-__global__ __launch_bounds__(512, 1) void conv_fwd_h3s_kernel(ConvParams p, H3Args h, int G) {
-  constexpr int BM = 256, WM = 8, WN = 1, NW = 8;
-  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
-  constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per tap (16 rows x 64 B)
-  constexpr int BPW = (BTOT + NW - 1) / NW;
-  constexpr int BP_BYTES = BN * 64;
-  constexpr int B_TAP = 2 * BP_BYTES;
-  constexpr int NS = 9;                    // stages (taps) per chunk
-  constexpr int LAG = 2;                   // a halo slice DMA'd in stage s is split in stage s + LAG
-  constexpr int NDMA = NS - LAG;           // stages that issue halo slices (one per wave each)
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  char* lds = reinterpret_cast<char*>(smem);
-  const int arows = h.arows;
-  const int splane = arows * 64;           // one fp16 plane of an S buffer
-  char* const fbuf = lds;
-  char* const sbuf0 = fbuf + arows * ROW2;
-  char* const bbuf0 = sbuf0 + 4 * splane;
-  char* const zrow = bbuf0 + 2 * B_TAP;
-  char* const sink = zrow + 64;
-  float* const aff = reinterpret_cast<float*>(sink + 1024);   // [2][Cin] in_scale | in_shift (fused input BN)
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nbn = (p.Cout + BN - 1) / BN;
-  const int nbm = (p.P + BM - 1) / BM;
-  const int nfull = nbm * nbn;
-  int vt = blockIdx.x;
-  if (vt >= nfull) return;   // (the host launches G <= nfull workgroups)
-
-  if (tid < 16) reinterpret_cast<float*>(zrow)[tid] = 0.f;
-  // the fused input affine lives in LDS: the split then reads it without a vector-memory wait
-  // (a compiler-visible global load there would wait on the in-flight halo DMAs as well)
-  if (h.in_scale != nullptr)
-    for (int k = tid; k < p.Cin; k += 512) {
-      aff[k] = h.in_scale[k];
-      aff[p.Cin + k] = h.in_shift[k];
-    }
-
-  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
-  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
-  const size_t plane = (size_t)p.Cout * p.K;
-  const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
-  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
-
-  unsigned ab = h.amax0 ? *h.amax0 : 0u;
-  if (p.c1 && h.amax1) ab = max(ab, *h.amax1);
-  const int ea = h3_exp(ab);
-  const float sa = exp2i(ea);
-
-  const int lr = lane & 31, lh = lane >> 5;
-  const int wmi = wave % WM, wni = wave / WM;
-  const int wm0 = wmi * TM, wn0 = wni * TN;
-  // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot); byte offset for N-tile
-  // origin 0 (the tile's n0 * K is added at issue)
-  int b_off[BPW], b_row[BPW];
-#pragma unroll
-  for (int j = 0; j < BPW; ++j) {
-    const int q = wave + j * NW;
-    const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
-    const int r = rb * 16 + (lane >> 2);
-    b_row[j] = r;
-    b_off[j] = q < BTOT ? (int)((pl * plane + (size_t)r * p.K + swzh(r, lane & 3) * 8) * 2) : -1;
-  }
-  const int nch = p.Cin / BK2;
-  const int na = arows / 8;
-  const size_t xplane = (size_t)p.P * p.Cin;
-
-  auto issue_a = [&](int pbase, int ch, int q) {   // halo slice q (8 rows, fp32) of chunk ch -> F slot q
-    const int ch0 = ch * BK2;
-    const bool second = ch0 >= p.c0;
-    const int32x4 rs = second ? rs1 : rs0;
-    const int ld = second ? ld1 : p.ldx0;
-    const int cb = second ? ch0 - p.c0 : ch0;
-    const int r = q * 8 + (lane >> 3);
-    const int pix = pbase + r;
-    const bool real = q < na;
-    const unsigned off = (real && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + swz(r, lane & 7) * 4) * 4) : OOB;
-    dma16(rs, off, lds_addr_of(real ? fbuf + q * 1024 : sink));
-  };
-  auto issue_b = [&](int nb0, int ch, int tap, int buf) {
-    const int k0 = tap * p.Cin + ch * BK2;
-    char* bbase = bbuf0 + buf * B_TAP;
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) {
-      const int q = wave + j * NW;
-      if (q < BTOT) {
-        const unsigned off = (nb0 + b_row[j] < p.Cout) ? (unsigned)(b_off[j] + (nb0 * p.K + k0) * 2) : OOB;
-        dma16(rsw, off, lds_addr_of(bbase + q * 1024));
-      }
-    }
-  };
-  // split F slot q (this wave's own DMA, landed) into S buffer `sd`: lane -> (row, 16-B slot j
-  // holding channel quad swz(r, j)); the same expressions as conv_fwd_h3_kernel's convert.  The
-  // lane's piece of the input split (xsplit, for the weight gradient) is returned in pend and
-  // stored by flush() at the start of the next stage, ahead of that stage's DMAs (vmcnt order).
-  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-  struct Pending { half4 hv, lv; _Float16* dst; };
-  Pending pend;
-  pend.dst = nullptr;
-  auto split_slice = [&](int pbase, int ch, int q, char* sd, bool wsp) {
-    const int r = q * 8 + (lane >> 3);
-    const int c = swz(r, lane & 7);
-    float4 v = *reinterpret_cast<const float4*>(fbuf + q * 1024 + lane * 16);
-    const int pix = pbase + r;
-    if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
-      const int cc = ch * BK2 + c * 4;
-      const bool inside = pix >= 0 && pix < p.P;
-      const float4 s4 = *reinterpret_cast<const float4*>(aff + cc);
-      const float4 t4 = *reinterpret_cast<const float4*>(aff + p.Cin + cc);
-      v.x = inside ? fmaxf(v.x * s4.x + t4.x, 0.f) : 0.f;
-      v.y = inside ? fmaxf(v.y * s4.y + t4.y, 0.f) : 0.f;
-      v.z = inside ? fmaxf(v.z * s4.z + t4.z, 0.f) : 0.f;
-      v.w = inside ? fmaxf(v.w * s4.w + t4.w, 0.f) : 0.f;
-    }
-    const float vs[4] = {v.x * sa, v.y * sa, v.z * sa, v.w * sa};
-    half4 hv, lv;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const _Float16 hh = (_Float16)vs[k];
-      hv[k] = hh;
-      lv[k] = (_Float16)(vs[k] - (float)hh);
-    }
-    const int o = r * 64 + swzh(r, c >> 1) * 16 + (c & 1) * 8;
-    *reinterpret_cast<half4*>(sd + o) = hv;
-    *reinterpret_cast<half4*>(sd + splane + o) = lv;
-    pend.hv = hv;
-    pend.lv = lv;
-    pend.dst = (wsp && r >= h.halo && r < h.halo + BM && pix < p.P)
-                   ? h.xsplit + (size_t)pix * p.Cin + ch * BK2 + c * 4 : nullptr;
-  };
-  auto flush = [&]() {
-    if (pend.dst != nullptr) {
-      *reinterpret_cast<half4*>(pend.dst) = pend.hv;
-      *reinterpret_cast<half4*>(pend.dst + xplane) = pend.lv;
-      pend.dst = nullptr;
-    }
-  };
-
-  // current tile
-  int wg = xcd_remap(vt, nfull);
-  int m0 = (wg / nbn) * BM, n0 = (wg - (wg / nbn) * nbn) * BN;
-  int pbase = m0 - h.halo;
-  bool wsp = h.xsplit != nullptr && n0 == 0;
-  unsigned tmask[TI];
-  auto set_masks = [&]() {
-    const int HW = p.H * p.W;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int m = m0 + wm0 + i * 32 + lr;
-      unsigned mask = 0;
-      if (m < p.P) {
-        const int rem = m % HW, yy = rem / p.W, xx = rem - yy * p.W;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
-          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
-        }
-      }
-      tmask[i] = mask;
-    }
-  };
-  set_masks();
-
-  floatx16 acc[TI][TJ], part[TI][TJ];
-
-  // prologue (once per workgroup): the first chunk's halo tile and weight stage
-  for (int q = wave; q < na; q += NW) issue_a(pbase, 0, q);
-  issue_b(n0, 0, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();   // (the affine table)
-  for (int q = wave; q < na; q += NW) {
-    split_slice(pbase, 0, q, sbuf0, wsp);
-    flush();
-  }
-  __syncthreads();
-
-  auto tap_body = [&](const char* sh, const char* b, auto tap_tag) {
-    constexpr int TAP = decltype(tap_tag)::value;
-    constexpr int KY = TAP / 3, KX = TAP % 3;
-    const char* sl = sh + splane;
-    const int toff = p.sign > 0 ? (KY * p.W + KX) * p.dil : ((2 - KY) * p.W + (2 - KX)) * p.dil;
-    constexpr int NG = BK2 / 16;
-    half8 ah[NG][TI], al[NG][TI], bh[NG][TJ], bl[NG][TJ];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wm0 + i * 32 + lr + toff;
-        const bool ok = (tmask[i] >> TAP) & 1u;
-        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        ah[g][i] = *reinterpret_cast<const half8*>(ok ? sh + o : zrow);
-        al[g][i] = *reinterpret_cast<const half8*>(ok ? sl + o : zrow);
-      }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn0 + j * 32 + lr;
-        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        bh[g][j] = *reinterpret_cast<const half8*>(b + o);
-        bl[g][j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          floatx16 c0;
-          if (TAP == 0 && g == 0)
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], floatx16{}, 0, 0, 0);
-          else
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], part[i][j], 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bl[g][j], c0, 0, 0, 0);
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bh[g][j], c0, 0, 0, 0);
-        }
-    constexpr int RD = 2 * (TI + TJ), MF = 3 * TI * TJ;
-    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
-#pragma unroll
-    for (int k = 0; k < RD; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
-  };
-
-  int sidx = 0;   // stage counter (B buffer parity)
-  int spar = 0;   // chunk-step counter (S buffer parity)
-  for (;;) {      // tiles
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // the next tile of this workgroup (its chunk 0 is streamed in during this tile's last chunk)
-    const bool tile_next = vt + G < nfull;
-    int nwg = 0, nm0 = 0, nn0 = 0;
-    if (tile_next) {
-      nwg = xcd_remap(vt + G, nfull);
-      nm0 = (nwg / nbn) * BM;
-      nn0 = (nwg - (nwg / nbn) * nbn) * BN;
-    }
-    for (int ch = 0; ch < nch; ++ch) {
-      const bool more = ch + 1 < nch;
-      const bool pref = more || tile_next;                    // a next chunk-step exists
-      const int tch = more ? ch + 1 : 0;
-      const int tpb = more ? pbase : nm0 - h.halo;
-      const int tn0 = more ? n0 : nn0;
-      const bool twsp = more ? wsp : (h.xsplit != nullptr && nn0 == 0);
-      const char* scur = sbuf0 + (spar & 1) * 2 * splane;
-      char* snext = sbuf0 + ((spar + 1) & 1) * 2 * splane;
-      auto stage = [&](auto st_tag) {
-        constexpr int ST = decltype(st_tag)::value;
-        flush();   // the previous stage's xsplit piece: before the DMAs, so vmcnt(1) below leaves only the halo slice
-        if (ST < NS - 1) issue_b(n0, ch, ST + 1, (sidx + 1) & 1);
-        else if (pref) issue_b(tn0, tch, 0, (sidx + 1) & 1);
-        const bool a_now = ST < NDMA && pref;
-        if (a_now) issue_a(tpb, tch, wave + ST * NW);
-        const int q = wave + (ST - LAG) * NW;
-        const bool split_now = ST >= LAG && pref && q < na;
-        const char* bcur = bbuf0 + (sidx & 1) * B_TAP;
-        // waves w and w + 4 share a SIMD: one splits before its MFMAs, the other after, so each
-        // wave's split (VALU + LDS) runs under the other's MFMAs
-        if (wave < 4) {
-          if (split_now) split_slice(tpb, tch, q, snext, twsp);
-          tap_body(scur, bcur, std::integral_constant<int, ST>{});
-        } else {
-          tap_body(scur, bcur, std::integral_constant<int, ST>{});
-          if (split_now) split_slice(tpb, tch, q, snext, twsp);
-        }
-        ++sidx;
-        // the next stage's weights (and every halo slice but this stage's) have landed
-        if (a_now)
-          asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      };
-      stage(std::integral_constant<int, 0>{});
-      stage(std::integral_constant<int, 1>{});
-      stage(std::integral_constant<int, 2>{});
-      stage(std::integral_constant<int, 3>{});
-      stage(std::integral_constant<int, 4>{});
-      stage(std::integral_constant<int, 5>{});
-      stage(std::integral_constant<int, 6>{});
-      stage(std::integral_constant<int, 7>{});
-      stage(std::integral_constant<int, 8>{});
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
-      ++spar;
-    }
-    float colscale[TJ];
-    const float ia = exp2i(-ea);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + lr;
-      const int we = col < p.Cout ? h.wexp[col] : 0;
-      const int e = ea + we;
-      if (e > 126 || e < -126) {
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] *= ia;
-        colscale[j] = exp2i(-we);
-      } else {
-        colscale[j] = exp2i(-e);
-      }
-      if (col >= p.Cout) colscale[j] = 0.f;
-    }
-    // F is free (every slice of the next chunk-step was split by the last stage): epilogue scratch
-    x6_finish<BM, BN, WM, WN, SRB>(p, acc, false, wg, nfull, 0, m0, n0, wmi, wni, lane, smem,
-                                   h.wide ? smem + 2 * WM * BN : nullptr, colscale);
-    if (!tile_next) break;
-    __syncthreads();   // the epilogue's scratch reads are done before the next DMA into F
-    vt += G;
-    wg = nwg;
-    m0 = nm0;
-    n0 = nn0;
-    pbase = m0 - h.halo;
-    wsp = h.xsplit != nullptr && n0 == 0;
-    set_masks();
-  }
-}
-
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
 // Same tiling and staging as conv_wgrad_x6 (conv.hip): dW tile [BM couts][BN k-columns] over a
 // pixel chunk (split-K), 16 pixels per stage, register-staged pixel rows split into hi / lo
@@ -1404,54 +1067,6 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   return 0;
 }
 
-// h3s (persistent, streamed) eligibility: enough row tiles for several rounds per CU, the halo
-// tile in at most 7 slices per wave (arows <= 448), and two S buffers in LDS.
-static size_t h3s_lds(int bn, int arows, int cin_aff = 0) {
-  return (size_t)arows * (ROW2 + 256) + (size_t)2 * 2 * bn * 64 + 64 + 1024 + (size_t)cin_aff * 8;
-}
-// SRPDE_H3S or srpde_conv_h3_set_streamed: 0 = never; 1 (default) = when eligible
-static std::atomic<int> g_h3s{-1};
-static int h3s_mode() {
-  int v = g_h3s.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("SRPDE_H3S");
-    v = e ? std::max(0, atoi(e)) : 0;
-    int expect = -1;
-    g_h3s.compare_exchange_strong(expect, v);
-    v = g_h3s.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-static int h3_cus() {
-  static const int c = [] {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max(1, cus);
-  }();
-  return c;
-}
-static bool h3s_eligible(int P, int cout, int arows, int cin_aff = 0) {
-  if (h3s_mode() == 0 || arows > 448) return false;
-  const int bn = h3_bn(h3_cfg(cout));
-  // (the 128-column tile does not fit its registers with the streamed walk's extra state)
-  if (bn > 64 || h3s_lds(bn, arows, cin_aff) > 160 * 1024) return false;
-  const long long tiles = (long long)ceil_div(P, 256) * ceil_div(cout, bn);
-  return tiles >= 4LL * h3_cus();
-}
-
-template <int BN>
-static int launch_fwd_h3s(ConvParams p, H3Args h, hipStream_t st) {
-  const int nfull = ceil_div(p.P, 256) * ceil_div(p.Cout, BN);
-  const int G = std::min(nfull, h3_cus());
-  const size_t lds = h3s_lds(BN, h.arows, h.in_scale != nullptr ? p.Cin : 0);
-  if ((size_t)h.arows * ROW2 < (size_t)(2 * 8 * BN + 8 * 512) * 4) h.wide = 0;   // F too small to stage
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
-  hipLaunchKernelGGL((conv_fwd_h3s_kernel<BN, H3_SRB>), dim3(G), dim3(512), lds, st, p, h, G);
-  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3s)");
-  return 0;
-}
-
 int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigned* amax0, const unsigned* amax1,
                     hipStream_t st) {
   const H3W sc{amax_dy, amax0, p.c1 ? amax1 : amax0};
@@ -1557,16 +1172,6 @@ extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
 
-int srpde_conv_h3_streamed_taken(long long P, int cout, int w, int dil) {
-  return P > 0 && P < (1LL << 31) && h3s_eligible((int)P, cout, h3_arows(w, dil)) ? 1 : 0;
-}
-
-int srpde_conv_h3_set_streamed(int mode) {
-  const int prev = h3s_mode();
-  g_h3s.store(std::max(0, mode));
-  return prev;
-}
-
 int srpde_conv_h3_set_half(int max_chunks) {
   const int prev = h3_half_max();
   g_h3_half.store(std::max(0, max_chunks));
@@ -1666,9 +1271,6 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
   p.out_max = out_max;
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
-  if (h3s_eligible(p.P, cout, a.arows, in_scale != nullptr ? p.Cin : 0)) {   // persistent, streamed walk (same results)
-    return h3_cfg(cout) == 2 ? launch_fwd_h3s<64>(p, a, stream) : launch_fwd_h3s<32>(p, a, stream);
-  }
   if (p.Cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) {   // shallow K: 128-row tiles, 2 per CU
     a.arows = h3_arows(w, dil, 128);
     switch (h3_cfg(cout)) {
@@ -1754,8 +1356,7 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
 // Number of output tiles (= out_max slots) srpde_conv_fwd_h3 uses for this shape; 0 if unsupported.
 long long srpde_conv_h3_tiles(long long P, int cin, int cout, int w, int dil) {
   if (P <= 0 || !srpde_conv_h3_supported(cin, 0, cout, w, dil, 3)) return 0;
-  const int bm = (!h3s_eligible((int)P, cout, h3_arows(w, dil)) && cin / BK2 <= h3_half_max() &&
-                  h3_arows(w, dil, 128) <= 256) ? 128 : 256;
+  const int bm = (cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) ? 128 : 256;
   const int bn = h3_bn(h3_cfg(cout));
   return ((P + bm - 1) / bm) * ((cout + bn - 1) / bn);
 }

@@ -110,15 +110,6 @@ def set_h3_half(max_chunks: int) -> int:
     return int(query("srpde_conv_h3_set_half", int(max_chunks)))
 
 
-def set_h3_streamed(mode: int) -> int:
-    """h3 persistent streamed walk: 1 = taken for eligible shapes, 0 = never.  Returns the previous value."""
-    return int(query("srpde_conv_h3_set_streamed", int(mode)))
-
-
-def h3_streamed_taken(P, cout, w, dil=1) -> bool:
-    return bool(query("srpde_conv_h3_streamed_taken", int(P), int(cout), int(w), int(dil)))
-
-
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
     return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, ksize))
 

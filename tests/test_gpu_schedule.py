@@ -162,67 +162,3 @@ def test_conv_h3_half_tiles_equal_full_tiles(n, c0, c1, cout, hw, dil):
         H.set_h3_half(prev)
     for k, (a, b_) in enumerate(zip(*outs)):
         assert torch.equal(a, b_), k
-
-
-# sizes with more than half a round of tiles left over on a 256-CU part, so the tile-per-block
-# reference runs no K-split tail (whose fixup sums the BN partials in another order)
-@pytest.mark.parametrize("n,c0,c1,cout,hw,dil,fused", [(195, 64, 0, 64, 40, 1, True), (200, 128, 64, 64, 40, 1, False),
-                                                       (195, 64, 0, 32, 40, 1, True), (195, 32, 0, 16, 40, 1, True),
-                                                       (750, 128, 0, 64, 20, 1, True)])
-def test_conv_h3_streamed_walk_equals_tile_per_block(n, c0, c1, cout, hw, dil, fused):
-    """The persistent streamed walk (srpde_conv_h3_set_streamed) computes outputs, BN partials,
-    stored splits, the fused input BN+ReLU, the fused BN-backward partials and the per-tile max
-    in the same order as one tile per workgroup: equal bits, forward and dgrad (a ragged last
-    row tile at these sizes)."""
-    from superresolution_for_pdes_amd import hipops as H
-    if H.conv_math() != "h3" or not (H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, c0 + c1, hw, dil)):
-        pytest.skip("not an h3 shape")
-    P, cin = n * hw * hw, c0 + c1
-    assert H.h3_streamed_taken(P, cout, hw, dil)
-    g = torch.Generator(device=DEV).manual_seed(5)
-    x = torch.randn(P, cin, device=DEV, generator=g)
-    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
-    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
-    b = torch.randn(cout, device=DEV, generator=g)
-    wf, wd = H.pack_conv_weights(w, cin, True, True)
-    dy = torch.randn(P, cout, device=DEV, generator=g)
-    aff = None
-    if fused and not c1:
-        aff = (torch.rand(cin, device=DEV, generator=g) + 0.5, torch.randn(cin, device=DEV, generator=g) * 0.3)
-    # the dgrad's fused BN-backward reduction reads a BN + ReLU of the forward input
-    bny = torch.randn(P, cin, device=DEV, generator=g)
-    mean = torch.randn(cin, device=DEV, generator=g) * 0.1
-    invstd = torch.rand(cin, device=DEV, generator=g) + 0.5
-    gam = torch.randn(cin, device=DEV, generator=g)
-    bet = torch.randn(cin, device=DEV, generator=g) * 0.2
-    for t in (x0, x1, dy):
-        if t is not None:
-            t._srpde_amax = H.amax_of(t)
-    if aff is not None:   # the operand scale bounds the transformed input
-        x0._srpde_amax = H.amax_of(torch.relu(x0 * aff[0] + aff[1]))
-    outs = []
-    prev = H.set_h3_streamed(0)
-    try:
-        for mode in (0, 1):
-            H.set_h3_streamed(mode)
-            y = torch.empty(P, cout, device=DEV)
-            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
-            xp = H.split_planes_buffer(P, cin, DEV)
-            if aff is not None:
-                H.conv_fwd(x0, None, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp, in_affine=aff)
-            else:
-                H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
-            dx = torch.empty(P, cin, device=DEV)
-            dyp = H.split_planes_buffer(P, cout, DEV)
-            extra = {}
-            if fused:
-                part = H.bn_bwd_partials(n, hw, hw, cin, DEV)
-                omax = H.out_max_slots(n, hw, hw, cout, cin, dil, DEV)
-                extra = dict(bn_bwd=(bny, mean, invstd, gam, bet, part), out_max=omax)
-            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp, **extra)
-            torch.cuda.synchronize()
-            outs.append((y, stats, xp, dx, dyp) + ((part, omax) if fused else ()))
-    finally:
-        H.set_h3_streamed(prev)
-    for k, (a, b_) in enumerate(zip(*outs)):
-        assert torch.equal(a, b_), k
