@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -x -q --timeout 120 --timeout-method
 tail -1 gpurun_out/pytest_$T.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$T.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke_$T.log; exit 1; }
 tail -1 gpurun_out/smoke_$T.log
-cp profiles/traffic_r01.json gpurun_out/traffic_$T.json
+cp profiles/traffic_r02.json gpurun_out/traffic_$T.json
 cd /tmp
 i=0
 for C in FETCH_SIZE WRITE_SIZE; do
