@@ -96,18 +96,22 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   constexpr int AD = BNB ? 2 : 1;               // DMAs per halo slice (BNB: the gradient and the BN input)
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
   static_assert(TPS >= 1 && TPS <= 3, "taps per stage");
-  // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its hi / lo fp16 planes (64-B rows)
-  //      | B = two weight stages | 64 zero bytes (the padding row) | 1 KiB DMA sink
+  // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its split, 128-B rows of eight 16-B
+  //      chunks: hi pieces of channel group c8 in chunk c8, lo pieces in chunk 4 + c8, chunk k at
+  //      slot swz(r, k) (conflict-free reads at any tap shift; a row's four fragments of one
+  //      lane are XOR 32 / 64 / 96 of each other) | B = two weight stages | 128 zero bytes
+  //      (the padding row, 128-B aligned so the XORs stay in it) | 1 KiB DMA sink
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int arows = h.arows;
   char* const fbuf = lds;
   char* const fbuf2 = fbuf + arows * ROW2;      // BNB: fp32 halo tile of the BN input y
-  char* const shi = fbuf + (BNB ? 2 : 1) * arows * ROW2;
-  char* const slo = shi + arows * 64;
-  char* const bbuf0 = slo + arows * 64;
+  const int soff = (BNB ? 2 : 1) * arows * ROW2;   // S, as a byte offset from lds
+  char* const sbuf = lds + soff;
+  char* const bbuf0 = sbuf + arows * 128;
   char* const zrow = bbuf0 + 2 * B_STAGE;
-  char* const sink = zrow + 64;
+  const int zoff = soff + arows * 128 + 2 * B_STAGE;
+  char* const sink = zrow + 128;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -127,7 +131,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int m0 = mt * BM, n0 = nt * BN;
   const int HW = p.H * p.W;
 
-  if (tid < 16) reinterpret_cast<float*>(zrow)[tid] = 0.f;
+  if (tid < 32) reinterpret_cast<float*>(zrow)[tid] = 0.f;
 
   const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
@@ -142,25 +146,29 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int ea = h3_exp(ab);
   const float sa = exp2i(ea);
 
-  // per-lane tap masks of this wave's output rows
+  // per tap: the LDS byte offset of this lane's first A fragment (hi pieces, k-group 0) of its
+  // output row shifted by the tap; the zero row for taps outside the image.  Computed once per
+  // tile, so a tap stage's A reads cost no address arithmetic beyond three XORs.
   const int lr = lane & 31, lh = lane >> 5;
   const int wmi = wave % WM, wni = wave / WM;
   const int wm0 = wmi * TM, wn0 = wni * TN;
-  unsigned tmask[TI];
+  int aoff[9][TI];
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int m = m0 + wm0 + i * 32 + lr;
-    unsigned mask = 0;
+    int yy = -(1 << 20), xx = 0;   // rows past the tensor: every tap reads the zero row
     if (m < p.P) {
-      const int n = m / HW, rem = m - n * HW, yy = rem / p.W, xx = rem - yy * p.W;
-      (void)n;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
-        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) mask |= 1u << t;
-      }
+      const int rem = m % HW;
+      yy = rem / p.W;
+      xx = rem - yy * p.W;
     }
-    tmask[i] = mask;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
+      const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
+      const int r = wm0 + i * 32 + lr + (ky * p.W + kx) * p.dil;
+      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? soff + r * 128 + swz(r, lh) * 16 : zoff;
+    }
   }
   // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1
   int b_off[BPW];
@@ -268,9 +276,8 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
       }
       half8 hv, lv;
       split2h(v0, v1, sa, hv, lv);
-      const int o = r * 64 + swzh(r, c8) * 16;
-      *reinterpret_cast<half8*>(shi + o) = hv;
-      *reinterpret_cast<half8*>(slo + o) = lv;
+      *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, c8) * 16) = hv;
+      *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, 4 + c8) * 16) = lv;
       if (wsplit) {
         const int pix = pix0 + r;
         if (r >= h.halo && r < h.halo + BM && pix < p.P) {
@@ -309,19 +316,14 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   // reads complete under the first group's MFMAs)
   auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
-    constexpr int KY = TAP / 3, KX = TAP % 3;
-    const int toff = p.sign > 0 ? (KY * p.W + KX) * p.dil : ((2 - KY) * p.W + (2 - KX)) * p.dil;
     constexpr int NG = BK2 / 16;
     half8 ah[NG][TI], al[NG][TI], bh[NG][TJ], bl[NG][TJ];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int r = wm0 + i * 32 + lr + toff;
-        const bool ok = (tmask[i] >> TAP) & 1u;
-        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        ah[g][i] = *reinterpret_cast<const half8*>(ok ? shi + o : zrow);
-        al[g][i] = *reinterpret_cast<const half8*>(ok ? slo + o : zrow);
+      for (int i = 0; i < TI; ++i) {   // k-group g: XOR 32; lo pieces: XOR 64 (see the LDS layout)
+        ah[g][i] = *reinterpret_cast<const half8*>(lds + (aoff[TAP][i] ^ (32 * g)));
+        al[g][i] = *reinterpret_cast<const half8*>(lds + (aoff[TAP][i] ^ (32 * g + 64)));
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
@@ -1024,7 +1026,7 @@ static int h3_half_max() {
 }
 
 static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false) {
-  return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 64 + 1024;
+  return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 128 + 1024;
 }
 // taps per stage: the most (<= SRPDE_H3_TPS, default 2) whose weight double-buffer fits in LDS
 static int h3_tps(int bn, int arows) {
