@@ -309,6 +309,27 @@ size_t srpde_poisson_cg_grid_done_offset(int B, int n);
 int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit, void* ws, size_t ws_bytes,
                                  hipStream_t stream);
 
+/* ---- Row-sharded CG for ONE n x n problem over `world` ranks (the 640^2 ground
+ *      truth of solve_multi_resolution, src/resolution_comparison.py:62-73).  Rank `rank` owns the
+ *      rows [row0, row0 + nloc) (rank order tiles [0, n)); f / theta / u are its [nloc][n] fp64
+ *      rows.  Per iteration k the caller runs
+ *        iter_a(k) -> all-gather spq (1 double per rank) into gpq[world]
+ *        iter_b(k) -> all-gather send (4n + 1 doubles per rank) into gath[world][4n + 1]
+ *      after init (whose send buffer is gathered first); gath / gpq may alias send / spq at world 1.
+ *      Convergence (rr <= rtol^2 rr_0 or k = maxit) is decided identically on every rank; the int
+ *      at byte srpde_poisson_rows_done_offset of the workspace turns nonzero then (poll it every few
+ *      dozen iterations; further calls are no-ops).  No call synchronises the host. */
+size_t srpde_poisson_rows_workspace_size(int n, int nloc);
+size_t srpde_poisson_rows_done_offset(int n, int nloc);
+int srpde_poisson_rows_init(const double* f, const double* theta, int n, int nloc, void* ws, size_t ws_bytes,
+                            double* send, hipStream_t stream);
+int srpde_poisson_rows_iter_a(int n, int nloc, int row0, int rank, int world, const double* gath, int k, int maxit,
+                              double rtol, void* ws, size_t ws_bytes, double* spq, hipStream_t stream);
+int srpde_poisson_rows_iter_b(int n, int nloc, int world, const double* gath, const double* gpq, int k, void* ws,
+                              size_t ws_bytes, double* send, hipStream_t stream);
+int srpde_poisson_rows_finish(double* u, int* iters, int n, int nloc, int maxit, void* ws, size_t ws_bytes,
+                              hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,3 +55,81 @@ def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, devic
     call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),
          iters.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
     return (u, iters) if return_iters else u
+
+
+def solve_rows_sharded(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, device="cuda", group=None,
+                       check_every: int = 64, return_iters: bool = False):
+    """ONE n x n problem (theta*Lap(u) = f) with its rows sharded over the ranks of ``group``
+    (the ground-truth solve of solve_multi_resolution, resolution_comparison.py:62-73):
+    every rank passes the whole f / theta (the seeded draws are replicated), solves the rows
+    shard_range(n, rank, world) with the srpde_poisson_rows_* kernels -- per iteration two launches
+    and two all-gathers (one scalar, then the rank's <r,r> partial with its first / last rows of r and
+    p, which is what the neighbours' stencils need) -- and all ranks return the full u[n, n].  At
+    world 1 (no process group) it runs the same kernels without collectives."""
+    import torch.distributed as dist
+
+    from .data_generation import shard_range
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    f = _dev_f64(f, device)
+    theta = _dev_f64(theta, device)
+    if theta.shape != f.shape:
+        theta = theta.expand_as(f).contiguous()
+    n = f.shape[-1]
+    if f.dim() != 2 or f.shape[0] != n:
+        raise ValueError("one square problem [n, n]")
+    if world > n:
+        raise ValueError(f"more ranks ({world}) than grid rows ({n})")
+    if maxit is None:
+        maxit = 20 * n * n
+    lo, hi = shard_range(n, rank, world)
+    nloc = hi - lo
+    fl, tl = f[lo:hi].contiguous(), theta[lo:hi].contiguous()
+    ws_bytes = int(query("srpde_poisson_rows_workspace_size", n, nloc))
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=device)
+    done_at = int(query("srpde_poisson_rows_done_offset", n, nloc))
+    done = ws[done_at:done_at + 4].view(torch.int32)
+    send = torch.zeros(4 * n + 1, dtype=torch.float64, device=device)
+    spq = torch.zeros(1, dtype=torch.float64, device=device)
+    if world > 1:
+        gath = torch.zeros(world, 4 * n + 1, dtype=torch.float64, device=device)
+        gpq = torch.zeros(world, 1, dtype=torch.float64, device=device)
+        gath_parts, gpq_parts = list(gath.unbind(0)), list(gpq.unbind(0))
+
+        def gather_send():
+            dist.all_gather(gath_parts, send, group=group)
+
+        def gather_pq():
+            dist.all_gather(gpq_parts, spq, group=group)
+    else:
+        gath, gpq = send, spq
+        gather_send = gather_pq = (lambda: None)
+    sp = stream_ptr()
+    call("srpde_poisson_rows_init", fl.data_ptr(), tl.data_ptr(), n, nloc, ws.data_ptr(), ws_bytes,
+         send.data_ptr(), sp)
+    gather_send()
+    for k in range(maxit + 1):
+        call("srpde_poisson_rows_iter_a", n, nloc, lo, rank, world, gath.data_ptr(), k, int(maxit), float(rtol),
+             ws.data_ptr(), ws_bytes, spq.data_ptr(), sp)
+        gather_pq()
+        call("srpde_poisson_rows_iter_b", n, nloc, world, gath.data_ptr(), gpq.data_ptr(), k, ws.data_ptr(),
+             ws_bytes, send.data_ptr(), sp)
+        gather_send()
+        # every rank decides convergence from the same gathered values, so all leave together
+        if (k + 1) % check_every == 0 and int(done.item()):
+            break
+    ul = torch.empty(nloc, n, dtype=torch.float64, device=device)
+    it = torch.zeros(1, dtype=torch.int32, device=device)
+    call("srpde_poisson_rows_finish", ul.data_ptr(), it.data_ptr(), n, nloc, int(maxit), ws.data_ptr(), ws_bytes, sp)
+    if world > 1:
+        counts = [shard_range(n, r, world) for r in range(world)]
+        cmax = max(b - a for a, b in counts)
+        pad = torch.zeros(cmax, n, dtype=torch.float64, device=device)
+        pad[:nloc] = ul
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        u = torch.cat([parts[r][:b - a] for r, (a, b) in enumerate(counts)])
+    else:
+        u = ul
+    return (u, int(it.item())) if return_iters else u

@@ -22,9 +22,19 @@ from . import poisson as P
 from .models import upsample_bilinear
 
 
+def _world() -> int:
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
 def solve_multi_resolution(n_coarse: int = 40, resolutions: List[int] = (80, 160, 320, 640), device="cuda",
-                           verbose: bool = False):
-    """resolution_comparison.py:13-78 with the GT solves on device (returns numpy fields)."""
+                           verbose: bool = False, shard_gt: bool = False):
+    """resolution_comparison.py:13-78 with the GT solves on device (returns numpy fields).
+
+    ``shard_gt``: under a process group of world > 1, the finest level's solve runs row-sharded
+    over the ranks (poisson.solve_rows_sharded); every rank still returns every
+    field.  Off by default: at 640^2 the solve is latency-bound (two collectives per CG
+    iteration), and the replicated single-GPU solve is the faster one."""
     resolutions = list(resolutions)
     k1 = np.random.uniform(10.0, 11.0)
     k2 = np.random.uniform(10.0, 11.0)
@@ -38,7 +48,10 @@ def solve_multi_resolution(n_coarse: int = 40, resolutions: List[int] = (80, 160
         step = n_finest // res
         data["f"][res] = f_finest if res == n_finest else f_finest[::step, ::step]
         data["theta"][res] = theta_finest if res == n_finest else theta_finest[::step, ::step]
-        data["u"][res] = P.solve_batched(data["f"][res], data["theta"][res], device=device)[0].cpu().numpy()
+        if shard_gt and res == n_finest and _world() > 1:
+            data["u"][res] = P.solve_rows_sharded(data["f"][res], data["theta"][res], device=device).cpu().numpy()
+        else:
+            data["u"][res] = P.solve_batched(data["f"][res], data["theta"][res], device=device)[0].cpu().numpy()
         if verbose:
             print(f"u_{res} - min: {data['u'][res].min():.6f}, max: {data['u'][res].max():.6f}")
     return data
