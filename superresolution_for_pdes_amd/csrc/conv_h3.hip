@@ -1101,8 +1101,16 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
   int bm, bn;
   h3p_tiles(cout, K, &bm, &bn);
   const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
-  // one workgroup per CU (LDS): ~4 rounds of 256 CUs, chunks a multiple of the 32-pixel stage
-  const long long want = std::max(1LL, 1024 / tiles);
+  // one workgroup per CU (LDS): ~2 rounds of 256 CUs, chunks a multiple of the 32-pixel stage.
+  // The weight gradients run on a side stream next to the dgrad chain; half the workgroups of the
+  // earlier 4-round target leave CUs to the critical path and halve the split-K reduction
+  // (step 34.94 / 35.06 -> 34.56 / 34.59 ms same box; 256 the same, 128: 37.1 ms).
+  // SRPDE_WGRAD_WG overrides the target (tuning).
+  static const long long target = [] {
+    const char* e = getenv("SRPDE_WGRAD_WG");
+    return e ? std::max(1LL, atoll(e)) : 512LL;
+  }();
+  const long long want = std::max(1LL, target / tiles);
   long long c = (P + want - 1) / want;
   c = (c + 31) / 32 * 32;
   if (c < 256) c = 256;
