@@ -337,8 +337,16 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
+        # SRPDE_BENCH_BACKEND=gloo: rehearse the N > 1 path with several ranks on one GPU (RCCL
+        # refuses two ranks on one device); the driver's runs use RCCL ("nccl")
+        backend = os.environ.get("SRPDE_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.workload != "train":
