@@ -91,6 +91,11 @@ int srpde_conv_h3_stats_rows(void);
  * on 128-row tiles, two workgroups per CU (0: never).  Returns the previous value.  Tuning and
  * tests; the default comes from SRPDE_H3_HALF. */
 int srpde_conv_h3_set_half(int max_chunks);
+/* Kernel choice of srpde_conv_fwd_h3 for output tiles of <= 64 channels: 1 = the register-staged
+ * 4-wave kernel, two workgroups per CU (default; SRPDE_H3R=0 turns it off), 0 = the 8-wave
+ * kernel.  Both compute the same outputs, statistics and stored splits bit for bit (outside a
+ * K-split tail).  Returns the previous value.  Tuning and tests. */
+int srpde_conv_h3r_set(int on);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]

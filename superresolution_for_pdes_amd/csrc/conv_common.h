@@ -174,9 +174,9 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
           float xh, dz;
 #define BNP_ACC(X)                                     \
   xh = (yv.X - mu.X) * is.X;                           \
-  dz = xh * ga.X + be.X > 0.f ? v[i].X : 0.f;          \
+  dz = __builtin_fmaf(xh, ga.X, be.X) > 0.f ? v[i].X : 0.f; \
   s1.X += dz;                                          \
-  s2.X += dz * xh;
+  s2.X = __builtin_fmaf(dz, xh, s2.X);
           BNP_ACC(x) BNP_ACC(y) BNP_ACC(z) BNP_ACC(w)
 #undef BNP_ACC
         }
@@ -250,8 +250,8 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
 }
 
 // epilogue shared by the x6 / h3 forward kernels: raw tail-piece tiles, or bias + store + BN
-// partial statistics per SRB rows.  `stage` (nullable): 2 KiB of LDS per wave, past the
-// reduction scratch, through which the output leaves as 16-B row stores (needs ldy % 4 == 0 and
+// partial statistics per SRB rows.  Reduction scratch: smem[2][WM * TI][BN] floats.  `stage`
+// (nullable): 2 KiB of LDS per wave, past the reduction scratch, through which the output leaves as 16-B row stores (needs ldy % 4 == 0 and
 // a 16-B aligned y): 4 dwordx4 stores per lane and 32x32 block instead of 16 dword stores.
 // `colscale` (nullable): per accumulator column block j, an exact power-of-two scale still to be
 // applied (h3: the operand scales); it is fused with the bias into one FMA (bit-identical to the
@@ -361,7 +361,7 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
     __syncthreads();
   }
   if (p.bn_part != nullptr) {         // fused BN-backward reduction of the layer below (see ConvParams)
-    float* red = smem;                // [2][WM][BN]
+    float* red = smem;                // [2][WM * TI][BN]: one partial per 32-row block
     const int sb = wmi / WPS;
     const int rb0 = m0 + sb * SRB;
 #pragma unroll
@@ -370,24 +370,26 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
       const bool cok = col < p.Cout;
       const float mu = cok ? p.bn_mean[col] : 0.f, is = cok ? p.bn_invstd[col] : 0.f;
       const float ga = cok ? p.bn_gamma[col] : 0.f, be = cok ? p.bn_beta[col] : 0.f;
-      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI; ++i) {
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (row_ok(row) && cok) {
+            // explicit FMAs: the same instructions in every kernel instantiation (equal bits)
             const float xh = (byv[i][j][r] - mu) * is;
-            const float dz = xh * ga + be > 0.f ? acc[i][j][r] : 0.f;
+            const float dz = __builtin_fmaf(xh, ga, be) > 0.f ? acc[i][j][r] : 0.f;
             s1 += dz;
-            s2 += dz * xh;
+            s2 = __builtin_fmaf(dz, xh, s2);
           }
         }
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (lh == 0) {
-        red[wmi * BN + wn0 + j * 32 + lr] = s1;
-        red[WM * BN + wmi * BN + wn0 + j * 32 + lr] = s2;
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (lh == 0) {
+          red[(wmi * TI + i) * BN + wn0 + j * 32 + lr] = s1;
+          red[(WM + wmi) * TI * BN + i * BN + wn0 + j * 32 + lr] = s2;
+        }
       }
     }
     __syncthreads();
@@ -397,9 +399,9 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
         const int cl = wn0 + j * 32 + lr, col = n0 + cl;
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < WPS; ++w) {
-          t1 += red[(sb * WPS + w) * BN + cl];
-          t2 += red[WM * BN + (sb * WPS + w) * BN + cl];
+        for (int w = 0; w < WPS * TI; ++w) {
+          t1 += red[(sb * WPS * TI + w) * BN + cl];
+          t2 += red[WM * TI * BN + (sb * WPS * TI + w) * BN + cl];
         }
         if (col < p.Cout) p.bn_part[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(t1, t2);
       }
@@ -407,47 +409,49 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
     __syncthreads();
   }
   if (p.stats == nullptr) return;
-  float* red = smem;                  // [WM][BN] per-wave-row column partials
+  // per-32-row-block column partials [WM * TI][BN], combined in row order: the statistics of a
+  // tile do not depend on how its rows are dealt to waves (equal bits across wave layouts)
+  float* red = smem;
   const int sb = wmi / WPS;           // this wave's statistics sub-block
   const int rb0 = m0 + sb * SRB;
   const int cnt = FULL ? SRB : min(SRB, p.P - rb0);
   float mean[TJ];
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
+  for (int j = 0; j < TJ; ++j)
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+    for (int i = 0; i < TI; ++i) {
+      float s = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         s += row_ok(row) ? acc[i][j][r] : 0.f;
       }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
+      s += __shfl_xor(s, 32, 64);
+      if (lh == 0) red[(wmi * TI + i) * BN + wn0 + j * 32 + lr] = s;
+    }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + wn0 + j * 32 + lr];
+    for (int w = 0; w < WPS * TI; ++w) s += red[(sb * WPS * TI + w) * BN + wn0 + j * 32 + lr];
     mean[j] = cnt > 0 ? s / (float)cnt : 0.f;
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
+  for (int j = 0; j < TJ; ++j)
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+    for (int i = 0; i < TI; ++i) {
+      float s = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const float d = acc[i][j][r] - mean[j];
         s = row_ok(row) ? __builtin_fmaf(d, d, s) : s;   // the same FMA on both paths (bit-equal tiles)
       }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
+      s += __shfl_xor(s, 32, 64);
+      if (lh == 0) red[(wmi * TI + i) * BN + wn0 + j * 32 + lr] = s;
+    }
   __syncthreads();
   if (wmi % WPS == 0 && lh == 0 && cnt > 0) {
 #pragma unroll
@@ -455,7 +459,7 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
       const int cl = wn0 + j * 32 + lr, col = n0 + cl;
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < WPS; ++w) s += red[(sb * WPS + w) * BN + cl];
+      for (int w = 0; w < WPS * TI; ++w) s += red[(sb * WPS * TI + w) * BN + cl];
       if (col < p.Cout) p.stats[(size_t)(rb0 / SRB) * p.Cout + col] = make_float2(mean[j], s);
     }
   }

@@ -442,6 +442,329 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
                                  h.wide ? smem + 2 * WM * BN : nullptr, colscale);
 }
 
+// ------------- h3r: register-staged halo tiles, 4 waves, two workgroups per CU -------------
+// The shallow-K layers (output tiles of 64 / 32 channels: the 40x40 convolutions and the dgrads
+// into 64 channels) run only 2-6 channel chunks per tile, so the per-tile work -- tap-address
+// setup, halo split, bias + BatchNorm-statistics epilogue, DMA latency at the prologue -- weighs
+// as much as the MFMAs, and with one 8-wave workgroup per CU (conv_fwd_h3_kernel: fp32 halo tile
+// F + its split S + weight stages = 120 KiB of LDS) every wave of the CU reaches those phases at
+// the same barriers and the MFMA pipes idle through them.  Here the next chunk's halo tile is
+// loaded into VGPRs (buffer_load_dwordx4, issued in slices behind the weight DMAs of the first
+// stages) instead of into an fp32 LDS tile, and split from registers into S after the chunk:
+// no F, so a workgroup needs S + two weight stages (<= 77 KiB) and two workgroups share a CU --
+// one's setup / split / epilogue runs under the other's MFMAs.  A workgroup is 4 waves stacked
+// along M, each 64 rows x BN columns (8 fragment reads per 12 MFMAs at BN = 64, against 6 per 6
+// in the 8-wave 32-row layout).  Same arithmetic (the same split, product order and two-level
+// accumulation per chunk) and the same epilogue, statistics blocks and output as the 8-wave kernel.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ f32x4 llvm_raw_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+
+template <int BN, int TPS, int NTK, bool EARLY>
+__global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Args h) {
+  constexpr int BM = 256, WM = 4, WN = 1, NW = 4, NT = 256, SRB = 128;
+  constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
+  constexpr int BTOT = 2 * BN / 16;        // B DMA instructions per tap (16 rows x 64 B)
+  constexpr int BPW = (BTOT + NW - 1) / NW;
+  constexpr int BP_BYTES = BN * 64;
+  constexpr int B_TAP = 2 * BP_BYTES;
+  constexpr int B_STAGE = TPS * B_TAP;
+  constexpr int NS = (9 + TPS - 1) / TPS;
+  constexpr int PFS = NS - 1 < 3 ? NS - 1 : 3;      // EARLY: stages that issue halo loads for the next chunk
+  constexpr int TPST = (NTK + PFS - 1) / PFS;       // halo tasks per such stage (2 loads each)
+  // LDS: 128 zero bytes (the padding row) | S (arows 128-B rows: hi / lo fp16 pieces of 32
+  // channels, slot swz(r, k)) | two weight stages.  Every A-fragment offset is below 64 KiB, so
+  // the per-tap offsets of a lane's two row blocks share one VGPR.
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  const int arows = h.arows;
+  char* const zrow = lds;
+  char* const sbuf = lds + 128;
+  char* const bbuf0 = sbuf + arows * 128;
+  constexpr int zoff = 0;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int nbm = (p.P + BM - 1) / BM;
+  const int nfull = nbm * nbn - p.ntail;
+  int wg, piece = 0;
+  if ((int)blockIdx.x < nfull) {
+    wg = xcd_remap(blockIdx.x, nfull);
+  } else {
+    const int q = blockIdx.x - nfull;
+    wg = nfull + q / p.tsplit;
+    piece = q - (q / p.tsplit) * p.tsplit;
+  }
+  const bool tail = wg >= nfull;
+  const int mt = wg / nbn, nt = wg - mt * nbn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HW = p.H * p.W;
+
+  if (tid < 32) reinterpret_cast<float*>(zrow)[tid] = 0.f;
+
+  const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
+  const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
+  const size_t plane = (size_t)p.Cout * p.K;
+  const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
+  const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
+
+  unsigned ab = h.amax0 ? *h.amax0 : 0u;
+  if (p.c1 && h.amax1) ab = max(ab, *h.amax1);
+  const int ea = h3_exp(ab);
+  const float sa = exp2i(ea);
+
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wmi = wave, wni = 0;
+  const int wm0 = wmi * TM, wn0 = 0;
+  static_assert(TI == 2, "two row blocks per wave: one packed offset word per tap");
+  int aoff[9][TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int m = m0 + wm0 + i * 32 + lr;
+    int yy = -(1 << 20), xx = 0;
+    if (m < p.P) {
+      const int rem = m % HW;
+      yy = rem / p.W;
+      xx = rem - yy * p.W;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
+      const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
+      const int r = wm0 + i * 32 + lr + (ky * p.W + kx) * p.dil;
+      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? 128 + r * 128 + swz(r, lh) * 16 : zoff;
+    }
+  }
+  unsigned apk[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) apk[t] = (unsigned)aoff[t][0] | ((unsigned)aoff[t][1] << 16);
+  int b_off[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int q = wave + j * NW;
+    const int pl = q / (BN / 16), rb = q - pl * (BN / 16);
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzh(r, lane & 3);
+    const int nn = n0 + r;
+    b_off[j] = (q < BTOT && nn < p.Cout) ? (int)((pl * plane + (size_t)nn * p.K + c * 8) * 2) : -1;
+  }
+
+  const int nch = p.Cin / BK2;
+  const int c_beg = tail ? (piece * nch) / p.tsplit : 0;
+  const int c_end = tail ? ((piece + 1) * nch) / p.tsplit : nch;
+  const int ntask = arows * 4;                // (halo row, 8-channel group) tasks of one chunk
+  const int pix0 = m0 - h.halo;
+
+  // the halo tile of chunk `ch`, task k of this thread -> pf[k] (8 fp32 channels; rows outside
+  // the tensor and tasks past the tile: the range check returns zeros)
+  f32x4 pf[NTK][2];
+  auto load_task = [&](int ch, int k) {
+    const int ch0 = ch * BK2;
+    const bool second = ch0 >= p.c0;
+    const int32x4 rs = second ? rs1 : rs0;
+    const int ld = second ? ld1 : p.ldx0;
+    const int cb = second ? ch0 - p.c0 : ch0;
+    int t = tid;
+    asm volatile("" : "+v"(t));   // recompute the task addresses per call (no registers held across the loop)
+    const int sg = t + NT * k;
+    const int r = sg >> 2, c8 = sg & 3;
+    const int pix = pix0 + r;
+    const unsigned off = (sg < ntask && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + c8 * 8) * 4) : OOB;
+    pf[k][0] = llvm_raw_buffer_load_f4(rs, (int)off, 0, 0);
+    pf[k][1] = llvm_raw_buffer_load_f4(rs, (int)(off + 16u), 0, 0);
+  };
+  auto issue_b = [&](int ch, int st, int buf) {
+#pragma unroll
+    for (int u = 0; u < TPS; ++u) {
+      const int tap = st * TPS + u;
+      if (tap < 9) {
+        const int k0 = tap * p.Cin + ch * BK2;
+        char* bbase = bbuf0 + buf * B_STAGE + u * B_TAP;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) {
+          const int q = wave + j * NW;
+          if (q < BTOT) {
+            const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+            dma16(rsw, off, lds_addr_of(bbase + q * 1024));
+          }
+        }
+      }
+    }
+  };
+  const bool wsplit = h.xsplit != nullptr && nt == 0;
+  const size_t xplane = (size_t)p.P * p.Cin;
+  // registers (chunk ch) -> S: scale and split every halo element once per chunk
+  auto convert = [&](int ch) {
+    int t = tid;
+    asm volatile("" : "+v"(t));   // as in load_task
+#pragma unroll
+    for (int k = 0; k < NTK; ++k) {
+      const int sg = t + NT * k;
+      if (sg < ntask) {
+        const int r = sg >> 2, c8 = sg & 3;
+        float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
+        float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
+        if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
+          const int cc = ch * BK2 + c8 * 8, pix = pix0 + r;
+          const bool inside = pix >= 0 && pix < p.P;
+          const float4 s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
+          const float4 s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
+          const float4 t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
+          const float4 t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
+#define AFF(V, S, T, X) V.X = inside ? fmaxf(V.X * S.X + T.X, 0.f) : 0.f;
+          AFF(v0, s0, t0, x) AFF(v0, s0, t0, y) AFF(v0, s0, t0, z) AFF(v0, s0, t0, w)
+          AFF(v1, s1, t1, x) AFF(v1, s1, t1, y) AFF(v1, s1, t1, z) AFF(v1, s1, t1, w)
+#undef AFF
+        }
+        half8 hv, lv;
+        split2h(v0, v1, sa, hv, lv);
+        *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, c8) * 16) = hv;
+        *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, 4 + c8) * 16) = lv;
+        if (wsplit) {
+          const int pix = pix0 + r;
+          if (r >= h.halo && r < h.halo + BM && pix < p.P) {
+            _Float16* dst = h.xsplit + (size_t)pix * p.Cin + ch * BK2 + c8 * 8;
+            *reinterpret_cast<half8*>(dst) = hv;
+            *reinterpret_cast<half8*>(dst + xplane) = lv;
+          }
+        }
+      }
+    }
+  };
+
+  floatx16 acc[TI][TJ], part[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // prologue: the first chunk's halo tile + first weight stage
+#pragma unroll
+  for (int k = 0; k < NTK; ++k) load_task(c_beg, k);
+  issue_b(c_beg, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  convert(c_beg);
+  __syncthreads();
+
+  int sidx = 0;
+  auto tap_body = [&](const char* b, auto tap_tag) {
+    constexpr int TAP = decltype(tap_tag)::value;
+    constexpr int NG = BK2 / 16;
+    unsigned pk = apk[TAP];
+    asm volatile("" : "+v"(pk));   // the four XOR'd fragment addresses per row block are formed here,
+                                    // not hoisted out of the chunk loop (72 live addresses would spill)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int ao = i == 0 ? (int)(pk & 0xffffu) : (int)(pk >> 16);
+        ah[i] = *reinterpret_cast<const half8*>(lds + (ao ^ (32 * g)));
+        al[i] = *reinterpret_cast<const half8*>(lds + (ao ^ (32 * g + 64)));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int r = wn0 + j * 32 + lr;
+        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
+        bh[j] = *reinterpret_cast<const half8*>(b + o);
+        bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          floatx16 c0;
+          if (TAP == 0 && g == 0)
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], floatx16{}, 0, 0, 0);
+          else
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], part[i][j], 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
+        }
+      // one k-group's fragments live at a time (the register budget of two workgroups per CU);
+      // the other workgroup's waves cover the read latency
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto stage = [&](int ch, auto st_tag) {
+    constexpr int ST = decltype(st_tag)::value;
+    const bool more = ch + 1 < c_end;
+    if (ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
+    else if (more) issue_b(ch + 1, 0, (sidx + 1) & 1);
+    // EARLY: the next chunk's halo tile is loaded in slices behind the weight DMAs of stages
+    // 0..PFS-1 (its latency hidden by the chunk's MFMAs); otherwise after the chunk's last fragment
+    // reads (the prefetch registers never live together with the fragments; the other workgroup
+    // on the CU runs its MFMAs through the load latency)
+    constexpr int K0 = ST * TPST, K1 = (ST + 1) * TPST < NTK ? (ST + 1) * TPST : NTK;
+    constexpr int NLD = (EARLY && ST < PFS && K1 > K0) ? 2 * (K1 - K0) : 0;
+    if constexpr (NLD > 0) {
+      if (more) {
+#pragma unroll
+        for (int k = K0; k < K1; ++k) load_task(ch + 1, k);
+      }
+    }
+    const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+    tap_body(b, std::integral_constant<int, ST * TPS>{});
+    if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
+    if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
+    ++sidx;
+    if (!EARLY && ST == NS - 1 && more) {
+#pragma unroll
+      for (int k = 0; k < NTK; ++k) load_task(ch + 1, k);
+    }
+    // the next stage's weights must have landed (vector-memory loads complete in order: halo
+    // loads issued after them may still be in flight)
+    if (NLD > 0 && more)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    stage(ch, std::integral_constant<int, 0>{});
+    if constexpr (NS > 1) stage(ch, std::integral_constant<int, 1>{});
+    if constexpr (NS > 2) stage(ch, std::integral_constant<int, 2>{});
+    if constexpr (NS > 3) stage(ch, std::integral_constant<int, 3>{});
+    if constexpr (NS > 4) stage(ch, std::integral_constant<int, 4>{});
+    if constexpr (NS > 5) stage(ch, std::integral_constant<int, 5>{});
+    if constexpr (NS > 6) stage(ch, std::integral_constant<int, 6>{});
+    if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
+    if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+    if (ch + 1 < c_end) {   // every wave is past the chunk's last stage barrier: S is free
+      convert(ch + 1);
+      __syncthreads();
+    }
+  }
+  float colscale[TJ];
+  const float ia = exp2i(-ea);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn0 + j * 32 + lr;
+    const int we = col < p.Cout ? h.wexp[col] : 0;
+    const int e = ea + we;
+    if (e > 126 || e < -126) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= ia;
+      colscale[j] = exp2i(-we);
+    } else {
+      colscale[j] = exp2i(-e);
+    }
+    if (col >= p.Cout) colscale[j] = 0.f;
+  }
+  // S is free now: reduction scratch [2][WM * TI][BN] floats, then 2 KiB per wave of store stage
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
+                                 h.wide ? smem + 2 * WM * TI * BN : nullptr, colscale);
+}
+
 // ------------------- weight gradient h3: scaled 2-way fp16 split, 3 MFMA products -------------------
 // Same tiling and staging as conv_wgrad_x6 (conv.hip): dW tile [BM couts][BN k-columns] over a
 // pixel chunk (split-K), 16 pixels per stage, register-staged pixel rows split into hi / lo
@@ -1069,6 +1392,62 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   return 0;
 }
 
+// h3r (register-staged halo, two workgroups per CU): LDS = S + two weight stages + the zero row
+constexpr int H3R_NTK = 6;   // halo tasks per thread: arows <= 6 * 256 / 4 = 384
+static size_t h3r_lds(int bn, int arows, int tps) { return 128 + (size_t)arows * 128 + (size_t)2 * tps * 2 * bn * 64; }
+static int h3r_tps(int bn) { return bn >= 64 ? 2 : 3; }
+static std::atomic<int> g_h3r{-1};
+static bool h3r_on() {
+  int v = g_h3r.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("SRPDE_H3R");   // tuning/diagnostics: 0 = the 8-wave kernel for every shape
+    v = (!e || atoi(e) != 0) ? 1 : 0;
+    int expect = -1;
+    g_h3r.compare_exchange_strong(expect, v);
+    v = g_h3r.load(std::memory_order_relaxed);
+  }
+  return v != 0;
+}
+// the h3r kernel takes this shape: an output tile of <= 64 channels, a halo tile that fits the
+// registers, and two workgroups' LDS per CU
+static bool h3r_fits(int bn, int arows) {
+  return h3r_on() && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
+}
+
+template <int BN, int TPS>
+static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
+  constexpr int BM = 256, WM = 4, SRB = 128;
+  const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
+  const int T = nbm * nbn;
+  const size_t lds = h3r_lds(BN, h.arows, TPS);
+  if ((size_t)h.arows * 128 < (size_t)(2 * WM * 2 * BN + WM * 512) * 4) h.wide = 0;   // S too small to stage
+  static int slots = [&] {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, cus) * 2;   // resident workgroups: two per CU
+  }();
+  plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  const int nch = p.Cin / BK2;
+  if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
+  if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
+  const int grid = T - p.ntail + p.ntail * p.tsplit;
+  static const bool early = [] {
+    const char* e = getenv("SRPDE_H3R_EARLY");   // tuning: 1 = prefetch the next halo tile during the chunk
+    return e && atoi(e) != 0;
+  }();
+  if (early)
+    hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, true>), dim3(grid), dim3(256), lds, st, p, h);
+  else
+    hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, false>), dim3(grid), dim3(256), lds, st, p, h);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
+  if (p.ntail > 0) {
+    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
+    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r tail fixup)");
+  }
+  return 0;
+}
+
 int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigned* amax0, const unsigned* amax1,
                     hipStream_t st) {
   const H3W sc{amax_dy, amax0, p.c1 ? amax1 : amax0};
@@ -1188,6 +1567,12 @@ int srpde_conv_h3_set_half(int max_chunks) {
   return prev;
 }
 
+int srpde_conv_h3r_set(int on) {
+  const int prev = h3r_on() ? 1 : 0;
+  g_h3r.store(on ? 1 : 0);
+  return prev;
+}
+
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
   // cout % 16: a 16-channel output (out_conv2) runs on the 32-column tile with the weight rows past
   // Cout zero-filled by the DMA range check
@@ -1289,8 +1674,12 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
       default: return launch_fwd_h3<128, 32, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
     }
   }
+  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
+    if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 2>(p, a, stream, workspace, ws_bytes);
+    return launch_fwd_h3r<32, 3>(p, a, stream, workspace, ws_bytes);
+  }
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
-#define H3_LAUNCH(BN_)                                                                         \
+#define H3_LAUNCH(BN_)                                                                        \
   (tps >= 3 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 3>(p, a, stream, workspace, ws_bytes) \
    : tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
               : launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes))

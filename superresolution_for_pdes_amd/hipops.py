@@ -110,6 +110,12 @@ def set_h3_half(max_chunks: int) -> int:
     return int(query("srpde_conv_h3_set_half", int(max_chunks)))
 
 
+def set_h3r(on: bool) -> bool:
+    """h3 kernel choice for output tiles of <= 64 channels: the register-staged 4-wave kernel
+    (two workgroups per CU) or the 8-wave one.  Returns the previous choice."""
+    return bool(query("srpde_conv_h3r_set", int(bool(on))))
+
+
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
     return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, ksize))
 

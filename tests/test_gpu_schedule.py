@@ -162,3 +162,61 @@ def test_conv_h3_half_tiles_equal_full_tiles(n, c0, c1, cout, hw, dil):
         H.set_h3_half(prev)
     for k, (a, b_) in enumerate(zip(*outs)):
         assert torch.equal(a, b_), k
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (5, 128, 64, 64, 40, 1), (3, 64, 0, 32, 40, 1),
+                                                 (4, 32, 0, 16, 40, 1), (6, 128, 0, 64, 20, 1), (2, 64, 0, 64, 10, 2)])
+def test_conv_h3r_equals_8wave(n, c0, c1, cout, hw, dil):
+    """The register-staged 4-wave h3 kernel (two workgroups per CU) against the 8-wave kernel:
+    forward (bias, BN statistics, stored input split, fused input BN + ReLU) and dgrad (stored
+    dy split, fused BN-backward partials, per-tile max|dx|) in equal bits -- same products, same
+    accumulation order, statistics combined per 32-row block in row order (no K-split tail at
+    these sizes)."""
+    from superresolution_for_pdes_amd import hipops as H
+    cin = c0 + c1
+    if H.conv_math() != "h3" or not H.h3_capable(c0, c1, cout, hw, dil):
+        pytest.skip("not an h3 shape")
+    back = H.h3_capable(cout, 0, cin, hw, dil)   # out_conv2's 16-channel dy: forward only
+    g = torch.Generator(device=DEV).manual_seed(5)
+    P = n * hw * hw
+    x = torch.randn(P, cin, device=DEV, generator=g)
+    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, wd = H.pack_conv_weights(w, cin, True, back)
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    by = torch.randn(P, cin, device=DEV, generator=g)        # the BN input below the dgrad's output
+    bmean, binv = torch.randn(cin, device=DEV, generator=g) * 0.1, torch.rand(cin, device=DEV, generator=g) + 0.5
+    bga, bbe = torch.randn(cin, device=DEV, generator=g), torch.randn(cin, device=DEV, generator=g) * 0.1
+    for t in (x0, x1, dy):
+        if t is not None:
+            t._srpde_amax = H.amax_of(t)
+    aff = None
+    if c1 == 0:   # fused input BN + ReLU (the second conv of a ConvBlock)
+        sc = torch.rand(c0, device=DEV, generator=g) + 0.5
+        sh = torch.randn(c0, device=DEV, generator=g) * 0.2
+        aff = (sc, sh)
+    outs = []
+    prev = H.set_h3r(True)
+    try:
+        for on in (False, True):
+            H.set_h3r(on)
+            y = torch.empty(P, cout, device=DEV)
+            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
+            xp = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp, in_affine=aff)
+            dx = dyp = part = dmax = torch.zeros(1, device=DEV)
+            if back:
+                dx = torch.empty(P, cin, device=DEV)
+                dyp = H.split_planes_buffer(P, cout, DEV)
+                part = H.bn_bwd_partials(n, hw, hw, cin, DEV)
+                dmax = H.out_max_slots(n, hw, hw, cout, cin, dil, DEV)
+                H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp,
+                           bn_bwd=(by, bmean, binv, bga, bbe, part), out_max=dmax)
+            torch.cuda.synchronize()
+            outs.append((y, stats, xp, dx, dyp, part, dmax))
+    finally:
+        H.set_h3r(prev)
+    names = ("y", "stats", "xsplit", "dx", "dysplit", "bn_part", "dx_max")
+    for name, a, b_ in zip(names, *outs):
+        assert torch.equal(a, b_), name
