@@ -449,10 +449,13 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
 // as much as the MFMAs, and with one 8-wave workgroup per CU (conv_fwd_h3_kernel: fp32 halo tile
 // F + its split S + weight stages = 120 KiB of LDS) every wave of the CU reaches those phases at
 // the same barriers and the MFMA pipes idle through them.  Here the next chunk's halo tile is
-// loaded into VGPRs (buffer_load_dwordx4, issued in slices behind the weight DMAs of the first
-// stages) instead of into an fp32 LDS tile, and split from registers into S after the chunk:
-// no F, so a workgroup needs S + two weight stages (<= 77 KiB) and two workgroups share a CU --
-// one's setup / split / epilogue runs under the other's MFMAs.  A workgroup is 4 waves stacked
+// loaded into VGPRs (buffer_load_dwordx4, issued after the chunk's last fragment reads, so the
+// prefetch registers never live together with the fragments) instead of into an fp32 LDS tile,
+// and split from registers into S after the chunk: no F, so a workgroup needs S + a ring of NB
+// weight stages (<= 78 KiB) and two workgroups share a CU -- one's setup / split / epilogue and
+// halo-load latency run under the other's MFMAs.  The weight ring is fed NB - 1 stages ahead,
+// across chunk boundaries (a one-stage lead does not cover an L2 round trip under load: one tap
+// is 24 MFMAs per wave).  A workgroup is 4 waves stacked
 // along M, each 64 rows x BN columns (8 fragment reads per 12 MFMAs at BN = 64, against 6 per 6
 // in the 8-wave 32-row layout).  Same arithmetic (the same split, product order and two-level
 // accumulation per chunk) and the same epilogue, statistics blocks and output as the 8-wave kernel.
@@ -460,7 +463,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ f32x4 llvm_raw_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
                                          int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
-template <int BN, int TPS, int NTK, bool EARLY>
+template <int BN, int TPS, int NTK, int NB>
 __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Args h) {
   constexpr int BM = 256, WM = 4, WN = 1, NW = 4, NT = 256, SRB = 128;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -470,17 +473,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   constexpr int B_TAP = 2 * BP_BYTES;
   constexpr int B_STAGE = TPS * B_TAP;
   constexpr int NS = (9 + TPS - 1) / TPS;
-  constexpr int PFS = NS - 1 < 3 ? NS - 1 : 3;      // EARLY: stages that issue halo loads for the next chunk
-  constexpr int TPST = (NTK + PFS - 1) / PFS;       // halo tasks per such stage (2 loads each)
+  constexpr int DPS = TPS * BPW;           // weight DMAs per wave per stage (spares into the sink: exact counts)
+  static_assert(NB >= 2 && NB <= NS + 1, "weight ring");
   // LDS: 128 zero bytes (the padding row) | S (arows 128-B rows: hi / lo fp16 pieces of 32
-  // channels, slot swz(r, k)) | two weight stages.  Every A-fragment offset is below 64 KiB, so
-  // the per-tap offsets of a lane's two row blocks share one VGPR.
+  // channels, slot swz(r, k)) | NB weight stages | 1 KiB DMA sink.  Every A-fragment offset is
+  // below 64 KiB, so the per-tap offsets of a lane's two row blocks share one VGPR.
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int arows = h.arows;
   char* const zrow = lds;
   char* const sbuf = lds + 128;
   char* const bbuf0 = sbuf + arows * 128;
+  char* const sink = bbuf0 + NB * B_STAGE;
   constexpr int zoff = 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -574,21 +578,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     pf[k][0] = llvm_raw_buffer_load_f4(rs, (int)off, 0, 0);
     pf[k][1] = llvm_raw_buffer_load_f4(rs, (int)(off + 16u), 0, 0);
   };
+  // the TPS taps of stage `st` of chunk `ch` into ring slot `buf`; exactly DPS DMAs per wave
+  // (missing taps / rows, or ch < 0 = past the last stage: zero fills into the sink)
   auto issue_b = [&](int ch, int st, int buf) {
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
       const int tap = st * TPS + u;
-      if (tap < 9) {
-        const int k0 = tap * p.Cin + ch * BK2;
-        char* bbase = bbuf0 + buf * B_STAGE + u * B_TAP;
+      const int k0 = tap * p.Cin + ch * BK2;
+      char* bbase = bbuf0 + buf * B_STAGE + u * B_TAP;
 #pragma unroll
-        for (int j = 0; j < BPW; ++j) {
-          const int q = wave + j * NW;
-          if (q < BTOT) {
-            const unsigned off = b_off[j] >= 0 ? (unsigned)(b_off[j] + k0 * 2) : OOB;
-            dma16(rsw, off, lds_addr_of(bbase + q * 1024));
-          }
-        }
+      for (int j = 0; j < BPW; ++j) {
+        const int q = wave + j * NW;
+        const bool real = ch >= 0 && tap < 9 && q < BTOT;
+        const unsigned off = (real && b_off[j] >= 0) ? (unsigned)(b_off[j] + k0 * 2) : OOB;
+        dma16(rsw, off, lds_addr_of(real ? bbase + q * 1024 : sink));
       }
     }
   };
@@ -641,15 +644,19 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // prologue: the first chunk's halo tile + first weight stage
+  // prologue: the first chunk's halo tile + the first NB - 1 weight stages
 #pragma unroll
   for (int k = 0; k < NTK; ++k) load_task(c_beg, k);
-  issue_b(c_beg, 0, 0);
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s) {
+    const int c = c_beg + s / NS;
+    issue_b(c < c_end ? c : -1, s % NS, s);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   convert(c_beg);
   __syncthreads();
 
-  int sidx = 0;
+  int cur = 0;   // ring slot of the current stage
   auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
     constexpr int NG = BK2 / 16;
@@ -692,35 +699,29 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   auto stage = [&](int ch, auto st_tag) {
     constexpr int ST = decltype(st_tag)::value;
     const bool more = ch + 1 < c_end;
-    if (ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
-    else if (more) issue_b(ch + 1, 0, (sidx + 1) & 1);
-    // EARLY: the next chunk's halo tile is loaded in slices behind the weight DMAs of stages
-    // 0..PFS-1 (its latency hidden by the chunk's MFMAs); otherwise after the chunk's last fragment
-    // reads (the prefetch registers never live together with the fragments; the other workgroup
-    // on the CU runs its MFMAs through the load latency)
-    constexpr int K0 = ST * TPST, K1 = (ST + 1) * TPST < NTK ? (ST + 1) * TPST : NTK;
-    constexpr int NLD = (EARLY && ST < PFS && K1 > K0) ? 2 * (K1 - K0) : 0;
-    if constexpr (NLD > 0) {
-      if (more) {
-#pragma unroll
-        for (int k = K0; k < K1; ++k) load_task(ch + 1, k);
-      }
+    {   // the ring slot the previous stage read (every wave is past its barrier) gets stage + NB - 1
+      constexpr int TGT = ST + NB - 1;
+      const int c = ch + TGT / NS;
+      issue_b(c < c_end ? c : -1, TGT % NS, cur == 0 ? NB - 1 : cur - 1);
     }
-    const char* b = bbuf0 + (sidx & 1) * B_STAGE;
+    const char* b = bbuf0 + cur * B_STAGE;
     tap_body(b, std::integral_constant<int, ST * TPS>{});
     if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
     if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
-    ++sidx;
-    if (!EARLY && ST == NS - 1 && more) {
+    cur = cur == NB - 1 ? 0 : cur + 1;
+    if (ST == NS - 1) {
+      // the next chunk's halo tile, after the chunk's last fragment reads; the split after the
+      // chunk needs it (and every weight stage issued so far) landed
+      if (more) {
 #pragma unroll
-      for (int k = 0; k < NTK; ++k) load_task(ch + 1, k);
-    }
-    // the next stage's weights must have landed (vector-memory loads complete in order: halo
-    // loads issued after them may still be in flight)
-    if (NLD > 0 && more)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
-    else
+        for (int k = 0; k < NTK; ++k) load_task(ch + 1, k);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      // the next stage's weights must have landed; the NB - 2 stages issued after them may still
+      // be in flight (vector-memory loads complete in order)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPS) : "memory");
+    }
     __syncthreads();
   };
   for (int ch = c_beg; ch < c_end; ++ch) {
@@ -1258,9 +1259,11 @@ __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __re
 // H3W_DESC per layer): w, cout, cin_real, cin_pad, planes_f, exp_f, planes_d, exp_d, row_begin
 // (rows of a layer: Cout forward rows then Cin_pad dgrad rows; planes_f / planes_d may be 0).
 constexpr int H3W_DESC = 9;
+constexpr int H3W_TMAX = 512;   // dgrad rows of layers with cout <= this stage their source through LDS
 
 __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long* __restrict__ desc, int nlayers,
                                                                  int total_rows) {
+  __shared__ float T[H3W_TMAX * 37];   // a block's 4 rows' sources (the staged paths below)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= total_rows) return;
@@ -1274,10 +1277,82 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
   if (!fwd) r -= cout;
   _Float16* planes = reinterpret_cast<_Float16*>(fwd ? d[4] : d[6]);
   int* wexp = reinterpret_cast<int*>(fwd ? d[5] : d[7]);
-  if (planes == nullptr) return;
+  if (planes == nullptr) return;   // uniform over the block: its 4 rows are of one layer and kind
   const int inner = fwd ? cin_pad : cout;          // k = tap * inner + i
   const int K = 9 * inner;
   const int rows = fwd ? cout : cin_pad;
+  if (fwd && 4 * cin_real * 9 <= H3W_TMAX * 37 && cin_pad % 8 == 0) {
+    // forward rows n0..n0+3: their sources are 4 * cin_real * 9 contiguous floats, staged once
+    const int n0 = r - (threadIdx.x >> 6), span = cin_real * 9;
+    const float* src = w + (size_t)n0 * span;
+    for (int e = threadIdx.x; e < 4 * span; e += 256) T[e] = src[e];
+    __syncthreads();
+    const float* t = T + (threadIdx.x >> 6) * span;
+    auto v = [&](int k) {
+      const int tap = k / cin_pad, c = k - tap * cin_pad;
+      return c < cin_real ? t[c * 9 + tap] : 0.f;
+    };
+    float m = 0.f;
+    for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(v(k)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const int e = h3_exp(__float_as_uint(m));
+    const float sc = exp2i(e);
+    _Float16* hi = planes + (size_t)r * K;
+    _Float16* lo = planes + (size_t)rows * K + (size_t)r * K;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k of one tap per lane
+      half8 hv, lv;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float x = v(k0 + i) * sc;
+        const _Float16 h = (_Float16)x;
+        hv[i] = h;
+        lv[i] = (_Float16)(x - (float)h);
+      }
+      *reinterpret_cast<half8*>(hi + k0) = hv;
+      *reinterpret_cast<half8*>(lo + k0) = lv;
+    }
+    if (lane == 0) wexp[r] = e;
+    return;
+  }
+  if (!fwd && cout <= H3W_TMAX) {
+    // dgrad rows c0..c0+3 of this block: the source W[n][c0..c0+3][0..8] is 36 contiguous floats
+    // per n -- staged through LDS once by the block, so HBM / L2 reads are row-contiguous (a wave
+    // walking k = tap * cout + n directly reads one scattered 4-B word per cache line, 18 times)
+    const int c0 = r - (threadIdx.x >> 6);
+    for (int e = threadIdx.x; e < cout * 36; e += 256) {
+      const int n = e / 36, q = e - n * 36;
+      T[n * 37 + q] = c0 + q / 9 < cin_real ? w[((size_t)n * cin_real + c0) * 9 + q] : 0.f;
+    }
+    __syncthreads();
+    const int cq = (threadIdx.x >> 6) * 9;   // this wave's row within the staged columns
+    float m = 0.f;
+    for (int k = lane; k < K; k += 64) {
+      const int tap = k / cout, n = k - tap * cout;
+      m = fmaxf(m, fabsf(T[n * 37 + cq + tap]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const int e = h3_exp(__float_as_uint(m));
+    const float sc = exp2i(e);
+    _Float16* hi = planes + (size_t)r * K;
+    _Float16* lo = planes + (size_t)rows * K + (size_t)r * K;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k (same tap: cout % 8 == 0) per lane
+      const int tap = k0 / cout, n = k0 - tap * cout;
+      half8 hv, lv;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float v = T[(n + i) * 37 + cq + tap] * sc;
+        const _Float16 h = (_Float16)v;
+        hv[i] = h;
+        lv[i] = (_Float16)(v - (float)h);
+      }
+      *reinterpret_cast<half8*>(hi + k0) = hv;
+      *reinterpret_cast<half8*>(lo + k0) = lv;
+    }
+    if (lane == 0) wexp[r] = e;
+    return;
+  }
   auto val = [&](int k) -> float {
     const int tap = k / inner, i = k - tap * inner;
     const int n = fwd ? r : i, c = fwd ? i : r;
@@ -1394,8 +1469,11 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
 
 // h3r (register-staged halo, two workgroups per CU): LDS = S + two weight stages + the zero row
 constexpr int H3R_NTK = 6;   // halo tasks per thread: arows <= 6 * 256 / 4 = 384
-static size_t h3r_lds(int bn, int arows, int tps) { return 128 + (size_t)arows * 128 + (size_t)2 * tps * 2 * bn * 64; }
-static int h3r_tps(int bn) { return bn >= 64 ? 2 : 3; }
+constexpr int H3R_NB = 4;    // weight ring depth (stages of one tap)
+static size_t h3r_lds(int bn, int arows, int tps) {
+  return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024;
+}
+static int h3r_tps(int bn) { (void)bn; return 1; }
 static std::atomic<int> g_h3r{-1};
 static bool h3r_on() {
   int v = g_h3r.load(std::memory_order_relaxed);
@@ -1432,14 +1510,7 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  static const bool early = [] {
-    const char* e = getenv("SRPDE_H3R_EARLY");   // tuning: 1 = prefetch the next halo tile during the chunk
-    return e && atoi(e) != 0;
-  }();
-  if (early)
-    hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, true>), dim3(grid), dim3(256), lds, st, p, h);
-  else
-    hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, false>), dim3(grid), dim3(256), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -1675,8 +1746,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
     }
   }
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
-    if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 2>(p, a, stream, workspace, ws_bytes);
-    return launch_fwd_h3r<32, 3>(p, a, stream, workspace, ws_bytes);
+    if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
+    return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);
   }
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_)                                                                        \
