@@ -601,6 +601,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   auto convert = [&](int ch) {
     int t = tid;
     asm volatile("" : "+v"(t));   // as in load_task
+    // fused BN + ReLU of the producer: every task of a thread has the same 8 channels (t & 3),
+    // so their (scale, shift) are loaded once per chunk, not once per task
+    float4 s0, s1, t0, t1;
+    if (h.in_scale != nullptr) {
+      const int cc = ch * BK2 + (t & 3) * 8;
+      s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
+      s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
+      t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
+      t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
+    }
 #pragma unroll
     for (int k = 0; k < NTK; ++k) {
       const int sg = t + NT * k;
@@ -608,14 +618,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
         const int r = sg >> 2, c8 = sg & 3;
         float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
         float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
-        if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
-          const int cc = ch * BK2 + c8 * 8, pix = pix0 + r;
+        if (h.in_scale != nullptr) {   // rows outside the tensor stay 0
+          const int pix = pix0 + r;
           const bool inside = pix >= 0 && pix < p.P;
-          const float4 s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
-          const float4 s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
-          const float4 t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
-          const float4 t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
-#define AFF(V, S, T, X) V.X = inside ? fmaxf(V.X * S.X + T.X, 0.f) : 0.f;
+#define AFF(V, S, T, X) V.X = inside ? fmaxf(__builtin_fmaf(V.X, S.X, T.X), 0.f) : 0.f;
           AFF(v0, s0, t0, x) AFF(v0, s0, t0, y) AFF(v0, s0, t0, z) AFF(v0, s0, t0, w)
           AFF(v1, s1, t1, x) AFF(v1, s1, t1, y) AFF(v1, s1, t1, z) AFF(v1, s1, t1, w)
 #undef AFF
