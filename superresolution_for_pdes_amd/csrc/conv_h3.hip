@@ -463,7 +463,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ f32x4 llvm_raw_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
                                          int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
-template <int BN, int TPS, int NTK, int NB>
+// BNB = true: the dgrad with the BatchNorm (+ReLU) backward apply fused into the operand transform
+// (as conv_fwd_h3_kernel<..., BNB>): x0 is da (halo tile in registers), and the halo tile of the
+// BN input y is DMA'd as fp32 into S itself once S is free; the split forms dy = gamma*invstd*(dz -
+// m1 - xhat*m2) per element and overwrites its row of S in place (a row's four tasks are four lanes
+// of one wave instruction, so every read of the row precedes every write).
+template <int BN, int TPS, int NTK, int NB, bool BNB = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Args h) {
   constexpr int BM = 256, WM = 4, WN = 1, NW = 4, NT = 256, SRB = 128;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -485,6 +490,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   char* const sbuf = lds + 128;
   char* const bbuf0 = sbuf + arows * 128;
   char* const sink = bbuf0 + NB * B_STAGE;
+  float* const bnbt = reinterpret_cast<float*>(sink + 1024);   // BNB: [6][32] coefficients of the chunk
   constexpr int zoff = 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -511,6 +517,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const size_t plane = (size_t)p.Cout * p.K;
   const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
+  const int32x4 rsy = BNB ? make_rsrc(h.bnb_y, (unsigned)((size_t)p.P * h.bnb_ldy * 4)) : rs0;
   const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
 
   unsigned ab = h.amax0 ? *h.amax0 : 0u;
@@ -578,6 +585,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     pf[k][0] = llvm_raw_buffer_load_f4(rs, (int)off, 0, 0);
     pf[k][1] = llvm_raw_buffer_load_f4(rs, (int)(off + 16u), 0, 0);
   };
+  // BNB: the y halo tile of chunk `ch` into S (fp32, 16-B chunk k of row r at slot swz(r, k))
+  auto issue_y = [&](int ch) {
+    const int cb = ch * BK2;
+    for (int q = wave; q < arows / 8; q += NW) {
+      const int r = q * 8 + (lane >> 3);
+      const int pix = pix0 + r;
+      const unsigned off = (pix >= 0 && pix < p.P) ? (unsigned)((pix * h.bnb_ldy + cb + swz(r, lane & 7) * 4) * 4) : OOB;
+      dma16(rsy, off, lds_addr_of(sbuf + q * 1024));
+    }
+  };
   // the TPS taps of stage `st` of chunk `ch` into ring slot `buf`; exactly DPS DMAs per wave
   // (missing taps / rows, or ch < 0 = past the last stage: zero fills into the sink)
   auto issue_b = [&](int ch, int st, int buf) {
@@ -611,6 +628,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
       t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
     }
+    if constexpr (BNB) {   // the chunk's per-channel BN-backward terms -> an LDS table (read per task:
+                           // 48 coefficient registers held across the tasks would not fit)
+      if (t < 6 * BK2) {
+        const int q = t / BK2, c = ch * BK2 + t % BK2;
+        const float* src = q == 0 ? h.bnb_mean : q == 1 ? h.bnb_invstd : q == 2 ? h.bnb_gamma
+                         : q == 3 ? h.bnb_beta : q == 4 ? h.bnb_m1 : h.bnb_m2;
+        bnbt[t] = src[c];
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < NTK; ++k) {
       const int sg = t + NT * k;
@@ -618,6 +645,36 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
         const int r = sg >> 2, c8 = sg & 3;
         float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
         float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
+        if constexpr (BNB) {   // fused BN (+ReLU) backward: da and y -> dy; rows outside the tensor stay 0
+          const bool inside = pix0 + r >= 0 && pix0 + r < p.P;
+          const float4 y0 = *reinterpret_cast<const float4*>(sbuf + r * 128 + swz(r, 2 * c8) * 16);
+          const float4 y1 = *reinterpret_cast<const float4*>(sbuf + r * 128 + swz(r, 2 * c8 + 1) * 16);
+          const float yy8[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+          float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+          for (int hq = 0; hq < 2; ++hq) {   // four channels' coefficients at a time (registers)
+            int to = c8 * 8 + hq * 4;
+            asm volatile("" : "+v"(to));   // re-read per task and half (not hoisted into live registers)
+            const float4 mu = *reinterpret_cast<const float4*>(bnbt + 0 * BK2 + to);
+            const float4 is = *reinterpret_cast<const float4*>(bnbt + 1 * BK2 + to);
+            const float4 ga = *reinterpret_cast<const float4*>(bnbt + 2 * BK2 + to);
+            const float4 be = *reinterpret_cast<const float4*>(bnbt + 3 * BK2 + to);
+            const float4 m1 = *reinterpret_cast<const float4*>(bnbt + 4 * BK2 + to);
+            const float4 m2 = *reinterpret_cast<const float4*>(bnbt + 5 * BK2 + to);
+            const float cm[6][4] = {{mu.x, mu.y, mu.z, mu.w}, {is.x, is.y, is.z, is.w}, {ga.x, ga.y, ga.z, ga.w},
+                                    {be.x, be.y, be.z, be.w}, {m1.x, m1.y, m1.z, m1.w}, {m2.x, m2.y, m2.z, m2.w}};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              // the same expressions as bn_bwd_apply_kernel (bn.hip) and conv_fwd_h3_kernel<..., BNB>
+              const int e = hq * 4 + q;
+              const float xh = (yy8[e] - cm[0][q]) * cm[1][q];
+              const float dz = (!h.bnb_relu || xh * cm[2][q] + cm[3][q] > 0.f) ? vv[e] : 0.f;
+              vv[e] = inside ? (dz - cm[4][q] - xh * cm[5][q]) * (cm[2][q] * cm[1][q]) : 0.f;
+            }
+          }
+          v0 = make_float4(vv[0], vv[1], vv[2], vv[3]);
+          v1 = make_float4(vv[4], vv[5], vv[6], vv[7]);
+        }
         if (h.in_scale != nullptr) {   // rows outside the tensor stay 0
           const int pix = pix0 + r;
           const bool inside = pix >= 0 && pix < p.P;
@@ -639,20 +696,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
           }
         }
       }
+      if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);   // one task's 48 coefficients live at a time
     }
   };
 
   floatx16 acc[TI][TJ], part[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // prologue: the first chunk's halo tile + the first NB - 1 weight stages
 #pragma unroll
   for (int k = 0; k < NTK; ++k) load_task(c_beg, k);
+  if constexpr (BNB) issue_y(c_beg);
 #pragma unroll
   for (int s = 0; s < NB - 1; ++s) {
     const int c = c_beg + s / NS;
@@ -661,6 +714,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   convert(c_beg);
   __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   int cur = 0;   // ring slot of the current stage
   auto tap_body = [&](const char* b, auto tap_tag) {
@@ -711,11 +770,19 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       issue_b(c < c_end ? c : -1, TGT % NS, cur == 0 ? NB - 1 : cur - 1);
     }
     const char* b = bbuf0 + cur * B_STAGE;
-    tap_body(b, std::integral_constant<int, ST * TPS>{});
-    if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
-    if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
+    if (!(p.dbg & 128)) {   // diagnostics (SRPDE_CONV_DBG, results wrong): 128 = no MFMA work
+      tap_body(b, std::integral_constant<int, ST * TPS>{});
+      if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
+      if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
+    }
     cur = cur == NB - 1 ? 0 : cur + 1;
     if (ST == NS - 1) {
+      // two-level accumulation: the chunk's partial chain folds into the accumulator here, so it
+      // is dead before the prefetch registers come alive
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
       // the next chunk's halo tile, after the chunk's last fragment reads; the split after the
       // chunk needs it (and every weight stage issued so far) landed
       if (more) {
@@ -740,12 +807,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     if constexpr (NS > 6) stage(ch, std::integral_constant<int, 6>{});
     if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
     if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
     if (ch + 1 < c_end) {   // every wave is past the chunk's last stage barrier: S is free
-      convert(ch + 1);
+      if constexpr (BNB) {
+        issue_y(ch + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      if (!(p.dbg & 4)) convert(ch + 1);   // diagnostics: 4 = no per-chunk split
       __syncthreads();
     }
   }
@@ -766,6 +834,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       colscale[j] = exp2i(-e);
     }
     if (col >= p.Cout) colscale[j] = 0.f;
+  }
+  if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] * colscale[j] + acc[i][j][15];
+    if (t == 123.f) p.y[tid] = t;
+    return;
   }
   // S is free now: reduction scratch [2][WM * TI][BN] floats, then 2 KiB per wave of store stage
   x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
@@ -1476,8 +1553,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
 // h3r (register-staged halo, two workgroups per CU): LDS = S + two weight stages + the zero row
 constexpr int H3R_NTK = 6;   // halo tasks per thread: arows <= 6 * 256 / 4 = 384
 constexpr int H3R_NB = 4;    // weight ring depth (stages of one tap)
-static size_t h3r_lds(int bn, int arows, int tps) {
-  return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024;
+static size_t h3r_lds(int bn, int arows, int tps) {   // zero row | S | weight ring | DMA sink | BNB table
+  return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024 + 1024;
 }
 static int h3r_tps(int bn) { (void)bn; return 1; }
 static std::atomic<int> g_h3r{-1};
@@ -1498,7 +1575,7 @@ static bool h3r_fits(int bn, int arows) {
   return h3r_on() && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
 }
 
-template <int BN, int TPS>
+template <int BN, int TPS, bool BNB = false>
 static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int BM = 256, WM = 4, SRB = 128;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
@@ -1512,11 +1589,13 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
     return std::max(1, cus) * 2;   // resident workgroups: two per CU
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
+  static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
+  p.dbg = dbg;   // diagnostics only (timing experiments; results wrong when non-zero)
   const int nch = p.Cin / BK2;
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB>), dim3(grid), dim3(256), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB, BNB>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
   if (p.ntail > 0) {
     hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
@@ -1825,6 +1904,17 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
   // one tap per stage: the second fp32 halo tile takes the second weight stage's LDS.  (The
   // 128-column tile does not fit its registers with the fused transform -- 46 VGPRs of scratch --
   // so outputs with a multiple of 128 channels keep srpde_bn_relu_bwd + srpde_conv_fwd_h3.)
+  // the register-staged kernel for the BNB dgrads: measured slower in the step (34.41 / 34.54 vs
+  // 34.05 / 34.10 ms same box) -- the 64-column instantiation spills (140 B) around its halo loads,
+  // which the compiler then serialises -- so off unless SRPDE_H3R_BNB=1 (bit-equal either way)
+  static const int bnb_r = [] {
+    const char* e = getenv("SRPDE_H3R_BNB");
+    return e ? atoi(e) : 0;
+  }();
+  if (bnb_r && h3r_fits(h3_bn(h3_cfg(cin_dx)), a.arows)) {
+    if (h3_cfg(cin_dx) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
+    return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
+  }
   if (h3_cfg(cin_dx) == 2) return launch_fwd_h3<256, 64, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
   return launch_fwd_h3<256, 32, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
 }

@@ -296,7 +296,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
     dyp = None
     out_part = None
     if (_FUSE_BN_APPLY and train and dx is not None and xp is not None and not dx_accumulate
-            and cin <= 64 and cout >= 64 and H.bnb_capable(cout, cin, w, dil)):
+            and cin <= _BNB_MAX_CIN and cout >= _BNB_MIN_COUT and H.bnb_capable(cout, cin, w, dil)):
         m1, m2, dyw = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
                                        grads[conv.bias], part=part_t, da_max=da_max)
         wd = _dgrad_weights(conv, cin, w, dil)
@@ -351,6 +351,10 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
 # the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
 # (srpde_conv_dgrad_h3_bnb; SRPDE_FUSE_BN_APPLY=0: off)
 _FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
+# layers it is taken for: dgrad output channels <= _BNB_MAX_CIN, dy channels >= _BNB_MIN_COUT
+# (SRPDE_BNB_WIDE=1: also dec1.conv1's 3-tile dgrad and out_conv1's one-chunk dy)
+_BNB_WIDE = os.environ.get("SRPDE_BNB_WIDE", "0") == "1"
+_BNB_MAX_CIN, _BNB_MIN_COUT = (192, 32) if _BNB_WIDE else (64, 64)
 
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)

@@ -6,6 +6,8 @@ or changing which workgroup computes which tile (the persistent walk of the h3 c
 srpde_conv_h3_set_persistent) must not change a single bit.  Anything else is a race or a
 wrong tile, which a tolerance-based parity test could hide.
 """
+import os
+
 import pytest
 import torch
 
@@ -219,4 +221,47 @@ def test_conv_h3r_equals_8wave(n, c0, c1, cout, hw, dil):
         H.set_h3r(prev)
     names = ("y", "stats", "xsplit", "dx", "dysplit", "bn_part", "dx_max")
     for name, a, b_ in zip(names, *outs):
+        assert torch.equal(a, b_), name
+
+
+@pytest.mark.parametrize("n,cout_dy,cin_dx,hw", [(4, 64, 64, 40), (3, 32, 64, 40), (2, 64, 192, 40), (6, 128, 64, 20)])
+def test_conv_dgrad_bnb_h3r_equals_8wave(n, cout_dy, cin_dx, hw):
+    """The fused BN-backward dgrad (srpde_conv_dgrad_h3_bnb) on the register-staged kernel (y halo
+    DMA'd into S and transformed in place) against the 8-wave kernel: dx, dy's stored split, the
+    next BN's partials and per-tile max|dx| in equal bits (same expressions, same order)."""
+    from superresolution_for_pdes_amd import hipops as H
+    if H.conv_math() != "h3" or not H.bnb_capable(cout_dy, cin_dx, hw, 1):
+        pytest.skip("not a BNB shape")
+    g = torch.Generator(device=DEV).manual_seed(9)
+    P = n * hw * hw
+    da = torch.randn(P, cout_dy, device=DEV, generator=g)
+    y = torch.randn(P, cout_dy, device=DEV, generator=g) * 2 + 0.3
+    mean, invstd = y.mean(0), y.var(0, unbiased=False).add(1e-5).rsqrt()
+    gamma = torch.randn(cout_dy, device=DEV, generator=g)
+    beta = torch.randn(cout_dy, device=DEV, generator=g) * 0.1
+    dg, db, dbias = (torch.empty(cout_dy, device=DEV) for _ in range(3))
+    m1, m2, word = H.bn_bwd_prepare(y, da, mean, invstd, gamma, beta, dg, db, dbias)
+    w = torch.randn(cout_dy, cin_dx, 3, 3, device=DEV, generator=g) * 0.05
+    wd = H.pack_conv_weights(w, cin_dx, False, True)[1]
+    by = torch.randn(P, cin_dx, device=DEV, generator=g)
+    bmean, binv = torch.randn(cin_dx, device=DEV, generator=g) * 0.1, torch.rand(cin_dx, device=DEV, generator=g) + 0.5
+    bga, bbe = torch.randn(cin_dx, device=DEV, generator=g), torch.randn(cin_dx, device=DEV, generator=g) * 0.1
+    if os.environ.get("SRPDE_H3R_BNB") != "1":
+        pytest.skip("the register-staged BNB dgrad is off (SRPDE_H3R_BNB=1 turns it on)")
+    outs = []
+    prev = H.set_h3r(True)
+    try:
+        for on in (False, True):
+            H.set_h3r(on)
+            dx = torch.empty(P, cin_dx, device=DEV)
+            dyp = H.split_planes_buffer(P, cout_dy, DEV)
+            part = H.bn_bwd_partials(n, hw, hw, cin_dx, DEV)
+            dmax = H.dx_max_slots(n, hw, hw, cin_dx, DEV)
+            H.conv_dgrad_bnb(da, y, mean, invstd, gamma, beta, m1, m2, word, wd, dx, n, hw, hw, cout_dy, cin_dx, 1,
+                             dyp, bn_bwd=(by, bmean, binv, bga, bbe, part), dx_max=dmax)
+            torch.cuda.synchronize()
+            outs.append((dx, dyp, part, dmax))
+    finally:
+        H.set_h3r(prev)
+    for name, a, b_ in zip(("dx", "dysplit", "bn_part", "dx_max"), *outs):
         assert torch.equal(a, b_), name
