@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--roofline-layer", default="bridge.3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02b.json"))
     ap.add_argument("--workload", choices=("train", "poisson", "cascade"), default="train",
                     help="train = the BASELINE metric (default); poisson = config #3 CG data-gen solve; "
                          "cascade = config #5 20->640 multi-level inference")
