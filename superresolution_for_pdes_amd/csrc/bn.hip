@@ -27,39 +27,61 @@ __device__ __forceinline__ Chan chan_merge(Chan a, Chan b) {
   return r;
 }
 
-// one block per channel
+// one block per channel.  The equal-count row blocks (all but a ragged last one) merge without a
+// division per partial: with a shift s (block 0's mean), each thread sums (mean_b - s), (mean_b -
+// s)^2 and M2_b in fp64; one fixed-order tree combines the threads; then
+// mean = s + S1 / k  and  M2 = sum M2_b + n * (S2 - S1^2 / k)  (the parallel-variance identity for k
+// blocks of n rows), and the ragged block joins with one Chan merge.  (A Chan merge per partial is
+// a dependent chain of fp64 divisions: 50 of them per thread at the 40x40 layers.)  Also bumps
+// num_batches_tracked (block 0), which used to be a launch of its own.
 __global__ __launch_bounds__(256) void bn_train_finalize_kernel(
     const float2* __restrict__ stats, int nblk, int rows_per_blk, long long P, int C,
     float* running_mean, float* running_var, float momentum, float eps,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches_tracked) {
   const int c = blockIdx.x;
-  __shared__ double sn[256], sm[256], s2[256];
-  Chan acc{0.0, 0.0, 0.0};
-  for (int b = threadIdx.x; b < nblk; b += 256) {
+  __shared__ double s1[256], s2[256], sm[256];
+  const long long nfull_ll = P / rows_per_blk;
+  const int nfull = (int)(nfull_ll < nblk ? nfull_ll : nblk);
+  const double shift = nfull > 0 ? (double)stats[c].x : 0.0;
+  double a1 = 0.0, a2 = 0.0, am = 0.0;
+  for (int b = threadIdx.x; b < nfull; b += 256) {
     const float2 v = stats[(size_t)b * C + c];
-    const long long rem = P - (long long)b * rows_per_blk;
-    const double cnt = (double)(rem < rows_per_blk ? rem : rows_per_blk);
-    acc = chan_merge(acc, Chan{cnt, (double)v.x, (double)v.y});
+    const double d = (double)v.x - shift;
+    a1 += d;
+    a2 = fma(d, d, a2);
+    am += (double)v.y;
   }
-  sn[threadIdx.x] = acc.n; sm[threadIdx.x] = acc.mean; s2[threadIdx.x] = acc.m2;
+  s1[threadIdx.x] = a1; s2[threadIdx.x] = a2; sm[threadIdx.x] = am;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      Chan a{sn[threadIdx.x], sm[threadIdx.x], s2[threadIdx.x]};
-      Chan b{sn[threadIdx.x + s], sm[threadIdx.x + s], s2[threadIdx.x + s]};
-      a = chan_merge(a, b);
-      sn[threadIdx.x] = a.n; sm[threadIdx.x] = a.mean; s2[threadIdx.x] = a.m2;
+    if ((int)threadIdx.x < s) {
+      s1[threadIdx.x] += s1[threadIdx.x + s];
+      s2[threadIdx.x] += s2[threadIdx.x + s];
+      sm[threadIdx.x] += sm[threadIdx.x + s];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double n = sn[0], mean = sm[0], m2 = s2[0];
+    Chan acc{0.0, 0.0, 0.0};
+    if (nfull > 0) {
+      const double k = (double)nfull, n0 = (double)rows_per_blk;
+      const double m2 = sm[0] + n0 * fmax(s2[0] - s1[0] * s1[0] / k, 0.0);
+      acc = Chan{k * n0, shift + s1[0] / k, m2};
+    }
+    for (int b = nfull; b < nblk; ++b) {   // the ragged last block, if any
+      const float2 v = stats[(size_t)b * C + c];
+      const long long rem = P - (long long)b * rows_per_blk;
+      const double cnt = (double)(rem < rows_per_blk ? rem : rows_per_blk);
+      acc = chan_merge(acc, Chan{cnt, (double)v.x, (double)v.y});
+    }
+    const double n = acc.n, mean = acc.mean, m2 = acc.m2;
     const double var_b = m2 / n;
     const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
     mean_out[c] = (float)mean;
     invstd_out[c] = (float)(1.0 / sqrt(var_b + (double)eps));
     if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
     if (running_var) running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)var_u;
+    if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
   }
 }
 
@@ -94,7 +116,6 @@ __global__ __launch_bounds__(256) void bn_affine_kernel(const float* __restrict_
   if (threadIdx.x == 0 && amax) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
-__global__ void increment_i64_kernel(long long* p) { *p += 1; }
 
 // *amax = max(*amax, block max of v) as float bits (v >= 0): the max|x| word the h3
 // convolutions (conv_h3.hip) derive their power-of-two operand scale from
@@ -373,12 +394,8 @@ int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long
   SRPDE_CHECK_ARG(stats && mean_out && invstd_out && C > 0 && nblk > 0, "srpde_bn_train_finalize: bad args");
   hipLaunchKernelGGL(bn_train_finalize_kernel, dim3(C), dim3(256), 0, stream,
                      reinterpret_cast<const float2*>(stats), nblk, rows_per_blk, P, C, running_mean, running_var,
-                     momentum, eps, mean_out, invstd_out);
+                     momentum, eps, mean_out, invstd_out, num_batches_tracked);
   SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize");
-  if (num_batches_tracked) {
-    hipLaunchKernelGGL(increment_i64_kernel, dim3(1), dim3(1), 0, stream, num_batches_tracked);
-    SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize(nbt)");
-  }
   return 0;
 }
 
