@@ -1500,9 +1500,23 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_x6_kernel(WgradParams p) {
     }
 }
 
+// first level of a two-level slab sum (few elements, many slabs: enc1.conv1's 2304 weights over
+// ~2048 slabs): slab g*G <- sum of slabs [g*G, g*G + G) in order, one thread per (element, group)
+__global__ void slab_group_sum_kernel(float* __restrict__ part, int splits, int G, long long total) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long ngroups = (splits + G - 1) / G;
+  if (i >= total * ngroups) return;
+  const long long g = i / total, e = i - g * total;
+  const int q0 = (int)(g * G), q1 = min(splits, q0 + G);
+  float s = 0.f;
+  for (int q = q0; q < q1; ++q) s += part[(size_t)q * total + e];
+  part[(size_t)q0 * total + e] = s;
+}
+
 // sum the split-K slabs in fixed order, write dW in torch layout [Cout][Cin_real][k][k]
+// (slab q at part + q * stride * cout * K: stride > 1 after slab_group_sum_kernel)
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, int splits,
-                                    int cout, int cin, int cin_real, int taps, int accumulate) {
+                                    int cout, int cin, int cin_real, int taps, int accumulate, int stride) {
   // iterate in slab (k-contiguous) order so the split reads coalesce; the transposed
   // store into torch's [Cout][Cin][kh][kw] layout is the scattered side (written once)
   // block = 64 consecutive slab elements x 4 split groups; fixed-order combine
@@ -1513,7 +1527,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __res
   const long long e = (long long)blockIdx.x * 64 + el;
   float s = 0.f;
   if (e < total)
-    for (int q = grp; q < splits; q += 4) s += part[(size_t)q * cout * K + e];
+    for (int q = grp; q < splits; q += 4) s += part[(size_t)q * stride * cout * K + e];
   red[grp][el] = s;
   __syncthreads();
   if (grp == 0 && e < total) {
@@ -1532,8 +1546,18 @@ int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, in
                  hipStream_t stream) {
   const long long total = (long long)cout * taps * cin;
   const int blocks = (int)((total + 63) / 64);
+  int stride = 1;
+  if (total < 65536 && splits >= 128) {   // too few elements to keep the chip busy: sum groups of 32 first
+    constexpr int G = 32;
+    const long long work = total * ((splits + G - 1) / G);
+    hipLaunchKernelGGL(slab_group_sum_kernel, dim3((int)((work + 255) / 256)), dim3(256), 0, stream,
+                       const_cast<float*>(part), splits, G, total);
+    SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce groups)");
+    stride = G;
+    splits = (splits + G - 1) / G;
+  }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, part, dw, splits, cout, cin, cin_real,
-                     taps, accumulate);
+                     taps, accumulate, stride);
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce)");
   return 0;
 }
