@@ -67,6 +67,17 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                      int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* Weight gradient of a 3x3 conv on a 3-channel input (enc1.conv1, models.py:16 with the UNet's
+ * in_channels = 3) whose output feeds a train-mode BN (+ReLU, flags bit 0): dy is formed on the fly
+ * from the BN input y, the incoming gradient da and the per-channel m1 / m2 of srpde_bn_bwd_prepare
+ * (the expressions of srpde_bn_relu_bwd's apply), so it is never written -- replaces that apply pass
+ * plus srpde_conv_wgrad for the reference's conv1.weight.grad (train_enhanced.py:72 backward).
+ * x: NHWC rows of ldx >= 4 floats (channels past 3 ignored); dw [cout][3][3][3]; cout 16, 32 or 64. */
+size_t srpde_conv_wgrad_bnb_c3_workspace_size(long long P, int cout);
+int srpde_conv_wgrad_bnb_c3(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, const float* m1, const float* m2, int flags,
+                            const float* x, int ldx, float* dw, int accumulate, int n, int h, int w, int cout, int dil,
+                            void* workspace, size_t ws_bytes, hipStream_t stream);
 /* activations pre-split once into three bf16 planes [3][P][c] (truncation split, exact) ... */
 int srpde_split_planes(const float* x, int ldx, int c, long long P, void* planes, hipStream_t stream);
 /* ... and the x6 convolution reading them (no split inside the GEMM loop); x0p/x1p are

@@ -1562,6 +1562,141 @@ int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, in
   return 0;
 }
 
+// ------ weight gradient of a conv on a <= 3-channel input, with its BN (+ReLU) backward applied on the fly ------
+// enc1.conv1 (models.py:16,21 on the 3-channel input): dW[co][ci][tap] = sum_p dy[p][co] x[p + off(tap)][ci]
+// is a Cout x 27 sum of outer products over every pixel -- HBM-bound on reading dy, so dy is never
+// written: each thread forms dy = gamma*invstd*(dz - m1 - xhat*m2) (dz = da where the BN+ReLU output
+// is positive) for 4 channels of a pixel row from da and y with bn_bwd_apply_kernel's expressions,
+// and accumulates its 9 taps x 3 input channels x 4 products in fp32.  Rows of a block are combined
+// across lanes and waves in a fixed order and written as one slab [split][Cout][27] (k = tap*3 + ci,
+// the other wgrad kernels' K order), summed in fixed order by wgrad_reduce.  x: NHWC rows of ldx >= 4
+// floats (channels past 3 ignored).
+// Per block: a contiguous pixel range walked in tiles of TP pixels.  Each tile's y and da rows come
+// in as float4 loads (every thread TP*C/1024 of each, all in flight), dy is formed in registers and
+// parked in LDS next to the tile's x halo (TP + 2*(W+1)*dil rows, zero outside the tensor); then a
+// thread owns one channel of a quarter of the tile's pixels and does the 27 products per pixel from
+// LDS (x reads are wave-wide broadcasts).
+constexpr int C3_TP = 64;
+template <int C>
+__global__ __launch_bounds__(256) void wgrad_bnb_c3_kernel(const float* __restrict__ y, int ldy,
+                                                           const float* __restrict__ da, int ldda,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ m1v, const float* __restrict__ m2v,
+                                                           int relu, const float* __restrict__ x, int ldx, int H, int W,
+                                                           int dil, int P, int chunk, float* __restrict__ part) {
+  constexpr int TP = C3_TP, KK = 27, C4 = C / 4;
+  constexpr int RS = 256 / C;                 // pixel groups in the product phase
+  constexpr int LPT = TP * C4 / 256;          // float4 loads per thread per tensor and tile
+  static_assert(256 % C == 0 && (TP * C4) % 256 == 0 && TP % RS == 0, "tile geometry");
+  extern __shared__ float4 c3_lds[];
+  float* dys = reinterpret_cast<float*>(c3_lds);                  // [TP][C]
+  float4* xs = c3_lds + TP * C4;                                   // [TP + 2 * halo][4]
+  float (*red)[9][C] = reinterpret_cast<float (*)[9][C]>(c3_lds);   // after the last tile: [RS][9][C]
+  const int tid = threadIdx.x;
+  const int halo = (W + 1) * dil, HW = H * W;
+  // load-phase coordinates: float4 j of a tile is (pixel j / C4, channels 4 * (j % C4))
+  const int lc = 4 * (tid % C4);
+  const float4 mu = *reinterpret_cast<const float4*>(mean + lc);
+  const float4 is = *reinterpret_cast<const float4*>(invstd + lc);
+  const float4 g = *reinterpret_cast<const float4*>(gamma + lc);
+  const float4 b = *reinterpret_cast<const float4*>(beta + lc);
+  const float4 m1 = *reinterpret_cast<const float4*>(m1v + lc);
+  const float4 m2 = *reinterpret_cast<const float4*>(m2v + lc);
+  const float4 k = make_float4(g.x * is.x, g.y * is.y, g.z * is.z, g.w * is.w);
+  // product-phase coordinates
+  const int c = tid % C, q = C == 64 ? __builtin_amdgcn_readfirstlane(tid / C) : tid / C;
+  float acc[KK];
+#pragma unroll
+  for (int i = 0; i < KK; ++i) acc[i] = 0.f;
+  const int pb = blockIdx.x * chunk, pe = min(P, pb + chunk);
+  for (int t0 = pb; t0 < pe; t0 += TP) {
+    float4 v[LPT], d[LPT];
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int pp = t0 + (tid + 256 * i) / C4;
+      if (pp < pe) {
+        v[i] = *reinterpret_cast<const float4*>(y + (size_t)pp * ldy + lc);
+        d[i] = *reinterpret_cast<const float4*>(da + (size_t)pp * ldda + lc);
+      } else {
+        v[i] = d[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    const int nx = TP + 2 * halo;
+    for (int j = tid; j < nx; j += 256) {
+      const int pp = t0 - halo + j;
+      xs[j] = (pp >= 0 && pp < P) ? *reinterpret_cast<const float4*>(x + (size_t)pp * ldx) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int j = tid + 256 * i, pl = j / C4;
+      float4 o;
+      float xh, dz;
+#define BN_APPLY(X)                                            \
+  xh = (v[i].X - mu.X) * is.X;                                 \
+  dz = (!(relu & 1) || xh * g.X + b.X > 0.f) ? d[i].X : 0.f;   \
+  o.X = (dz - m1.X - xh * m2.X) * k.X;
+      BN_APPLY(x) BN_APPLY(y) BN_APPLY(z) BN_APPLY(w)
+#undef BN_APPLY
+      if (t0 + pl >= pe) o = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(dys + pl * C + lc) = o;
+    }
+    __syncthreads();
+    {
+      // this thread's pixels t0 + q, t0 + q + RS, ...: image coordinates stepped incrementally (q is
+      // wave-uniform when a wave holds one pixel row of channels, so this is scalar work there)
+      const int p0 = t0 + q;
+      int rem = p0 % HW;
+      int py = rem / W, px = rem - py * W;
+      for (int pl = q; pl < TP; pl += RS) {
+        const float o = dys[pl * C + c];
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) {
+          if ((unsigned)(py + (ty - 1) * dil) >= (unsigned)H) continue;
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            if ((unsigned)(px + (tx - 1) * dil) >= (unsigned)W) continue;
+            const float4 xv = xs[pl + halo + ((ty - 1) * W + (tx - 1)) * dil];
+            float* a = acc + (ty * 3 + tx) * 3;
+            a[0] += o * xv.x; a[1] += o * xv.y; a[2] += o * xv.z;
+          }
+        }
+        px += RS;
+        while (px >= W) { px -= W; if (++py == H) py = 0; }
+      }
+    }
+    __syncthreads();
+  }
+  // combine the RS pixel groups in three rounds of nine k-values (keeps the LDS footprint at one
+  // tile, so a weight-gradient workgroup of the side stream still fits next to this block)
+  float* out = part + (size_t)blockIdx.x * C * KK;
+#pragma unroll
+  for (int rd = 0; rd < 3; ++rd) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) red[q][i][c] = acc[rd * 9 + i];
+    __syncthreads();
+    for (int e = tid; e < C * 9; e += 256) {
+      const int co = e / 9, kk = e - co * 9;
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < RS; ++r) t += red[r][kk][co];
+      out[co * KK + rd * 9 + kk] = t;
+    }
+    __syncthreads();
+  }
+}
+
+static void wgrad_bnb_c3_split(long long P, int C, int* chunk, int* splits) {
+  // ~2048 blocks (8 per CU), chunks a multiple of the rows a block covers per sweep
+  const int rs = C3_TP;
+  long long c = (P + 2047) / 2048;
+  c = (c + rs - 1) / rs * rs;
+  *chunk = (int)c;
+  *splits = (int)((P + c - 1) / c);
+}
+
 // W[Cout][Cin_real][k][k] -> Wf[Cout][taps][Cin] and Wd[Cin][taps][Cout] (Cin >= Cin_real, zero pad)
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wf, float* __restrict__ wd,
                                     int cout, int cin, int cin_real, int taps) {
@@ -1984,6 +2119,46 @@ int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, cons
   SRPDE_CHECK_ARG(amax_dy, "srpde_conv_wgrad_h3: null amax_dy");
   return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
                          workspace, ws_bytes, stream, false, amax_dy, amax0, amax1);
+}
+
+size_t srpde_conv_wgrad_bnb_c3_workspace_size(long long P, int cout) {
+  int chunk, splits;
+  wgrad_bnb_c3_split(P, cout, &chunk, &splits);
+  return (size_t)splits * cout * 27 * sizeof(float);
+}
+
+int srpde_conv_wgrad_bnb_c3(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, const float* m1, const float* m2, int flags,
+                            const float* x, int ldx, float* dw, int accumulate, int n, int h, int w, int cout, int dil,
+                            void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && m1 && m2 && x && dw && workspace,
+                  "srpde_conv_wgrad_bnb_c3: null pointer");
+  SRPDE_CHECK_ARG((cout == 64 || cout == 32 || cout == 16) && ldy % 4 == 0 && ldda % 4 == 0 && ldx >= 4 &&
+                      ldx % 4 == 0 && aligned16(y) && aligned16(da) && aligned16(x),
+                  "srpde_conv_wgrad_bnb_c3: needs cout 16/32/64, 16-byte rows and ldx >= 4 (cout=%d ldx=%d)", cout, ldx);
+  const long long P = (long long)n * h * w;
+  int chunk, splits;
+  wgrad_bnb_c3_split(P, cout, &chunk, &splits);
+  const size_t need = (size_t)splits * cout * 27 * sizeof(float);
+  if (ws_bytes < need) {
+    set_error("srpde_conv_wgrad_bnb_c3: workspace %zu < %zu bytes", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  float* part = static_cast<float*>(workspace);
+  const int relu = flags & 1;
+  SRPDE_CHECK_ARG(P < (1LL << 31) / 64, "srpde_conv_wgrad_bnb_c3: tensor too large");
+  const size_t lds = std::max((size_t)C3_TP * cout + (size_t)(C3_TP + 2 * (w + 1) * dil) * 4,
+                              (size_t)(256 / cout) * 9 * cout) * sizeof(float);
+  SRPDE_CHECK_ARG(lds <= 96 * 1024, "srpde_conv_wgrad_bnb_c3: image too wide (w=%d dil=%d)", w, dil);
+#define L(C)                                                                                                     \
+  hipLaunchKernelGGL(wgrad_bnb_c3_kernel<C>, dim3(splits), dim3(256), lds, stream, y, ldy, da, ldda, mean, invstd, \
+                     gamma, beta, m1, m2, relu, x, ldx, h, w, dil, (int)P, chunk, part)
+  if (cout == 64) L(64);
+  else if (cout == 32) L(32);
+  else L(16);
+#undef L
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_bnb_c3");
+  return wgrad_reduce(part, dw, splits, cout, 3, 3, 9, accumulate, stream);
 }
 
 int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout, int cin, int cin_real, int ksize,

@@ -1624,12 +1624,22 @@ int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigne
 // (192-column tiles with 6 waves for K = 576 / 1728 / 3456, which avoid a partly empty last
 // 256-column tile, measured slower on every layer: the waves' efficiency loss outweighs the waste)
 
+// Cout <= 64 with K a multiple of 288 (nine taps of 32 channels: K = 576, 1728): 288-column tiles
+// of nine 64x32 / 32x32 wave tiles, so no column tile is partly empty (K = 576 filled 2.25 of three
+// 256-column tiles).  SRPDE_H3P_288=0 restores the 256-column tiles.
+static bool h3p_use288(int cout, int K) {
+  static const bool on = [] {
+    const char* e = getenv("SRPDE_H3P_288");
+    return !(e && e[0] == '0');
+  }();
+  return on && cout <= 64 && K % 288 == 0;
+}
+
 static void h3p_tiles(int cout, int K, int* bm, int* bn) {
   if (cout >= 256) { *bm = 256; *bn = 128; }
   else if (cout >= 128) { *bm = 128; *bn = 256; }
-  else if (cout >= 64) { *bm = 64; *bn = 256; }
-  else { *bm = 32; *bn = 256; }
-  (void)K;
+  else if (cout >= 64) { *bm = 64; *bn = h3p_use288(cout, K) ? 288 : 256; }
+  else { *bm = 32; *bn = h3p_use288(cout, K) ? 288 : 256; }
 }
 
 void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
@@ -1700,8 +1710,8 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   int rc;
   if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
   else if (cout >= 128) rc = launch_h3p<128, 256, 2, 4>(p, q, stream);
-  else if (cout >= 64) rc = launch_h3p<64, 256, 1, 8>(p, q, stream);
-  else rc = launch_h3p<32, 256, 1, 8>(p, q, stream);
+  else if (cout >= 64) rc = h3p_use288(cout, p.K) ? launch_h3p<64, 288, 1, 9>(p, q, stream) : launch_h3p<64, 256, 1, 8>(p, q, stream);
+  else rc = h3p_use288(cout, p.K) ? launch_h3p<32, 288, 1, 9>(p, q, stream) : launch_h3p<32, 256, 1, 8>(p, q, stream);
   if (rc) return rc;
   return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
 }

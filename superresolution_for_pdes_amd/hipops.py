@@ -336,6 +336,20 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
          int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
 
 
+def conv_wgrad_bnb_c3(y, da, mean, invstd, gamma, beta, m1, m2, x, dw, n, h, w, dil=1, relu=True, accumulate=False):
+    """srpde_conv_wgrad_bnb_c3: dW of a conv on a 3-channel input from the BN (+ReLU) backward terms
+    (m1, m2 of bn_bwd_prepare) -- dy = gamma*invstd*(dz - m1 - xhat*m2) is formed on the fly."""
+    P, cout = y.shape
+    py, ldy = _pl(y)
+    pda, ldda = _pl(da)
+    px, ldx = _pl(x)
+    ws_bytes = int(query("srpde_conv_wgrad_bnb_c3_workspace_size", P, cout))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
+    call("srpde_conv_wgrad_bnb_c3", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), BN_RELU if relu else 0, px, ldx, dw.data_ptr(),
+         int(accumulate), n, h, w, cout, dil, ws.data_ptr(), ws_bytes, stream_ptr())
+
+
 def split_planes_buffer(P, c, device):
     """[2, P, c] fp16 buffer for the h3 kernels' stored input split (planes_out)."""
     return torch.empty(2, P, c, dtype=torch.float16, device=device)

@@ -315,6 +315,14 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         else:
             wq.submit(fn, keep)
         return None if out_part is None else (out_part, dx_max)
+    if (_FUSE_C3 and train and dx is None and x0 is not None and x1 is None and conv.in_channels == 3
+            and x0.shape[1] >= 4 and cout in (16, 32, 64)):
+        # the network's first conv (no input gradient wanted): its BN backward apply runs inside the
+        # weight-gradient kernel, on the compute stream (nothing else is left to overlap with)
+        m1, m2, _ = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
+                                     grads[conv.bias], part=part_t, da_max=da_max)
+        H.conv_wgrad_bnb_c3(y, da, mean, invstd, bn.weight, bn.bias, m1, m2, x0, grads[conv.weight], n, h, w, dil)
+        return None
     dy = H.empty(P, cout, device=y.device)
     # eval mode: the forward normalised with the running statistics (constants), so the BN
     # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
@@ -356,6 +364,10 @@ _FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
 _BNB_WIDE = os.environ.get("SRPDE_BNB_WIDE", "0") == "1"
 _BNB_MAX_CIN, _BNB_MIN_COUT = (192, 32) if _BNB_WIDE else (64, 64)
 
+
+# the first conv's BN backward apply fused into its weight gradient (srpde_conv_wgrad_bnb_c3;
+# SRPDE_FUSE_C3=0: off)
+_FUSE_C3 = os.environ.get("SRPDE_FUSE_C3", "1") != "0"
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
 _FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"

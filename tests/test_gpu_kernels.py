@@ -414,7 +414,7 @@ def test_amax_words_match_outputs():
 
 @pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
     (4, 512, 0, 512, 10, 2), (3, 512, 256, 256, 10, 1), (2, 256, 128, 128, 20, 1), (2, 128, 64, 64, 40, 1),
-    (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1)])
+    (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1), (3, 64, 0, 64, 40, 1)])
 def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
     """h3p: the forward and dgrad kernels store their operand splits (planes_out) and the weight
     gradient consumes them (no split work of its own).  Against fp64: within 3x the fp32-MFMA
@@ -473,3 +473,43 @@ def test_batched_weight_prep_matches_per_layer(conv_math):
                 assert torch.equal(got.h3[0], ref[0]) and torch.equal(got.h3[1], ref[1]), name
                 checked += 1
     assert checked >= 25, checked
+
+
+@pytest.mark.parametrize("n,h,cout,dil", [(3, 40, 64, 1), (2, 13, 32, 1), (2, 9, 16, 2)])
+def test_wgrad_bnb_c3_matches_separate_pass(n, h, cout, dil):
+    """srpde_conv_wgrad_bnb_c3 (the first conv's weight gradient with its BN + ReLU backward formed
+    on the fly) equals the separate apply (srpde_bn_relu_bwd) + fp32 weight gradient to summation
+    order (<= 2e-6 relative), and both match fp64 (<= 1e-5); the input's 4th (padding) column is
+    ignored; the BN parameter / conv-bias gradients from bn_bwd_prepare equal the separate pass's."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(cout * 7 + h)
+    P = n * h * h
+    x = torch.randn(P, 4, generator=g)
+    x[:, 3] = 1e3   # padding column: must not contribute
+    y = torch.randn(P, cout, generator=g) * 2 + 0.3
+    da = torch.randn(P, cout, generator=g) * 1e-2
+    mean = y.mean(0)
+    invstd = 1.0 / torch.sqrt(y.var(0, unbiased=False) + 1e-5)
+    gam, bet = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.3
+    y, da, x, mean, invstd, gam, bet = (t.to(DEV) for t in (y, da, x, mean, invstd, gam, bet))
+    z = lambda: torch.zeros(cout, device=DEV)  # noqa: E731
+    dy = H.empty(P, cout, device=DEV)
+    dg1, db1, dc1 = z(), z(), z()
+    H.bn_relu_bwd(y, da, mean, invstd, gam, bet, dy, dg1, db1, dc1)
+    dw_ref = torch.empty(cout, 3, 3, 3, device=DEV)
+    H.conv_wgrad(dy, x, None, dw_ref, n, h, h, 3, dil)
+    dg2, db2, dc2 = z(), z(), z()
+    m1, m2, _ = H.bn_bwd_prepare(y, da, mean, invstd, gam, bet, dg2, db2, dc2)
+    dw = torch.empty(cout, 3, 3, 3, device=DEV)
+    H.conv_wgrad_bnb_c3(y, da, mean, invstd, gam, bet, m1, m2, x, dw, n, h, h, dil)
+    torch.cuda.synchronize()
+    x64 = x[:, :3].double().cpu().view(n, h, h, 3).permute(0, 3, 1, 2)
+    dy64 = dy.double().cpu().view(n, h, h, cout).permute(0, 3, 1, 2)
+    dw64 = torch.nn.grad.conv2d_weight(x64, (cout, 3, 3, 3), dy64, padding=dil, dilation=dil)
+    assert rel(dw, dw_ref) < 2e-6, rel(dw, dw_ref)
+    assert rel(dw, dw64) < 1e-5 and rel(dw_ref, dw64) < 1e-5, (rel(dw, dw64), rel(dw_ref, dw64))
+    for a, b in ((dg1, dg2), (db1, db2)):
+        assert rel(a, b) < 1e-6
+    # conv-bias gradient sum(dy) = 0 for batch statistics: both are rounding noise around it
+    scale = float(dy.abs().sum(0).max())
+    assert float(dc1.abs().max()) <= 1e-5 * scale and float(dc2.abs().max()) <= 1e-5 * scale
