@@ -1310,6 +1310,218 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
     }
 }
 
+// ------------- weight gradient h3h: the input operand staged once as a ring of pixel rows -------------
+// Same GEMM and operands as h3p (dW[m][tap*Cin + c] = sum_p dY[p][m] X[p + off(tap)][c] from the
+// stored fp16 splits), for a tile of BM output channels x one 32-channel input chunk x all nine taps.
+// In h3p every 32-channel column group of a tap DMA's its own copy of the shifted input rows, so each
+// input element is loaded nine times per pass and the kernel is bound by LDS-DMA issue (~60+ cycles
+// per 1 KiB piece, MI355X_MICROARCH.md) at ~0.4 pieces per MFMA.  Here the input chunk lives in LDS
+// as a ring of CAP pixel rows (slot = row & (CAP - 1)): each stage DMA's only its PS new rows (the
+// rows (W + 1) * dil ahead of the stage), and wave t reads tap t's B fragments at a row shift of
+// off(t) = dy * W + dx.  Input rows a tap must not see (it leaves the image: padding, row and image
+// wrap) are read from a zero row instead, per lane: each lane addresses one pixel row of the
+// transposed read.  Nine waves, one per tap, each a BM x 32 tile.  ~0.11 pieces per MFMA.
+template <int BM, int PS, int NST, int CAP>
+__global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H3P q, int cc_n) {
+  constexpr int NW = 9, TI = BM / 32;
+  constexpr int RA = BM * 2;                   // A image row bytes (one plane)
+  constexpr int IMG_A = PS * RA;               // one plane of one stage
+  constexpr int NA = 2 * IMG_A / 1024;         // A pieces per stage
+  constexpr int NBP = PS / 16;                 // B pieces per plane per stage (16 rows x 64 B)
+  constexpr int NB = 2 * NBP;
+  constexpr int TOT = NA + NB;                 // pieces per stage
+  constexpr int DLO = TOT / NW, NHI = TOT % NW;   // waves < NHI issue DLO + 1 pieces per stage
+  constexpr int RING = (CAP + 1) * 64;         // one plane of the input ring + its zero row
+  static_assert(IMG_A % 1024 == 0 && PS % 16 == 0 && (NST == 3 || NST == 4), "stage geometry");
+  static_assert((CAP & (CAP - 1)) == 0 && CAP >= 64, "ring rows: a power of two");
+  static_assert((NST - 2) * (DLO + 1) <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  char* const abuf = lds;                              // [NST][2][PS][RA]
+  char* const bring = abuf + NST * 2 * IMG_A;          // [2][CAP][64]
+  char* const zrow = bring + CAP * 64;                 // the hi plane's zero row (lo: + RING)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbm = (p.Cout + BM - 1) / BM;
+  const int ntile = nbm * cc_n;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / cc_n, cc = tile - mt * cc_n;
+  const int m0 = mt * BM, c0 = cc * 32;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int nsteps = (pend - pbeg + PS - 1) / PS;
+  const int halo = (p.W + 1) * p.dil;
+  const int rbase = (pbeg + halo + 15) & ~15;          // first row the stages DMA (16-aligned)
+  const int rlo = (pbeg - halo) & ~15;                 // first row of the prologue (may be < 0)
+
+  if (threadIdx.x < 8)
+    reinterpret_cast<float4*>(zrow + (threadIdx.x >> 2) * RING)[threadIdx.x & 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.Cout * 2));
+  const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
+  const unsigned aplane = (unsigned)((size_t)p.P * p.Cout * 2), bplane = (unsigned)((size_t)p.P * p.Cin * 2);
+
+  // B piece of rows [r, r + 16) of plane pl: lane -> row r + lane / 4, 16-B chunk lane % 4
+  auto bpiece = [&](int r, int pl) {
+    const int row = r + (lane >> 2);
+    const unsigned off = (row >= 0 && row < p.P)
+                             ? pl * bplane + (unsigned)(((size_t)row * p.Cin + c0 + 8 * (lane & 3)) * 2)
+                             : OOB;
+    dma16(rsb, off, lds_addr_of(bring + pl * RING + (r & (CAP - 1)) * 64));
+  };
+  // this wave's pieces of stage s (ring slot SLOT): piece u = wave + j * NW; u < NA: A, else B
+  auto issue = [&](int s, int slot) {
+    const int p0 = pbeg + s * PS;
+    const bool full = p0 + PS <= pend;
+#pragma unroll
+    for (int j = 0; j < DLO + 1; ++j) {
+      const int u = wave + j * NW;
+      if (j == DLO && wave >= NHI) break;
+      if (u < NA) {
+        const int pl = u / (NA / 2), idx = u - pl * (NA / 2);
+        const int byte = idx * 1024 + lane * 16;
+        const int row = byte / RA, sl = (byte - row * RA) >> 4;
+        const int m = m0 + 8 * (sl ^ wx_swz<RA>(row));
+        const bool ok = m < p.Cout && (full || p0 + row < pend);
+        dma16(rsa, ok ? pl * aplane + (unsigned)(((size_t)(p0 + row) * p.Cout + m) * 2) : OOB,
+              lds_addr_of(abuf + (slot * 2 + pl) * IMG_A + idx * 1024));
+      } else {
+        const int v = u - NA, pl = v / NBP, g = v - pl * NBP;
+        bpiece(rbase + s * PS + 16 * g, pl);
+      }
+    }
+  };
+  // prologue: the input rows [rlo, rbase) every later stage assumes resident
+  {
+    const int ng = (rbase - rlo) >> 4;
+    for (int v = wave; v < 2 * ng; v += NW) bpiece(rlo + 16 * (v >> 1), v & 1);
+  }
+
+  const int ea = h3_exp(*q.ady);
+  unsigned xb = *q.ax0;
+  if (p.c1) xb = max(xb, *q.ax1);
+  const int eb = h3_exp(xb);
+
+  floatx16 acc[TI], part[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  int2 oa[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) oa[i] = tr_offsets<RA>(32 * i, lane);
+  // this wave's tap and the lane's four pixel rows of a stage (kk, half): image coordinates
+  const int ty = wave / 3, tx = wave - 3 * (wave / 3);
+  const int dyo = (ty - 1) * p.dil, dxo = (tx - 1) * p.dil;
+  const int toff = dyo * p.W + dxo;
+  const int colb = 2 * ((lane & 16) + 4 * (lane & 3));
+  const int h = lane >> 5, qq = (lane & 15) >> 2;
+  const int HW = p.H * p.W;
+  const int psy = PS / p.W, psx = PS - psy * p.W;
+  int px[NBP][2], py[NBP][2];
+#pragma unroll
+  for (int kk = 0; kk < NBP; ++kk)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pl = pbeg + 16 * kk + 8 * h + 4 * j + qq;
+      const int rem = pl % HW;
+      py[kk][j] = rem / p.W;
+      px[kk][j] = rem - py[kk][j] * p.W;
+    }
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s, s);
+  const unsigned zaddr = lds_addr_of(zrow) + colb;
+  const unsigned bbase = lds_addr_of(bring) + colb;
+  auto stage = [&](int s, auto fresh_tag, auto slot_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    constexpr int SLOT = decltype(slot_tag)::value;
+    if (wave < NHI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * (DLO + 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DLO) : "memory");
+    __syncthreads();
+    issue(s + NST - 1, (SLOT + NST - 1) % NST);
+    const lds_char* sa = (const lds_char*)(uintptr_t)lds_addr_of(abuf) + SLOT * 2 * IMG_A;
+    const int p0 = pbeg + s * PS;
+    // fragments of kk + 1 are read while kk's MFMAs run (register double buffer)
+    auto bfrag = [&](int kk, half8& bh, half8& bl) {
+      // B rows of this lane for tap `wave`: the shifted input row, or the zero row (both planes
+      // keep one past the ring, so hi and lo addresses differ by RING either way)
+      unsigned ba[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = (unsigned)(py[kk][j] + dyo) < (unsigned)p.H && (unsigned)(px[kk][j] + dxo) < (unsigned)p.W;
+        const int row = p0 + 16 * kk + 8 * h + 4 * j + qq + toff;
+        ba[j] = ok ? bbase + (unsigned)((row & (CAP - 1)) * 64) : zaddr;
+      }
+      bh = tr_read((const lds_char*)(uintptr_t)ba[0], (const lds_char*)(uintptr_t)ba[1]);
+      bl = tr_read((const lds_char*)(uintptr_t)(ba[0] + RING), (const lds_char*)(uintptr_t)(ba[1] + RING));
+    };
+    auto afrag = [&](int kk, half8* ah, half8* al) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        ah[i] = tr_read(sa + oa[i].x + kk * 16 * RA, sa + oa[i].y + kk * 16 * RA);
+        al[i] = tr_read(sa + IMG_A + oa[i].x + kk * 16 * RA, sa + IMG_A + oa[i].y + kk * 16 * RA);
+      }
+    };
+    half8 bh[2], bl[2], ah[2][TI], al[2][TI];
+    bfrag(0, bh[0], bl[0]);
+    afrag(0, ah[0], al[0]);
+#pragma unroll
+    for (int kk = 0; kk < NBP; ++kk) {
+      const int cur = kk & 1;
+      if (kk + 1 < NBP) {
+        bfrag(kk + 1, bh[cur ^ 1], bl[cur ^ 1]);
+        afrag(kk + 1, ah[cur ^ 1], al[cur ^ 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        floatx16 c0v;
+        if (FRESH && kk == 0)
+          c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cur][i], bh[cur], floatx16{}, 0, 0, 0);   // small terms first
+        else
+          c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cur][i], bh[cur], part[i], 0, 0, 0);
+        c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][i], bl[cur], c0v, 0, 0, 0);
+        part[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][i], bh[cur], c0v, 0, 0, 0);
+      }
+    }
+    // the lane's pixels of the next stage
+#pragma unroll
+    for (int kk = 0; kk < NBP; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        int x = px[kk][j] + psx, y = py[kk][j] + psy;
+        if (x >= p.W) { x -= p.W; ++y; }
+        if (y >= p.H) y -= p.H;
+        px[kk][j] = x; py[kk][j] = y;
+      }
+  };
+  for (int s = 0; s < nsteps; s += NST) {
+    stage(s, std::true_type{}, std::integral_constant<int, 0>{});
+    if (s + 1 < nsteps) stage(s + 1, std::false_type{}, std::integral_constant<int, 1>{});
+    if (s + 2 < nsteps) stage(s + 2, std::false_type{}, std::integral_constant<int, 2>{});
+    if constexpr (NST > 3)
+      if (s + 3 < nsteps) stage(s + 3, std::false_type{}, std::integral_constant<int, NST - 1>{});
+#pragma unroll
+    for (int i = 0; i < TI; ++i) acc[i] += part[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // spare DMAs land before the workgroup retires
+
+  // slab [split][Cout][K], k = tap * Cin + c; scales undone (exact powers of two)
+  const float ua = exp2i(-ea), ub = exp2i(-eb);
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int n = wave * p.Cin + c0 + lr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (m < p.Cout) out[(size_t)m * p.K + n] = (acc[i][r] * ua) * ub;
+    }
+}
+
 // fp32 packed weights [rows][K] -> fp16 hi / lo planes [2][rows][K] with a power-of-two scale
 // per row (one wave per row)
 __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
@@ -1663,6 +1875,41 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
   *splits = ceil_div(P, c);
 }
 
+// h3h: the input-row-ring weight gradient for the 288-column shapes (one 32-channel input chunk x
+// nine taps per tile, the same tiles and split-K slabs as h3p's 288-column kernel) whose ring of
+// H3H_CAP rows holds a stage's reach: 3 stages of H3H_PS rows + 2 (W + 1) dil + alignment.
+// SRPDE_H3H=0: h3p instead.
+// pixels per stage, ring depth (stages), ring rows: SRPDE_H3H_CFG=1 -> 32 / 4 / 256, else 64 / 3 / 512
+constexpr int H3H_PS = 64, H3H_CAP = 512;
+static int h3h_cfg() {
+  static const int v = [] { const char* e = getenv("SRPDE_H3H_CFG"); return e ? atoi(e) : 0; }();
+  return v;
+}
+static bool h3h_ok(int cout, int K, int cin, int w, int dil) {
+  static const bool on = [] {
+    const char* e = getenv("SRPDE_H3H");
+    return !(e && e[0] == '0');
+  }();
+  return on && h3p_use288(cout, K) && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP &&
+         2 * (w + 1) * dil + 15 + 4 * 32 <= 256;
+}
+
+template <int BM, int PS, int NST, int CAP>
+static int launch_h3h_cfg(const WgradParams& p, const H3P& q, hipStream_t st) {
+  const int cc_n = p.Cin / 32;
+  const int nb = ceil_div(p.Cout, BM) * cc_n * p.splits;
+  const size_t lds = (size_t)NST * 2 * PS * BM * 2 + (size_t)2 * (CAP + 1) * 64;
+  hipLaunchKernelGGL((conv_wgrad_h3h_kernel<BM, PS, NST, CAP>), dim3(nb), dim3(576), lds, st, p, q, cc_n);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p(h3h)");
+  return 0;
+}
+template <int BM>
+static int launch_h3h(const WgradParams& p, const H3P& q, hipStream_t st) {
+  if (h3h_cfg() == 1) return launch_h3h_cfg<BM, 32, 4, 256>(p, q, st);
+  if (h3h_cfg() == 2) return launch_h3h_cfg<BM, 64, 4, 512>(p, q, st);
+  return launch_h3h_cfg<BM, H3H_PS, 3, H3H_CAP>(p, q, st);
+}
+
 template <int BM, int BN, int WM, int WN>
 static int launch_h3p(const WgradParams& p, const H3P& q, hipStream_t st) {
   constexpr int PS = 32, NST = 3;
@@ -1710,6 +1957,7 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   int rc;
   if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
   else if (cout >= 128) rc = launch_h3p<128, 256, 2, 4>(p, q, stream);
+  else if (h3h_ok(cout, p.K, p.Cin, w, dil)) rc = cout >= 64 ? launch_h3h<64>(p, q, stream) : launch_h3h<32>(p, q, stream);
   else if (cout >= 64) rc = h3p_use288(cout, p.K) ? launch_h3p<64, 288, 1, 9>(p, q, stream) : launch_h3p<64, 256, 1, 8>(p, q, stream);
   else rc = h3p_use288(cout, p.K) ? launch_h3p<32, 288, 1, 9>(p, q, stream) : launch_h3p<32, 256, 1, 8>(p, q, stream);
   if (rc) return rc;

@@ -365,9 +365,11 @@ _BNB_WIDE = os.environ.get("SRPDE_BNB_WIDE", "0") == "1"
 _BNB_MAX_CIN, _BNB_MIN_COUT = (192, 32) if _BNB_WIDE else (64, 64)
 
 
-# the first conv's BN backward apply fused into its weight gradient (srpde_conv_wgrad_bnb_c3;
-# SRPDE_FUSE_C3=0: off)
-_FUSE_C3 = os.environ.get("SRPDE_FUSE_C3", "1") != "0"
+# the first conv's BN backward apply fused into its weight gradient (srpde_conv_wgrad_bnb_c3):
+# 362 us against 417 + 182 us for the separate passes alone, but in the step it shares the GPU with
+# enc1.conv2's concurrent weight gradient, which sets the tail either way (measured +0.06 /
+# +0.09 / -0.02 ms on three boxes), so off unless SRPDE_FUSE_C3=1
+_FUSE_C3 = os.environ.get("SRPDE_FUSE_C3", "0") == "1"
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
 _FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"

@@ -414,7 +414,8 @@ def test_amax_words_match_outputs():
 
 @pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
     (4, 512, 0, 512, 10, 2), (3, 512, 256, 256, 10, 1), (2, 256, 128, 128, 20, 1), (2, 128, 64, 64, 40, 1),
-    (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1), (3, 64, 0, 64, 40, 1)])
+    (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1), (3, 64, 0, 64, 40, 1),
+    (3, 64, 0, 64, 13, 2), (2, 64, 32, 32, 20, 1)])
 def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
     """h3p: the forward and dgrad kernels store their operand splits (planes_out) and the weight
     gradient consumes them (no split work of its own).  Against fp64: within 3x the fp32-MFMA
