@@ -1879,19 +1879,17 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
 // nine taps per tile, the same tiles and split-K slabs as h3p's 288-column kernel) whose ring of
 // H3H_CAP rows holds a stage's reach: 3 stages of H3H_PS rows + 2 (W + 1) dil + alignment.
 // SRPDE_H3H=0: h3p instead.
-// pixels per stage, ring depth (stages), ring rows: SRPDE_H3H_CFG=1 -> 32 / 4 / 256, else 64 / 3 / 512
+// pixels per stage and ring rows (measured: 32-pixel stages 3-10% slower; a fourth ring stage of
+// 32 or 64 pixels within 1-2%)
 constexpr int H3H_PS = 64, H3H_CAP = 512;
-static int h3h_cfg() {
-  static const int v = [] { const char* e = getenv("SRPDE_H3H_CFG"); return e ? atoi(e) : 0; }();
-  return v;
-}
+// (Cout >= 128 would need 9 waves x 128 x 32 accumulators with the two-level chain: 168 VGPRs
+// and 312 B of spill scratch at three waves per SIMD -- not built; those layers keep h3p)
 static bool h3h_ok(int cout, int K, int cin, int w, int dil) {
   static const bool on = [] {
     const char* e = getenv("SRPDE_H3H");
     return !(e && e[0] == '0');
   }();
-  return on && h3p_use288(cout, K) && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP &&
-         2 * (w + 1) * dil + 15 + 4 * 32 <= 256;
+  return on && h3p_use288(cout, K) && K == 9 * cin && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP;
 }
 
 template <int BM, int PS, int NST, int CAP>
@@ -1905,8 +1903,6 @@ static int launch_h3h_cfg(const WgradParams& p, const H3P& q, hipStream_t st) {
 }
 template <int BM>
 static int launch_h3h(const WgradParams& p, const H3P& q, hipStream_t st) {
-  if (h3h_cfg() == 1) return launch_h3h_cfg<BM, 32, 4, 256>(p, q, st);
-  if (h3h_cfg() == 2) return launch_h3h_cfg<BM, 64, 4, 512>(p, q, st);
   return launch_h3h_cfg<BM, H3H_PS, 3, H3H_CAP>(p, q, st);
 }
 
