@@ -263,6 +263,14 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
 int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,
                   const float* b1, const float* w2, const float* b2, const float* wg, const float* bg, float* m,
                   float* hbuf, float* ca, float* sa, float* out, int ldo, hipStream_t stream);
+/* srpde_att_fwd in two halves: the channel attention (mean over the pixels, the two 1x1 convs,
+ * sigmoid -> ca [n][c]; depends on x alone, so it may run as soon as x exists, on another stream)
+ * and the gate (spatial attention of g -> sa [n*hw], out = x * ca * sa). */
+int srpde_att_channel_fwd(const float* x, int ldx, int n, int hw, int c, const float* w1, const float* b1,
+                          const float* w2, const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream);
+int srpde_att_gate_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc,
+                       const float* ca, const float* wg, const float* bg, float* sa, float* out, int ldo,
+                       hipStream_t stream);
 size_t srpde_att_bwd_workspace_size(int n, int hw, int c, int gc);
 /* dg == NULL: the gating gradient is not written; workspace[0, n*hw) floats then holds dsa (the
  * spatial gate's pre-sigmoid gradient) for srpde_upsample_bilinear_bwd_gated. */

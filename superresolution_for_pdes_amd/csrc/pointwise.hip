@@ -1145,6 +1145,32 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
   return 0;
 }
 
+int srpde_att_channel_fwd(const float* x, int ldx, int n, int hw, int c, const float* w1, const float* b1,
+                          const float* w2, const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && w1 && b1 && w2 && b2 && m && hbuf && ca, "srpde_att_channel_fwd: null");
+  SRPDE_CHECK_ARG(c % 32 == 0 && c <= 1024, "srpde_att_channel_fwd: channel count");
+  const int cr = c / 8;
+  const size_t lds = (4 * 256 + c + cr) * sizeof(float);
+  hipLaunchKernelGGL(att_channel_fwd_kernel, dim3(n), dim3(256), lds, stream, x, ldx, hw, c, cr, w1, b1, w2, b2, m,
+                     hbuf, ca);
+  SRPDE_LAUNCH_CHECK("srpde_att_channel_fwd");
+  return 0;
+}
+
+int srpde_att_gate_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc,
+                       const float* ca, const float* wg, const float* bg, float* sa, float* out, int ldo,
+                       hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && g && ca && wg && bg && sa && out, "srpde_att_gate_fwd: null");
+  SRPDE_CHECK_ARG(c % 32 == 0 && gc % 4 == 0 && c <= 1024, "srpde_att_gate_fwd: channel counts");
+  const long long P = (long long)n * hw;
+  hipLaunchKernelGGL(att_spatial_fwd_kernel, dim3(grid_for(P * 8)), dim3(256), 0, stream, g, ldg, P, gc, wg, bg, sa);
+  SRPDE_LAUNCH_CHECK("srpde_att_gate_fwd(spatial)");
+  hipLaunchKernelGGL(att_apply_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, x, ldx, ca, sa, out, ldo,
+                     P, hw, c);
+  SRPDE_LAUNCH_CHECK("srpde_att_gate_fwd(apply)");
+  return 0;
+}
+
 int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,
                   const float* b1, const float* w2, const float* b2, const float* wg, const float* bg, float* m,
                   float* hbuf, float* ca, float* sa, float* out, int ldo, hipStream_t stream) {

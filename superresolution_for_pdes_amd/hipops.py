@@ -539,6 +539,34 @@ def att_fwd(x, g, n, hw, w1, b1, w2, b2, wg, bg, out=None):
     return out, (m, hb, ca, sa)
 
 
+def att_channel_fwd(x, n, hw, w1, b1, w2, b2):
+    """srpde_att_channel_fwd -> (m, hb, ca): the gate's channel attention (x alone)."""
+    c = x.shape[1]
+    dev = x.device
+    m, hb, ca = empty(n, c, device=dev), empty(n, c // 8, device=dev), empty(n, c, device=dev)
+    px, ldx = _pl(x)
+    call("srpde_att_channel_fwd", px, ldx, n, hw, c, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+         m.data_ptr(), hb.data_ptr(), ca.data_ptr(), stream_ptr())
+    return m, hb, ca
+
+
+def att_gate_fwd(x, g, n, hw, chan, wg, bg, out=None):
+    """srpde_att_gate_fwd with ``chan`` = att_channel_fwd(x, ...): out = x * ca * sigmoid(conv1x1(g)).
+    Returns (out, saved) as att_fwd."""
+    m, hb, ca = chan
+    c, gc = x.shape[1], g.shape[1]
+    sa = empty(n * hw, device=x.device)
+    if out is None:
+        out = empty(n * hw, c, device=x.device)
+    px, ldx = _pl(x)
+    pg, ldg = _pl(g)
+    po, ldo = _pl(out)
+    call("srpde_att_gate_fwd", px, ldx, pg, ldg, n, hw, c, gc, ca.data_ptr(), wg.data_ptr(), bg.data_ptr(),
+         sa.data_ptr(), po, ldo, stream_ptr())
+    tag_amax(out, getattr(x, "_srpde_amax", None))   # x * sigmoid * sigmoid: |out| <= |x|
+    return out, (m, hb, ca, sa)
+
+
 def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg,
             defer_params=False):
     """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None) is the
