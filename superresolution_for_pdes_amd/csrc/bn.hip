@@ -34,17 +34,33 @@ __device__ __forceinline__ Chan chan_merge(Chan a, Chan b) {
 // blocks of n rows), and the ragged block joins with one Chan merge.  (A Chan merge per partial is
 // a dependent chain of fp64 divisions: 50 of them per thread at the 40x40 layers.)  Also bumps
 // num_batches_tracked (block 0), which used to be a launch of its own.
-__global__ __launch_bounds__(256) void bn_train_finalize_kernel(
+// 1024 threads, four partials in flight per thread: the kernel is latency-bound (one block per
+// channel reads nblk strided float2), e.g. 12,800 partials per channel at the 40x40 layers.
+constexpr int FIN_T = 1024;
+__global__ __launch_bounds__(FIN_T) void bn_train_finalize_kernel(
     const float2* __restrict__ stats, int nblk, int rows_per_blk, long long P, int C,
     float* running_mean, float* running_var, float momentum, float eps,
     float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches_tracked) {
   const int c = blockIdx.x;
-  __shared__ double s1[256], s2[256], sm[256];
+  __shared__ double s1[FIN_T], s2[FIN_T], sm[FIN_T];
   const long long nfull_ll = P / rows_per_blk;
   const int nfull = (int)(nfull_ll < nblk ? nfull_ll : nblk);
   const double shift = nfull > 0 ? (double)stats[c].x : 0.0;
   double a1 = 0.0, a2 = 0.0, am = 0.0;
-  for (int b = threadIdx.x; b < nfull; b += 256) {
+  int b = threadIdx.x;
+  for (; b + 3 * FIN_T < nfull; b += 4 * FIN_T) {
+    float2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = stats[(size_t)(b + u * FIN_T) * C + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double d = (double)v[u].x - shift;
+      a1 += d;
+      a2 = fma(d, d, a2);
+      am += (double)v[u].y;
+    }
+  }
+  for (; b < nfull; b += FIN_T) {
     const float2 v = stats[(size_t)b * C + c];
     const double d = (double)v.x - shift;
     a1 += d;
@@ -53,7 +69,7 @@ __global__ __launch_bounds__(256) void bn_train_finalize_kernel(
   }
   s1[threadIdx.x] = a1; s2[threadIdx.x] = a2; sm[threadIdx.x] = am;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = FIN_T / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
       s1[threadIdx.x] += s1[threadIdx.x + s];
       s2[threadIdx.x] += s2[threadIdx.x + s];
@@ -392,7 +408,7 @@ int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long
                             float* running_mean, float* running_var, long long* num_batches_tracked,
                             float momentum, float eps, float* mean_out, float* invstd_out, hipStream_t stream) {
   SRPDE_CHECK_ARG(stats && mean_out && invstd_out && C > 0 && nblk > 0, "srpde_bn_train_finalize: bad args");
-  hipLaunchKernelGGL(bn_train_finalize_kernel, dim3(C), dim3(256), 0, stream,
+  hipLaunchKernelGGL(bn_train_finalize_kernel, dim3(C), dim3(FIN_T), 0, stream,
                      reinterpret_cast<const float2*>(stats), nblk, rows_per_blk, P, C, running_mean, running_var,
                      momentum, eps, mean_out, invstd_out, num_batches_tracked);
   SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize");
