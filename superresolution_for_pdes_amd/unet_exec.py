@@ -131,13 +131,40 @@ def prepare_h3_weights(m):
         key = (sig, tuple(c.weight._version for c in convs), step_count())
         if getattr(m, "_srpde_h3w_key", None) == key:
             return
-    H.prepare_weights_h3(desc_t, nl, rows)
+    global _H3W_PENDING
+    dev = desc_t.device
+    if _H3W_SIDE and m.training and dev.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+        # on the side stream, beside the input transpose and enc1.conv1 (which reads no split):
+        # the first consumer of a split waits for it (_h3w_ready)
+        main = torch.cuda.current_stream(dev)
+        side = WgradStream(dev).side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            H.prepare_weights_h3(desc_t, nl, rows)
+        _H3W_PENDING = torch.cuda.Event()
+        _H3W_PENDING.record(side)
+    else:
+        H.prepare_weights_h3(desc_t, nl, rows)
     m._srpde_h3w_key = key
+
+
+# the per-step weight split on the side stream (SRPDE_H3W_SIDE=0: in line); its event until the
+# first h3 convolution of the step waits for it
+_H3W_SIDE = os.environ.get("SRPDE_H3W_SIDE", "1") != "0"
+_H3W_PENDING = None
+
+
+def _h3w_ready(dev):
+    global _H3W_PENDING
+    if _H3W_PENDING is not None:
+        torch.cuda.current_stream(dev).wait_event(_H3W_PENDING)
+        _H3W_PENDING = None
 
 
 def _fwd_weights(conv, cin, c0, c1, w, dil):
     wp = getattr(conv, "_srpde_h3f", None)
     if wp is not None and H.h3_capable(c0, c1, conv.out_channels, w, dil):
+        _h3w_ready(conv.weight.device)
         return wp
     return H.pack_conv_weights(conv.weight, cin)[0]
 
@@ -145,6 +172,7 @@ def _fwd_weights(conv, cin, c0, c1, w, dil):
 def _dgrad_weights(conv, cin, w, dil):
     wp = getattr(conv, "_srpde_h3d", None)
     if wp is not None and H.h3_capable(conv.out_channels, 0, cin, w, dil):
+        _h3w_ready(conv.weight.device)
         return wp
     return H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)[1]
 
