@@ -514,3 +514,36 @@ def test_wgrad_bnb_c3_matches_separate_pass(n, h, cout, dil):
     # conv-bias gradient sum(dy) = 0 for batch statistics: both are rounding noise around it
     scale = float(dy.abs().sum(0).max())
     assert float(dc1.abs().max()) <= 1e-5 * scale and float(dc2.abs().max()) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("n,h,w", [(3, 40, 40), (2, 13, 7)])
+def test_first_conv_direct_matches_fp64(n, h, w):
+    """The 3-channel input conv (enc1.conv1: padded 4-float rows, 64 outputs): y against fp64
+    (<= 1e-6 relative; the padding column meets zero weights) and the BN partials equal each
+    256-row block's (mean, M2) of y itself (<= 1e-5 relative)."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(n + h)
+    x = torch.randn(n, 3, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(64, 3, 3, 3, generator=g, dtype=torch.float64) * 0.3
+    b = torch.randn(64, generator=g, dtype=torch.float64)
+    ref = torch.nn.functional.conv2d(x, wt, b, padding=1)
+    P = n * h * w
+    x4 = torch.zeros(P, 4, dtype=torch.float32)
+    x4[:, :3] = rows(x.float())
+    x4[:, 3] = 7.0                       # padding column: must not contribute
+    x4 = x4.to(DEV)
+    wf = H.pack_conv_weights(wt.float().to(DEV), 4)[0]
+    y = H.empty(P, 64, device=DEV)
+    stats, nblk, rpb = H.conv_stats_buffer(n, h, w, 64, DEV, 4)
+    H.conv_fwd(x4, None, wf, b.float().to(DEV), y, n, h, w, 64, 3, 1, 1, False, stats)
+    torch.cuda.synchronize()
+    yr = rows(ref)
+    assert rel(y, yr) < 1e-6, rel(y, yr)
+    yc = y.double().cpu()
+    st = stats.double().cpu()
+    for k in range(nblk):
+        blk = yc[k * rpb:(k + 1) * rpb]
+        mean = blk.mean(0)
+        m2 = ((blk - mean) ** 2).sum(0)
+        assert float((st[k, :, 0] - mean).abs().max()) <= 1e-5 * float(blk.abs().max())
+        assert float((st[k, :, 1] - m2).abs().max()) <= 1e-5 * float(m2.abs().max()) + 1e-6

@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024)
-    a = ap.parse_args()
+    a, _ = ap.parse_known_args()
     dev = "cuda"
     n, h, C = a.batch, 40, 64
     P = n * h * h
@@ -50,5 +50,26 @@ def main():
           f"fused {t_fused * 1e3:.1f} us ({gb / (t_fused * 1e-3) / 1e3:.2f} TB/s of y + da)")
 
 
+
+
+def first_conv_fwd(iters=20):
+    """enc1.conv1 forward (4-float input rows -> 64 channels + BN partials) at batch 1024 (a vector-unit
+    kernel for this layer measured 347 us against the fp32 implicit GEMM's 220 us: not kept)."""
+    dev = "cuda"
+    n, h = 1024, 40
+    P = n * h * h
+    x = torch.randn(P, 4, device=dev)
+    wt = torch.randn(64, 3, 3, 3, device=dev)
+    b = torch.randn(64, device=dev)
+    wf = H.pack_conv_weights(wt, 4)[0]
+    y = H.empty(P, 64, device=dev)
+    stats, _, _ = H.conv_stats_buffer(n, h, h, 64, dev, 4)
+    t = timeit(lambda: H.conv_fwd(x, None, wf, b, y, n, h, h, 64, 3, 1, 1, False, stats), iters)
+    print(f"first conv forward: {t * 1e3:.1f} us ({P * 64 * 4 / (t * 1e-3) / 1e12:.2f} TB/s of y)")
+
+
 if __name__ == "__main__":
-    main()
+    if "--first-conv" in sys.argv:
+        first_conv_fwd()
+    else:
+        main()
