@@ -179,6 +179,12 @@ int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, i
 int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                       const float* beta, float* out, int ldo, long long P, int C, int relu, unsigned* amax,
                       hipStream_t stream);
+/* srpde_bn_relu_fwd of an [n][h][w][C] block output followed by srpde_maxpool2x2_fwd of it
+ * (models.py:22-23 then :79-80), in one pass: out = relu(bn(y)) and pool = its 2x2 max (same
+ * values and tie order as the separate calls).  h, w even. */
+int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w, int C,
+                           int relu, unsigned* amax, hipStream_t stream);
 /* train-mode BN folded into a per-channel affine for a consumer that applies it on the fly
  * (a = relu(y*scale + shift), srpde_conv_fwd_h3's in_scale / in_shift), plus a rigorous bound
  * on max|a| (|gamma| sqrt(P-1) + |beta|, Samuelson's inequality) into *amax_bound (nullable) */

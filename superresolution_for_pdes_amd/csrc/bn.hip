@@ -388,6 +388,59 @@ __global__ __launch_bounds__(256) void bn_bwd_coef_kernel(const double* __restri
   if (threadIdx.x == 0) *dy_amax = __float_as_uint(red[0] * 1.0001f);   // covers the float rounding of the sum
 }
 
+// BN + ReLU of a ConvBlock output that a 2x2 max-pool reads next (models.py:79-80): each thread
+// forms the four pixels of one pooling window for 4 channels with bn_relu_fwd_kernel's expressions,
+// stores them, and stores their max in maxpool2_fwd's comparison order (first max wins) -- the pool
+// no longer re-reads the activation.  amax: max|out| (the pooled tensor's bound as well).
+__global__ __launch_bounds__(256) void bn_relu_pool_fwd_kernel(const float* __restrict__ y, int ldy,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float* __restrict__ out,
+                                                               int ldo, float* __restrict__ pool, int ldp, int n, int H,
+                                                               int W, int C, int relu, unsigned* amax) {
+  const int C4 = C >> 2, Wo = W >> 1, Ho = H >> 1;
+  const long long total = (long long)n * Ho * Wo * C4;
+  float mx = 0.f;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long q = e / C4;
+    const int c = (int)(e - q * C4) * 4;
+    const int ox = (int)(q % Wo);
+    const long long t = q / Wo;
+    const int oy = (int)(t % Ho);
+    const long long nb = t / Ho;
+    const long long p00 = (nb * H + 2 * oy) * W + 2 * ox;
+    const long long pp[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    float4 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(y + pp[k] * ldy + c);
+      float4 r;
+      r.x = (v.x - mu.x) * is.x * g.x + b.x;
+      r.y = (v.y - mu.y) * is.y * g.y + b.y;
+      r.z = (v.z - mu.z) * is.z * g.z + b.z;
+      r.w = (v.w - mu.w) * is.w * g.w + b.w;
+      if (relu) {
+        r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+      }
+      *reinterpret_cast<float4*>(out + pp[k] * ldo + c) = r;
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w))));
+      o[k] = r;
+    }
+    float4 m;
+#define MX(X) { float v = o[0].X; if (o[1].X > v) v = o[1].X; if (o[2].X > v) v = o[2].X; if (o[3].X > v) v = o[3].X; m.X = v; }
+    MX(x) MX(y) MX(z) MX(w)
+#undef MX
+    *reinterpret_cast<float4*>(pool + q * ldp + c) = m;
+  }
+  if (amax) block_amax(mx, amax);
+}
+
 static int bwd_blocks(long long P, int C, int* rows_per_blk) {
   // ~1024 blocks; rows per block a multiple of the rows a block covers per sweep
   const int rs = 256 / (C >> 2);
@@ -435,6 +488,20 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
   hipLaunchKernelGGL(bn_relu_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
                      out, ldo, P, C, relu, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_fwd");
+  return 0;
+}
+
+int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w, int C,
+                           int relu, unsigned* amax, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && pool, "srpde_bn_relu_pool_fwd: null");
+  SRPDE_CHECK_ARG(C % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0 && ldp % 4 == 0 && h % 2 == 0 && w % 2 == 0,
+                  "srpde_bn_relu_pool_fwd: C / ld must be multiples of 4, h and w even");
+  const long long total = (long long)n * (h / 2) * (w / 2) * (C / 4);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, amax ? 1024 : 8192);
+  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
+                     out, ldo, pool, ldp, n, h, w, C, relu, amax);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_pool_fwd");
   return 0;
 }
 

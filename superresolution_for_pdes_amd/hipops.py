@@ -407,6 +407,17 @@ def bn_relu_fwd(y, mean, invstd, gamma, beta, out, relu=True, amax=None):
     tag_amax(out, amax)
 
 
+def bn_relu_pool_fwd(y, mean, invstd, gamma, beta, out, pool, n, h, w, relu=True, amax=None):
+    """bn_relu_fwd into ``out`` and maxpool_fwd of it into ``pool`` in one pass."""
+    py, ldy = _pl(y)
+    po, ldo = _pl(out)
+    pp, ldp = _pl(pool)
+    call("srpde_bn_relu_pool_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         po, ldo, pp, ldp, n, h, w, y.shape[1], int(relu), _p(amax), stream_ptr())
+    tag_amax(out, amax)
+    tag_amax(pool, amax)
+
+
 BN_RELU, BN_EVAL = 1, 2   # srpde_bn_relu_bwd flags (include/srpde.h)
 
 

@@ -182,12 +182,14 @@ def _splits_both_ways(c0, c1, cout, w, dil):
     return H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(cout, 0, c0 + c1, w, dil)
 
 
-def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True):
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False):
     """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48).
 
     ``activate=False`` (train mode): stop after the BN statistics and return the conv output y
     with the (scale, shift) that a fused consumer applies (``in_affine``) instead of a
-    materialised relu(bn(y)); y carries the rigorous max|relu(bn(y))| bound as its amax word."""
+    materialised relu(bn(y)); y carries the rigorous max|relu(bn(y))| bound as its amax word.
+    ``pool``: also return the 2x2 max-pool of the activation, formed in the same pass
+    (srpde_bn_relu_pool_fwd): ((a, pooled), saved)."""
     dev = x0.device
     cout = conv.out_channels
     c1 = x1.shape[1] if x1 is not None else 0
@@ -218,8 +220,18 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         y._srpde_amax = slot
         return (y, aff), saved
     a = H.empty(P, cout, device=dev)
+    if pool and _FUSE_POOL:
+        pooled = H.empty(n * (h // 2) * (w // 2), cout, device=dev)
+        H.bn_relu_pool_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w, amax=slots.take())
+        return (a, pooled), saved
     H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
+    if pool:
+        return (a, H.maxpool_fwd(a, n, h, w)), saved
     return a, saved
+
+
+# a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
+_FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
 
 
 class WgradStream:
@@ -409,20 +421,20 @@ def _fuse_pair(conv2, training, w, dil):
     return training and _splits_both_ways(conv2.in_channels, 0, conv2.out_channels, w, dil)
 
 
-def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots):
+def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False):
     """conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU, with the middle BN + ReLU fused into conv2's
     input transform when possible (saves a read and a write of the middle activation)."""
     if _fuse_pair(conv2, training, w, dil):
         (y1, aff), s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots, activate=False)
-        a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff)
+        a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff, pool=pool)
         return a2, (s1, s2)
     a1, s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots)
-    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots)
+    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool)
     return a2, (s1, s2)
 
 
-def _block_fwd(blk, x0, x1, n, h, w, training, slots):
-    return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots)
+def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False):
+    return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots, pool=pool)
 
 
 def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
@@ -512,12 +524,10 @@ def unet_forward(m, x, training, save=False):
     prepare_h3_weights(m)
     slots = H.AmaxSlots(16, x.device)   # max|x| words of the 16 BN+ReLU outputs (h3 operand scales)
     # encoder
-    e1, S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots)
+    (e1, p1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True)
     ch1 = _att_channel_early(m.att1, e1, n, hw1)
-    p1 = H.maxpool_fwd(e1, n, h, w)
-    e2, S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots)
+    (e2, p2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True)
     ch2 = _att_channel_early(m.att2, e2, n, hw2)
-    p2 = H.maxpool_fwd(e2, n, h2, w2)
     e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots)
     ch3 = _att_channel_early(m.att3, e3, n, hw3)
     # bridge (dilated)

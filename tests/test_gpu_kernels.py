@@ -547,3 +547,26 @@ def test_first_conv_direct_matches_fp64(n, h, w):
         m2 = ((blk - mean) ** 2).sum(0)
         assert float((st[k, :, 0] - mean).abs().max()) <= 1e-5 * float(blk.abs().max())
         assert float((st[k, :, 1] - m2).abs().max()) <= 1e-5 * float(m2.abs().max()) + 1e-6
+
+
+@pytest.mark.parametrize("n,h,w,c", [(3, 40, 40, 64), (2, 20, 6, 128)])
+def test_bn_relu_pool_equals_separate_passes(n, h, w, c):
+    """srpde_bn_relu_pool_fwd (a block output's BN + ReLU with its 2x2 max-pool in one pass) gives
+    the same bits as srpde_bn_relu_fwd then srpde_maxpool2x2_fwd, ReLU-zero ties included, and the
+    same max|out| word."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(c + h)
+    P = n * h * w
+    y = torch.randn(P, c, generator=g).to(DEV)
+    mean, invstd = y.mean(0), 1.0 / torch.sqrt(y.var(0) + 1e-5)
+    gam, bet = (torch.rand(c, generator=g) + 0.5).to(DEV), torch.randn(c, generator=g).to(DEV)
+    slots = H.AmaxSlots(2, DEV)
+    a1, a2 = H.empty(P, c, device=DEV), H.empty(P, c, device=DEV)
+    H.bn_relu_fwd(y, mean, invstd, gam, bet, a1, amax=slots.take())
+    p1 = H.maxpool_fwd(a1, n, h, w)
+    p2 = H.empty(P // 4, c, device=DEV)
+    H.bn_relu_pool_fwd(y, mean, invstd, gam, bet, a2, p2, n, h, w, amax=slots.take())
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2) and torch.equal(p1, p2)
+    words = slots.buf.cpu()
+    assert int(words[0]) == int(words[1])
