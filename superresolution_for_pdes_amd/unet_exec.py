@@ -230,6 +230,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     return a, saved
 
 
+_FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
 # a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
 _FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
 
@@ -421,20 +422,24 @@ def _fuse_pair(conv2, training, w, dil):
     return training and _splits_both_ways(conv2.in_channels, 0, conv2.out_channels, w, dil)
 
 
-def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False):
+def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False, activate=True):
     """conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU, with the middle BN + ReLU fused into conv2's
     input transform when possible (saves a read and a write of the middle activation)."""
     if _fuse_pair(conv2, training, w, dil):
         (y1, aff), s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots, activate=False)
-        a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff, pool=pool)
+        a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff, pool=pool,
+                          activate=activate)
         return a2, (s1, s2)
     a1, s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots)
-    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool)
+    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool, activate=activate)
     return a2, (s1, s2)
 
 
-def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False):
-    return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots, pool=pool)
+def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True):
+    """``activate=False`` (train mode): the block's output BN + ReLU is left to a fused consumer,
+    which gets ((y, (scale, shift)), saved) as from _cbr_fwd(activate=False)."""
+    return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots, pool=pool,
+                     activate=activate)
 
 
 def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
@@ -541,9 +546,14 @@ def unet_forward(m, x, training, save=False):
     d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
     u2 = H.upsample_fwd(d2, n, h2, w2, h, w)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1)
-    d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots)
-    # multi-scale head + residual
-    o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots)
+    # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
+    # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)
+    if _FUSE_D1 and _fuse_pair(m.out_conv1, training, w, 1):
+        (d1y, d1aff), S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots, activate=False)
+        o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1y, None, n, h, w, training, 1, slots, in_affine=d1aff)
+    else:
+        d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots)
+        o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots)
     o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots)
     out = H.head_fwd(o2, m.final.weight, m.final.bias, x, n, hw1)
     if not save:
