@@ -261,6 +261,11 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
  * dg[q][c] += dsa[q] * wg[c] (models.py:116, srpde_att_bwd called with dg == NULL leaves dsa in
  * workspace[0, P)) folded into the upsample backward that consumes dg (models.py:89,92), so the
  * gating gradient is never written.  Needs c / 4 a power of two <= 256. */
+/* relu(y * scale + shift) (the train-mode BN + ReLU as srpde_bn_affine's per-channel affine) upsampled
+ * x2 with align_corners in one pass, the activation never written (models.py:22-23 then :89,92);
+ * amax (nullable, zeroed beforehand): receives max|out|. */
+int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, const float* shift, float* out, int ldo,
+                               int n, int h, int w, int ho, int wo, int c, unsigned* amax, hipStream_t stream);
 int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
                                       int lddx, int n, int h, int w, int ho, int wo, int c, int accumulate,
                                       hipStream_t stream);

@@ -488,6 +488,17 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
 
 
+def bn_relu_upsample_fwd(y, aff, n, h, w, ho, wo, amax=None):
+    """upsample_fwd(relu(y * scale + shift)) with ``aff = (scale, shift)`` (bn_affine), one pass."""
+    c = y.shape[1]
+    out = empty(n * ho * wo, c, device=y.device)
+    py, ldy = _pl(y)
+    po, ldo = _pl(out)
+    call("srpde_bn_relu_upsample_fwd", py, ldy, aff[0].data_ptr(), aff[1].data_ptr(), po, ldo, n, h, w, ho, wo, c,
+         _p(amax), stream_ptr())
+    return tag_amax(out, amax)
+
+
 def resize_bicubic(x, ho, wo):
     """F.interpolate(mode='bicubic', align_corners=True) of single-channel fields: x [planes, h, w]
     contiguous fp32 -> [planes, ho, wo] (srpde_resize_bicubic_ac)."""
