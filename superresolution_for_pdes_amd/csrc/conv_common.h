@@ -96,20 +96,23 @@ __device__ __forceinline__ unsigned lds_addr_of(const void* p) {
 // and the same per-row-block BN partials (mean, M2) the main epilogue writes.
 // SRB = rows per BN-statistics block (srpde_conv_stats_rows_per_block); a tile of BM rows
 // writes BM / SRB statistics rows.
-template <int BM, int BN, int SRB = BM>
+// BMB: rows of the tile one block finishes (BM, or SRB with blockIdx.y the statistics sub-block: twice
+// the blocks for the same work when the tail has few tiles; needs out_max == nullptr)
+template <int BM, int BN, int SRB = BM, int BMB = BM>
 __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
   constexpr int CQ = BN / 4;          // column quads
   constexpr int G = 1024 / CQ;        // row groups
-  constexpr int RPT = BM / G;         // rows per thread
-  constexpr int NSB = BM / SRB;       // statistics sub-blocks per tile
-  static_assert(RPT >= 1 && BM % G == 0, "fixup geometry");
-  static_assert(BM % SRB == 0 && SRB % G == 0, "fixup statistics geometry");
+  constexpr int RPT = BMB / G;        // rows per thread
+  constexpr int NSB = BMB / SRB;      // statistics sub-blocks per block
+  static_assert(RPT >= 1 && BMB % G == 0 && BM % BMB == 0, "fixup geometry");
+  static_assert(BMB % SRB == 0 && SRB % G == 0, "fixup statistics geometry");
   __shared__ float4 red[G][CQ];
   const int nbn = (p.Cout + BN - 1) / BN, nbm = (p.P + BM - 1) / BM;
   const int nfull = nbm * nbn - p.ntail;
   const int wg = nfull + blockIdx.x;
   const int mt = wg / nbn, nt = wg - mt * nbn;
-  const int m0 = mt * BM, n0 = nt * BN;
+  const int rbase = blockIdx.y * BMB;  // first tile row of this block
+  const int m0 = mt * BM + rbase, n0 = nt * BN;
   const int cq = threadIdx.x % CQ, g = threadIdx.x / CQ;
   const int col = n0 + cq * 4;
   const bool cok = col < p.Cout;  // Cout % 4 == 0
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
     const int r = g + i * G;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int k = 0; k < p.tsplit; ++k) {
-      const float4 q = *reinterpret_cast<const float4*>(src + (size_t)k * (BM * BN) + r * BN + cq * 4);
+      const float4 q = *reinterpret_cast<const float4*>(src + (size_t)k * (BM * BN) + (rbase + r) * BN + cq * 4);
       a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
     }
     a.x += bias.x; a.y += bias.y; a.z += bias.z; a.w += bias.w;
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
     }
   }
   constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
-  if (p.out_max != nullptr) {         // max|out| of this tile -> its slot
+  if (BMB == BM && p.out_max != nullptr) {   // max|out| of this tile -> its slot (whole-tile blocks only)
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < RPT; ++i)

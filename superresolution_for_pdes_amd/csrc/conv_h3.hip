@@ -1718,6 +1718,24 @@ static int h3_half_max() {
   return v;
 }
 
+// the K-split tail's fixup: one block per statistics sub-block of each tail tile (twice the blocks of a
+// whole-tile fixup for the same work: the tail has few tiles) unless the per-tile max|out| slot is
+// wanted (SRPDE_FIXUP_SPLIT=0: whole tiles)
+template <int BM, int BN, int SRB>
+static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
+  static const bool split = [] { const char* e = getenv("SRPDE_FIXUP_SPLIT"); return !(e && e[0] == '0'); }();
+  if constexpr (BM > SRB) {
+    if (split && p.out_max == nullptr) {
+      hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB, SRB>), dim3(p.ntail, BM / SRB), dim3(1024), 0, st, p);
+      SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
+      return 0;
+    }
+  }
+  hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
+  return 0;
+}
+
 static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false) {
   return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 128 + 1024;
 }
@@ -1755,10 +1773,7 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, BNB>), dim3(grid), dim3(NT), lds, st, p,
                      h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
-  if (p.ntail > 0) {
-    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
-    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
-  }
+  if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
   return 0;
 }
 
@@ -1809,10 +1824,7 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
   const int grid = T - p.ntail + p.ntail * p.tsplit;
   hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB, BNB>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
-  if (p.ntail > 0) {
-    hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
-    SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r tail fixup)");
-  }
+  if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
   return 0;
 }
 
