@@ -266,6 +266,14 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
  * amax (nullable, zeroed beforehand): receives max|out|. */
 int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, const float* shift, float* out, int ldo,
                                int n, int h, int w, int ho, int wo, int c, unsigned* amax, hipStream_t stream);
+/* srpde_upsample_bilinear_fwd that also forms the spatial attention of the gate reading the result
+ * (models.py:124-125, 89/92): sa[q] = sigmoid(sum_c wg[c] out[q][c] + bg[0]).  c / 4 a power of two
+ * <= 64.  With srpde_att_channel_fwd's ca, srpde_att_apply_fwd then finishes the gate. */
+int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho,
+                                      int wo, int c, const float* wg, const float* bg, float* sa, hipStream_t stream);
+/* out[p][c] = x[p][c] * ca[n][c] * sa[p] (models.py:122, 128) */
+int srpde_att_apply_fwd(const float* x, int ldx, int n, int hw, int c, const float* ca, const float* sa, float* out,
+                        int ldo, hipStream_t stream);
 int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
                                       int lddx, int n, int h, int w, int ho, int wo, int c, int accumulate,
                                       hipStream_t stream);

@@ -387,6 +387,38 @@ __global__ __launch_bounds__(256) void bn_relu_upsample_fwd_kernel(const float* 
   if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
 
+// upsample_fwd_px_kernel plus the spatial attention of the gate that reads the upsampled tensor
+// (models.py:124-125: sa = sigmoid(conv1x1(g)) with g = up(d), models.py:89,92): the block's x
+// threads hold one output pixel's channels, so the 1x1 conv is a shuffle reduction over them and g
+// is not re-read for it.  c / 4 a power of two <= 64 (one pixel per half or whole wave).
+__global__ __launch_bounds__(256) void upsample_gate_fwd_px_kernel(const float* __restrict__ x, int ldx,
+                                                                   float* __restrict__ out, int ldo, unsigned npix,
+                                                                   int H, int W, int Ho, int Wo,
+                                                                   const float* __restrict__ wg,
+                                                                   const float* __restrict__ bg,
+                                                                   float* __restrict__ sa) {
+  const unsigned q = px_index();
+  const bool on = q < npix;
+  const unsigned qq = on ? q : 0;
+  const unsigned ox = qq % (unsigned)Wo, t = qq / (unsigned)Wo, oy = t % (unsigned)Ho, n = t / (unsigned)Ho;
+  const int c = threadIdx.x * 4;
+  const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
+  const float* base = x + (size_t)n * H * W * ldx + c;
+  const float4 a = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i0) * ldx);
+  const float4 b = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i1) * ldx);
+  const float4 d = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i0) * ldx);
+  const float4 f = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i1) * ldx);
+  float4 o;
+#define UP(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
+  UP(x) UP(y) UP(z) UP(w)
+#undef UP
+  if (on) *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
+  const float4 wv = *reinterpret_cast<const float4*>(wg + c);
+  float acc = o.x * wv.x + o.y * wv.y + o.z * wv.z + o.w * wv.w;
+  for (int off = 1; off < (int)blockDim.x; off <<= 1) acc += __shfl_xor(acc, off, 64);
+  if (on && threadIdx.x == 0) sa[q] = 1.f / (1.f + expf(-(acc + bg[0])));
+}
+
 // gsa / gw (nullable): the attention gating gradient folded in, the upsampled tensor's gradient
 // being dout[q][c] + gsa[q] * gw[c] (srpde_upsample_bilinear_bwd_gated)
 __global__ __launch_bounds__(256) void upsample_bwd_px_kernel(const float* __restrict__ dout, int lddo,
@@ -1162,6 +1194,28 @@ int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, cons
   hipLaunchKernelGGL(bn_relu_upsample_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, scale, shift, out, ldo,
                      n, h, w, ho, wo, c, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_upsample_fwd");
+  return 0;
+}
+
+int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho,
+                                      int wo, int c, const float* wg, const float* bg, float* sa, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && out && wg && bg && sa && ldx % 4 == 0 && ldo % 4 == 0 && c % 4 == 0 && c / 4 <= 64,
+                  "srpde_upsample_bilinear_gate_fwd: bad args (c / 4 a power of two <= 64)");
+  dim3 g, b;
+  SRPDE_CHECK_ARG(px_geometry((long long)n * ho * wo, c, &g, &b), "srpde_upsample_bilinear_gate_fwd: bad geometry");
+  hipLaunchKernelGGL(upsample_gate_fwd_px_kernel, g, b, 0, stream, x, ldx, out, ldo, (unsigned)(n * ho * wo), h, w,
+                     ho, wo, wg, bg, sa);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_gate_fwd");
+  return 0;
+}
+
+int srpde_att_apply_fwd(const float* x, int ldx, int n, int hw, int c, const float* ca, const float* sa, float* out,
+                        int ldo, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && ca && sa && out && c % 4 == 0, "srpde_att_apply_fwd: bad args");
+  const long long P = (long long)n * hw;
+  hipLaunchKernelGGL(att_apply_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, x, ldx, ca, sa, out, ldo,
+                     P, hw, c);
+  SRPDE_LAUNCH_CHECK("srpde_att_apply_fwd");
   return 0;
 }
 

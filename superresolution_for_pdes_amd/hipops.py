@@ -499,6 +499,32 @@ def bn_relu_upsample_fwd(y, aff, n, h, w, ho, wo, amax=None):
     return tag_amax(out, amax)
 
 
+def upsample_gate_fwd(x, n, h, w, ho, wo, wg, bg):
+    """upsample_fwd plus the spatial attention of the gate that reads it -> (out, sa)."""
+    c = x.shape[1]
+    out = empty(n * ho * wo, c, device=x.device)
+    sa = empty(n * ho * wo, device=x.device)
+    px, ldx = _pl(x)
+    po, ldo = _pl(out)
+    call("srpde_upsample_bilinear_gate_fwd", px, ldx, po, ldo, n, h, w, ho, wo, c, wg.data_ptr(), bg.data_ptr(),
+         sa.data_ptr(), stream_ptr())
+    return tag_amax(out, getattr(x, "_srpde_amax", None)), sa
+
+
+def att_apply_fwd(x, n, hw, chan, sa, out=None):
+    """The gate's output from att_channel_fwd's ``chan`` and a precomputed spatial attention ``sa``.
+    Returns (out, saved) as att_fwd."""
+    m, hb, ca = chan
+    c = x.shape[1]
+    if out is None:
+        out = empty(n * hw, c, device=x.device)
+    px, ldx = _pl(x)
+    po, ldo = _pl(out)
+    call("srpde_att_apply_fwd", px, ldx, n, hw, c, ca.data_ptr(), sa.data_ptr(), po, ldo, stream_ptr())
+    tag_amax(out, getattr(x, "_srpde_amax", None))
+    return out, (m, hb, ca, sa)
+
+
 def resize_bicubic(x, ho, wo):
     """F.interpolate(mode='bicubic', align_corners=True) of single-channel fields: x [planes, h, w]
     contiguous fp32 -> [planes, ho, wo] (srpde_resize_bicubic_ac)."""

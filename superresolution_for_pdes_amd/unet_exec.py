@@ -232,6 +232,9 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
 
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
 _FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "0") == "1"
+# the gates' spatial attention formed by the upsample that produces their gating input
+# (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
+_FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
 # a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
 _FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
 
@@ -458,15 +461,26 @@ def _att_params(att):
     return c1, c3, s0
 
 
-def _att_fwd(att, x, g, n, hw, early=None):
-    """``early``: the gate's channel attention already launched by _att_channel_early."""
+def _att_fwd(att, x, g, n, hw, early=None, sa=None):
+    """``early``: the gate's channel attention already launched by _att_channel_early; ``sa``: its
+    spatial attention already formed by the upsample that produced ``g`` (upsample_gate_fwd)."""
     c1, c3, s0 = _att_params(att)
     if early is None:
         return H.att_fwd(x, g, n, hw, c1.weight, c1.bias, c3.weight, c3.bias, s0.weight, s0.bias)
     chan, ev = early
     if ev is not None:
         torch.cuda.current_stream(x.device).wait_event(ev)
+    if sa is not None:
+        return H.att_apply_fwd(x, n, hw, chan, sa)
     return H.att_gate_fwd(x, g, n, hw, chan, s0.weight, s0.bias)
+
+
+def _upsample_for_gate(d, att, n, h, w, ho, wo):
+    """up(d) for the decoder, and (SRPDE_FUSE_SA) the spatial attention of ``att`` whose gate it is."""
+    if _FUSE_SA and d.shape[1] in (128, 256) and d.is_cuda:
+        s0 = att.spatial_attention[0]
+        return H.upsample_gate_fwd(d, n, h, w, ho, wo, s0.weight, s0.bias)
+    return H.upsample_fwd(d, n, h, w, ho, wo), None
 
 
 # SRPDE_ATT_EARLY=1: the attention gates' channel attention (models.py:119-121: a function of the
@@ -546,18 +560,18 @@ def unet_forward(m, x, training, save=False):
     # (train mode; d3 / d2 never written) -- measured step-neutral (33.02 vs 33.03 ms, 4 reps), off
     if training and _FUSE_UP:
         (d3y, d3aff), S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots, activate=False)
-        u3 = H.bn_relu_upsample_fwd(d3y, d3aff, n, h3, w3, h2, w2, amax=slots.take())
+        u3, sa2 = H.bn_relu_upsample_fwd(d3y, d3aff, n, h3, w3, h2, w2, amax=slots.take()), None
     else:
         d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
-        u3 = H.upsample_fwd(d3, n, h3, w3, h2, w2)
-    e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2)
+        u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2)
+    e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2, sa=sa2)
     if training and _FUSE_UP:
         (d2y, d2aff), S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots, activate=False)
-        u2 = H.bn_relu_upsample_fwd(d2y, d2aff, n, h2, w2, h, w, amax=slots.take())
+        u2, sa1 = H.bn_relu_upsample_fwd(d2y, d2aff, n, h2, w2, h, w, amax=slots.take()), None
     else:
         d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
-        u2 = H.upsample_fwd(d2, n, h2, w2, h, w)
-    e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1)
+        u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w)
+    e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1, sa=sa1)
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
     # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)
     if _FUSE_D1 and _fuse_pair(m.out_conv1, training, w, 1):
