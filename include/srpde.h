@@ -185,6 +185,13 @@ int srpde_bn_relu_fwd(const float* y, int ldy, const float* mean, const float* i
 int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                            const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w, int C,
                            int relu, unsigned* amax, hipStream_t stream);
+/* srpde_bn_relu_pool_fwd (ReLU always) with one block per sample, which also forms the channel branch
+ * of the AttentionGate reading the activation (models.py:106-112, 119-121; as srpde_att_channel_fwd:
+ * m [n][C], hbuf [n][C/8], ca [n][C]).  C a multiple of 32, <= 256. */
+int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                               const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
+                               int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
+                               const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream);
 /* train-mode BN folded into a per-channel affine for a consumer that applies it on the fly
  * (a = relu(y*scale + shift), srpde_conv_fwd_h3's in_scale / in_shift), plus a rigorous bound
  * on max|a| (|gamma| sqrt(P-1) + |beta|, Samuelson's inequality) into *amax_bound (nullable) */

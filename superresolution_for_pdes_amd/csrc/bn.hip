@@ -441,6 +441,81 @@ __global__ __launch_bounds__(256) void bn_relu_pool_fwd_kernel(const float* __re
   if (amax) block_amax(mx, amax);
 }
 
+// bn_relu_pool_fwd_kernel for one sample per block, which also forms the attention gate's channel
+// branch of the activation (models.py:106-112, 119-121: m = mean over the pixels, h = relu(W1 m + b1),
+// ca = sigmoid(W2 h + b2), as att_channel_fwd_kernel) from the sums of the values it writes, so the
+// activation is not re-read for it.  C / 4 divides 256; Cr = C / 8.
+__global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
+    const float* __restrict__ y, int ldy, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ out, int ldo,
+    float* __restrict__ pool, int ldp, int H, int W, int C, unsigned* amax, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ mo,
+    float* __restrict__ ho, float* __restrict__ cao) {
+  __shared__ float4 red4[256];
+  __shared__ float ms[256], hs[32];
+  const int nb = blockIdx.x, C4 = C >> 2, Wo = W >> 1, Ho = H >> 1, Cr = C >> 3;
+  const int c4 = threadIdx.x % C4, rs = 256 / C4, c = 4 * c4;
+  const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+  const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+  const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+  const float4 b = *reinterpret_cast<const float4*>(beta + c);
+  float mx = 0.f;
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  const long long pbase = (long long)nb * H * W;
+  for (int q = threadIdx.x / C4; q < Ho * Wo; q += rs) {
+    const int oy = q / Wo, ox = q - oy * Wo;
+    const long long p00 = pbase + (long long)(2 * oy) * W + 2 * ox;
+    const long long pp[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    float4 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(y + pp[k] * ldy + c);
+      float4 r;
+      r.x = fmaxf((v.x - mu.x) * is.x * g.x + b.x, 0.f);
+      r.y = fmaxf((v.y - mu.y) * is.y * g.y + b.y, 0.f);
+      r.z = fmaxf((v.z - mu.z) * is.z * g.z + b.z, 0.f);
+      r.w = fmaxf((v.w - mu.w) * is.w * g.w + b.w, 0.f);
+      *reinterpret_cast<float4*>(out + pp[k] * ldo + c) = r;
+      mx = fmaxf(mx, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
+      sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+      o[k] = r;
+    }
+    float4 m;
+#define MX(X) { float v = o[0].X; if (o[1].X > v) v = o[1].X; if (o[2].X > v) v = o[2].X; if (o[3].X > v) v = o[3].X; m.X = v; }
+    MX(x) MX(y) MX(z) MX(w)
+#undef MX
+    *reinterpret_cast<float4*>(pool + ((long long)nb * Ho * Wo + q) * ldp + c) = m;
+  }
+  if (amax) block_amax(mx, amax);
+  red4[threadIdx.x] = sum;
+  __syncthreads();
+  if ((int)threadIdx.x < C4) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red4[r * C4 + threadIdx.x];
+      t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+    }
+    const float inv = 1.f / (float)(H * W);
+    const int cc = threadIdx.x * 4;
+    ms[cc] = t.x * inv; ms[cc + 1] = t.y * inv; ms[cc + 2] = t.z * inv; ms[cc + 3] = t.w * inv;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) mo[(long long)nb * C + j] = ms[j];
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float a = b1[r];
+    for (int cc = 0; cc < C; ++cc) a += w1[r * C + cc] * ms[cc];
+    a = fmaxf(a, 0.f);
+    hs[r] = a;
+    ho[(long long)nb * Cr + r] = a;
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += blockDim.x) {
+    float a = b2[cc];
+    for (int r = 0; r < Cr; ++r) a += w2[cc * Cr + r] * hs[r];
+    cao[(long long)nb * C + cc] = 1.f / (1.f + expf(-a));
+  }
+}
+
 static int bwd_blocks(long long P, int C, int* rows_per_blk) {
   // ~1024 blocks; rows per block a multiple of the rows a block covers per sweep
   const int rs = 256 / (C >> 2);
@@ -502,6 +577,21 @@ int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const flo
   hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
                      out, ldo, pool, ldp, n, h, w, C, relu, amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_pool_fwd");
+  return 0;
+}
+
+int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                               const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
+                               int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
+                               const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && pool && w1 && b1 && w2 && b2 && m && hbuf && ca,
+                  "srpde_bn_relu_pool_att_fwd: null");
+  SRPDE_CHECK_ARG(C % 32 == 0 && C <= 256 && 256 % (C / 4) == 0 && ldy % 4 == 0 && ldo % 4 == 0 && ldp % 4 == 0 &&
+                      h % 2 == 0 && w % 2 == 0,
+                  "srpde_bn_relu_pool_att_fwd: C a multiple of 32 <= 256, ld multiples of 4, h and w even");
+  hipLaunchKernelGGL(bn_relu_pool_att_fwd_kernel, dim3(n), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
+                     out, ldo, pool, ldp, h, w, C, amax, w1, b1, w2, b2, m, hbuf, ca);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_pool_att_fwd");
   return 0;
 }
 

@@ -182,14 +182,16 @@ def _splits_both_ways(c0, c1, cout, w, dil):
     return H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(cout, 0, c0 + c1, w, dil)
 
 
-def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False):
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False, att=None):
     """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48).
 
     ``activate=False`` (train mode): stop after the BN statistics and return the conv output y
     with the (scale, shift) that a fused consumer applies (``in_affine``) instead of a
     materialised relu(bn(y)); y carries the rigorous max|relu(bn(y))| bound as its amax word.
     ``pool``: also return the 2x2 max-pool of the activation, formed in the same pass
-    (srpde_bn_relu_pool_fwd): ((a, pooled), saved)."""
+    (srpde_bn_relu_pool_fwd): ((a, pooled), saved).  With ``att`` (the AttentionGate that reads a)
+    also its channel branch, from the same pass when possible (srpde_bn_relu_pool_att_fwd):
+    ((a, pooled, early), saved), ``early`` as _att_channel_early returns it."""
     dev = x0.device
     cout = conv.out_channels
     c1 = x1.shape[1] if x1 is not None else 0
@@ -222,12 +224,20 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     a = H.empty(P, cout, device=dev)
     if pool and _FUSE_POOL:
         pooled = H.empty(n * (h // 2) * (w // 2), cout, device=dev)
+        if att is not None and _FUSE_ATT_CH and cout % 32 == 0 and cout <= 256:
+            c1, c3, _ = _att_params(att)
+            chan = H.bn_relu_pool_att_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w,
+                                          (c1.weight, c1.bias, c3.weight, c3.bias), amax=slots.take())
+            return (a, pooled, (chan, None)), saved
         H.bn_relu_pool_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w, amax=slots.take())
+    else:
+        H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
+        if not pool:
+            return a, saved
+        pooled = H.maxpool_fwd(a, n, h, w)
+    if att is None:
         return (a, pooled), saved
-    H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
-    if pool:
-        return (a, H.maxpool_fwd(a, n, h, w)), saved
-    return a, saved
+    return (a, pooled, _att_channel_early(att, a, n, h * w)), saved
 
 
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
@@ -235,6 +245,9 @@ _FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "0") == "1"
 # the gates' spatial attention formed by the upsample that produces their gating input
 # (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
 _FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
+# enc1's / enc2's gate channel branch from the BN + ReLU + pool pass (srpde_bn_relu_pool_att_fwd, one
+# block per sample; SRPDE_FUSE_ATT_CH=0: a separate pass over the activation)
+_FUSE_ATT_CH = os.environ.get("SRPDE_FUSE_ATT_CH", "1") != "0"
 # a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
 _FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
 
@@ -426,24 +439,24 @@ def _fuse_pair(conv2, training, w, dil):
     return training and _splits_both_ways(conv2.in_channels, 0, conv2.out_channels, w, dil)
 
 
-def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False, activate=True):
+def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False, activate=True, att=None):
     """conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU, with the middle BN + ReLU fused into conv2's
     input transform when possible (saves a read and a write of the middle activation)."""
     if _fuse_pair(conv2, training, w, dil):
         (y1, aff), s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots, activate=False)
         a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff, pool=pool,
-                          activate=activate)
+                          activate=activate, att=att)
         return a2, (s1, s2)
     a1, s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots)
-    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool, activate=activate)
+    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool, activate=activate, att=att)
     return a2, (s1, s2)
 
 
-def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True):
+def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True, att=None):
     """``activate=False`` (train mode): the block's output BN + ReLU is left to a fused consumer,
     which gets ((y, (scale, shift)), saved) as from _cbr_fwd(activate=False)."""
     return _pair_fwd(blk.conv1, blk.bn1, blk.conv2, blk.bn2, x0, x1, n, h, w, training, 1, slots, pool=pool,
-                     activate=activate)
+                     activate=activate, att=att)
 
 
 def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
@@ -545,10 +558,8 @@ def unet_forward(m, x, training, save=False):
     # max|x| words of the 16 BN+ReLU outputs and the 2 fused upsamples (h3 operand scales)
     slots = H.AmaxSlots(18, x.device)
     # encoder
-    (e1, p1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True)
-    ch1 = _att_channel_early(m.att1, e1, n, hw1)
-    (e2, p2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True)
-    ch2 = _att_channel_early(m.att2, e2, n, hw2)
+    (e1, p1, ch1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True, att=m.att1)
+    (e2, p2, ch2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True, att=m.att2)
     e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots)
     ch3 = _att_channel_early(m.att3, e3, n, hw3)
     # bridge (dilated)

@@ -570,3 +570,29 @@ def test_bn_relu_pool_equals_separate_passes(n, h, w, c):
     assert torch.equal(a1, a2) and torch.equal(p1, p2)
     words = slots.buf.cpu()
     assert int(words[0]) == int(words[1])
+
+
+@pytest.mark.parametrize("n,h,w,c", [(3, 40, 40, 64), (2, 20, 20, 128)])
+def test_bn_relu_pool_att_matches_separate_passes(n, h, w, c):
+    """srpde_bn_relu_pool_att_fwd: the activation and its pool bit-equal to srpde_bn_relu_pool_fwd, and
+    the attention channel branch (m, h, ca) equal to srpde_att_channel_fwd of the activation to fp32
+    summation order (<= 1e-6 relative)."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(c * 3 + h)
+    P = n * h * w
+    y = torch.randn(P, c, generator=g).to(DEV)
+    mean, invstd = y.mean(0), 1.0 / torch.sqrt(y.var(0) + 1e-5)
+    gam, bet = (torch.rand(c, generator=g) + 0.5).to(DEV), torch.randn(c, generator=g).to(DEV)
+    w1 = (torch.randn(c // 8, c, generator=g) * 0.2).to(DEV)
+    b1 = (torch.randn(c // 8, generator=g) * 0.1).to(DEV)
+    w2 = (torch.randn(c, c // 8, generator=g) * 0.2).to(DEV)
+    b2 = (torch.randn(c, generator=g) * 0.1).to(DEV)
+    a1, a2 = H.empty(P, c, device=DEV), H.empty(P, c, device=DEV)
+    p1, p2 = H.empty(P // 4, c, device=DEV), H.empty(P // 4, c, device=DEV)
+    H.bn_relu_pool_fwd(y, mean, invstd, gam, bet, a1, p1, n, h, w)
+    m1, h1, ca1 = H.att_channel_fwd(a1, n, h * w, w1, b1, w2, b2)
+    m2, h2, ca2 = H.bn_relu_pool_att_fwd(y, mean, invstd, gam, bet, a2, p2, n, h, w, (w1, b1, w2, b2))
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2) and torch.equal(p1, p2)
+    for u, v in ((m1, m2), (h1, h2), (ca1, ca2)):
+        assert rel(v, u) < 1e-6, rel(v, u)
