@@ -187,7 +187,8 @@ int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const flo
                            int relu, unsigned* amax, hipStream_t stream);
 /* srpde_bn_relu_pool_fwd (ReLU always) with one block per sample, which also forms the channel branch
  * of the AttentionGate reading the activation (models.py:106-112, 119-121; as srpde_att_channel_fwd:
- * m [n][C], hbuf [n][C/8], ca [n][C]).  C a multiple of 32, <= 256. */
+ * m [n][C], hbuf [n][C/8], ca [n][C]).  C a multiple of 32, <= 256.  pool == NULL: no pooling (the
+ * activation and the channel branch only). */
 int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                                const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
                                int C, unsigned* amax, const float* w1, const float* b1, const float* w2,

@@ -445,6 +445,7 @@ __global__ __launch_bounds__(256) void bn_relu_pool_fwd_kernel(const float* __re
 // branch of the activation (models.py:106-112, 119-121: m = mean over the pixels, h = relu(W1 m + b1),
 // ca = sigmoid(W2 h + b2), as att_channel_fwd_kernel) from the sums of the values it writes, so the
 // activation is not re-read for it.  C / 4 divides 256; Cr = C / 8.
+template <bool POOL>
 __global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
     const float* __restrict__ y, int ldy, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ out, int ldo,
@@ -462,13 +463,19 @@ __global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
   float mx = 0.f;
   float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
   const long long pbase = (long long)nb * H * W;
-  for (int q = threadIdx.x / C4; q < Ho * Wo; q += rs) {
-    const int oy = q / Wo, ox = q - oy * Wo;
-    const long long p00 = pbase + (long long)(2 * oy) * W + 2 * ox;
-    const long long pp[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+  constexpr int NPX = POOL ? 4 : 1;   // pixels per work item: a pooling window, or one pixel
+  for (int q = threadIdx.x / C4; q < (POOL ? Ho * Wo : H * W); q += rs) {
+    long long pp[4];
+    if (POOL) {
+      const int oy = q / Wo, ox = q - oy * Wo;
+      const long long p00 = pbase + (long long)(2 * oy) * W + 2 * ox;
+      pp[0] = p00; pp[1] = p00 + 1; pp[2] = p00 + W; pp[3] = p00 + W + 1;
+    } else {
+      pp[0] = pbase + q;
+    }
     float4 o[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NPX; ++k) {
       const float4 v = *reinterpret_cast<const float4*>(y + pp[k] * ldy + c);
       float4 r;
       r.x = fmaxf((v.x - mu.x) * is.x * g.x + b.x, 0.f);
@@ -480,11 +487,13 @@ __global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
       sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
       o[k] = r;
     }
-    float4 m;
+    if (POOL) {
+      float4 m;
 #define MX(X) { float v = o[0].X; if (o[1].X > v) v = o[1].X; if (o[2].X > v) v = o[2].X; if (o[3].X > v) v = o[3].X; m.X = v; }
-    MX(x) MX(y) MX(z) MX(w)
+      MX(x) MX(y) MX(z) MX(w)
 #undef MX
-    *reinterpret_cast<float4*>(pool + ((long long)nb * Ho * Wo + q) * ldp + c) = m;
+      *reinterpret_cast<float4*>(pool + ((long long)nb * Ho * Wo + q) * ldp + c) = m;
+    }
   }
   if (amax) block_amax(mx, amax);
   red4[threadIdx.x] = sum;
@@ -584,13 +593,17 @@ int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const
                                const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
                                int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
                                const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream) {
-  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && pool && w1 && b1 && w2 && b2 && m && hbuf && ca,
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && w1 && b1 && w2 && b2 && m && hbuf && ca,
                   "srpde_bn_relu_pool_att_fwd: null");
-  SRPDE_CHECK_ARG(C % 32 == 0 && C <= 256 && 256 % (C / 4) == 0 && ldy % 4 == 0 && ldo % 4 == 0 && ldp % 4 == 0 &&
-                      h % 2 == 0 && w % 2 == 0,
+  SRPDE_CHECK_ARG(C % 32 == 0 && C <= 256 && 256 % (C / 4) == 0 && ldy % 4 == 0 && ldo % 4 == 0 &&
+                      (pool == nullptr || (ldp % 4 == 0 && h % 2 == 0 && w % 2 == 0)),
                   "srpde_bn_relu_pool_att_fwd: C a multiple of 32 <= 256, ld multiples of 4, h and w even");
-  hipLaunchKernelGGL(bn_relu_pool_att_fwd_kernel, dim3(n), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
-                     out, ldo, pool, ldp, h, w, C, amax, w1, b1, w2, b2, m, hbuf, ca);
+  if (pool)
+    hipLaunchKernelGGL(bn_relu_pool_att_fwd_kernel<true>, dim3(n), dim3(256), 0, stream, y, ldy, mean, invstd, gamma,
+                       beta, out, ldo, pool, ldp, h, w, C, amax, w1, b1, w2, b2, m, hbuf, ca);
+  else
+    hipLaunchKernelGGL(bn_relu_pool_att_fwd_kernel<false>, dim3(n), dim3(256), 0, stream, y, ldy, mean, invstd, gamma,
+                       beta, out, ldo, pool, ldp, h, w, C, amax, w1, b1, w2, b2, m, hbuf, ca);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_pool_att_fwd");
   return 0;
 }

@@ -426,13 +426,14 @@ def bn_relu_pool_att_fwd(y, mean, invstd, gamma, beta, out, pool, n, h, w, att_p
     m, hb, ca = empty(n, C, device=dev), empty(n, C // 8, device=dev), empty(n, C, device=dev)
     py, ldy = _pl(y)
     po, ldo = _pl(out)
-    pp, ldp = _pl(pool)
+    pp, ldp = _pl(pool) if pool is not None else (0, 0)
     w1, b1, w2, b2 = att_params
     call("srpde_bn_relu_pool_att_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
          beta.data_ptr(), po, ldo, pp, ldp, n, h, w, C, _p(amax), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
          b2.data_ptr(), m.data_ptr(), hb.data_ptr(), ca.data_ptr(), stream_ptr())
     tag_amax(out, amax)
-    tag_amax(pool, amax)
+    if pool is not None:
+        tag_amax(pool, amax)
     return m, hb, ca
 
 

@@ -230,10 +230,16 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
                                           (c1.weight, c1.bias, c3.weight, c3.bias), amax=slots.take())
             return (a, pooled, (chan, None)), saved
         H.bn_relu_pool_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w, amax=slots.take())
+    elif (not pool and att is not None and _FUSE_ATT_CH and cout % 32 == 0 and cout <= 256
+          and a.is_cuda and not torch.cuda.is_current_stream_capturing()):
+        c1, c3, _ = _att_params(att)
+        chan = H.bn_relu_pool_att_fwd(y, mean, invstd, bn.weight, bn.bias, a, None, n, h, w,
+                                      (c1.weight, c1.bias, c3.weight, c3.bias), amax=slots.take())
+        return (a, (chan, None)), saved
     else:
         H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
         if not pool:
-            return a, saved
+            return (a, _att_channel_early(att, a, n, h * w)) if att is not None else a, saved
         pooled = H.maxpool_fwd(a, n, h, w)
     if att is None:
         return (a, pooled), saved
@@ -560,8 +566,7 @@ def unet_forward(m, x, training, save=False):
     # encoder
     (e1, p1, ch1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True, att=m.att1)
     (e2, p2, ch2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True, att=m.att2)
-    e3, S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots)
-    ch3 = _att_channel_early(m.att3, e3, n, hw3)
+    (e3, ch3), S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots, att=m.att3)
     # bridge (dilated)
     b, (S.br1, S.br2) = _pair_fwd(m.bridge[0], m.bridge[1], m.bridge[3], m.bridge[4], e3, None, n, h3, w3,
                                   training, 2, slots)

@@ -596,3 +596,24 @@ def test_bn_relu_pool_att_matches_separate_passes(n, h, w, c):
     assert torch.equal(a1, a2) and torch.equal(p1, p2)
     for u, v in ((m1, m2), (h1, h2), (ca1, ca2)):
         assert rel(v, u) < 1e-6, rel(v, u)
+
+
+def test_bn_relu_att_unpooled_matches_separate_passes():
+    """srpde_bn_relu_pool_att_fwd without a pool (enc3's output: 256 channels at 10x10): the activation
+    bit-equal to srpde_bn_relu_fwd, the channel branch to fp32 summation order."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(11)
+    n, h, w, c = 3, 10, 10, 256
+    P = n * h * w
+    y = torch.randn(P, c, generator=g).to(DEV)
+    mean, invstd = y.mean(0), 1.0 / torch.sqrt(y.var(0) + 1e-5)
+    gam, bet = (torch.rand(c, generator=g) + 0.5).to(DEV), torch.randn(c, generator=g).to(DEV)
+    prm = tuple((torch.randn(*s, generator=g) * 0.2).to(DEV) for s in ((c // 8, c), (c // 8,), (c, c // 8), (c,)))
+    a1, a2 = H.empty(P, c, device=DEV), H.empty(P, c, device=DEV)
+    H.bn_relu_fwd(y, mean, invstd, gam, bet, a1)
+    ref = H.att_channel_fwd(a1, n, h * w, *prm)
+    got = H.bn_relu_pool_att_fwd(y, mean, invstd, gam, bet, a2, None, n, h, w, prm)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2)
+    for u, v in zip(ref, got):
+        assert rel(v, u) < 1e-6, rel(v, u)
