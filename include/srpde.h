@@ -193,6 +193,11 @@ int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const
                                const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
                                int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
                                const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream);
+/* srpde_bn_relu_fwd (ReLU) that also forms the spatial attention of the gate whose gating input the
+ * result is (models.py:124-125): sa[p] = sigmoid(sum_c wg[c] out[p][c] + bg[0]).  C 256, 512 or 1024. */
+int srpde_bn_relu_gate_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, float* out, int ldo, long long P, int C, const float* wg,
+                           const float* bg, float* sa, unsigned* amax, hipStream_t stream);
 /* train-mode BN folded into a per-channel affine for a consumer that applies it on the fly
  * (a = relu(y*scale + shift), srpde_conv_fwd_h3's in_scale / in_shift), plus a rigorous bound
  * on max|a| (|gamma| sqrt(P-1) + |beta|, Samuelson's inequality) into *amax_bound (nullable) */

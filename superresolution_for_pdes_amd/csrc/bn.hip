@@ -525,6 +525,56 @@ __global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
   }
 }
 
+// BN + ReLU of the bridge output with the spatial attention of the gate it drives (models.py:44-48,
+// 124-125: sa = sigmoid(conv1x1(b)) for att3, whose gating input b is): a pixel's channels are spread
+// over whole waves (C / 4 >= 64 threads), its 1x1 conv reduced by shuffles and across the waves in
+// LDS, so b is not re-read for it.  Few, long blocks for the max|out| atomic.
+__global__ __launch_bounds__(256) void bn_relu_gate_fwd_kernel(const float* __restrict__ y, int ldy,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float* __restrict__ out,
+                                                               int ldo, long long P, int C, const float* __restrict__ wg,
+                                                               const float* __restrict__ bg, float* __restrict__ sa,
+                                                               unsigned* amax) {
+  __shared__ float wred[4];
+  const int C4 = C >> 2, ppb = 256 / C4, wpp = C4 >> 6;
+  const int c = 4 * (threadIdx.x % C4), pl = threadIdx.x / C4, wave = threadIdx.x >> 6;
+  const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+  const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+  const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+  const float4 b = *reinterpret_cast<const float4*>(beta + c);
+  const float4 wv = *reinterpret_cast<const float4*>(wg + c);
+  const float bias = bg[0];
+  float mx = 0.f;
+  for (long long p0 = (long long)blockIdx.x * ppb; p0 < P; p0 += (long long)gridDim.x * ppb) {
+    const long long p = p0 + pl;
+    float dot = 0.f;
+    if (p < P) {
+      const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
+      float4 r;
+      r.x = fmaxf((v.x - mu.x) * is.x * g.x + b.x, 0.f);
+      r.y = fmaxf((v.y - mu.y) * is.y * g.y + b.y, 0.f);
+      r.z = fmaxf((v.z - mu.z) * is.z * g.z + b.z, 0.f);
+      r.w = fmaxf((v.w - mu.w) * is.w * g.w + b.w, 0.f);
+      *reinterpret_cast<float4*>(out + p * ldo + c) = r;
+      mx = fmaxf(mx, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
+      dot = r.x * wv.x + r.y * wv.y + r.z * wv.z + r.w * wv.w;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+    if ((threadIdx.x & 63) == 0) wred[wave] = dot;
+    __syncthreads();
+    if ((threadIdx.x % C4) == 0 && p < P) {
+      float t = 0.f;
+      for (int k = 0; k < wpp; ++k) t += wred[pl * wpp + k];
+      sa[p] = 1.f / (1.f + expf(-(t + bias)));
+    }
+    __syncthreads();
+  }
+  if (amax) block_amax(mx, amax);
+}
+
 static int bwd_blocks(long long P, int C, int* rows_per_blk) {
   // ~1024 blocks; rows per block a multiple of the rows a block covers per sweep
   const int rs = 256 / (C >> 2);
@@ -605,6 +655,20 @@ int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const
     hipLaunchKernelGGL(bn_relu_pool_att_fwd_kernel<false>, dim3(n), dim3(256), 0, stream, y, ldy, mean, invstd, gamma,
                        beta, out, ldo, pool, ldp, h, w, C, amax, w1, b1, w2, b2, m, hbuf, ca);
   SRPDE_LAUNCH_CHECK("srpde_bn_relu_pool_att_fwd");
+  return 0;
+}
+
+int srpde_bn_relu_gate_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, float* out, int ldo, long long P, int C, const float* wg,
+                           const float* bg, float* sa, unsigned* amax, hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && wg && bg && sa, "srpde_bn_relu_gate_fwd: null");
+  SRPDE_CHECK_ARG((C == 256 || C == 512 || C == 1024) && ldy % 4 == 0 && ldo % 4 == 0,
+                  "srpde_bn_relu_gate_fwd: C 256, 512 or 1024, ld multiples of 4");
+  const long long ppb = 256 / (C / 4);
+  const int blocks = (int)std::min<long long>((P + ppb - 1) / ppb, 1024);
+  hipLaunchKernelGGL(bn_relu_gate_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, mean, invstd, gamma, beta,
+                     out, ldo, P, C, wg, bg, sa, amax);
+  SRPDE_LAUNCH_CHECK("srpde_bn_relu_gate_fwd");
   return 0;
 }
 

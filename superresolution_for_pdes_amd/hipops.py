@@ -437,6 +437,18 @@ def bn_relu_pool_att_fwd(y, mean, invstd, gamma, beta, out, pool, n, h, w, att_p
     return m, hb, ca
 
 
+def bn_relu_gate_fwd(y, mean, invstd, gamma, beta, out, wg, bg, amax=None):
+    """bn_relu_fwd into ``out`` that also returns sa = sigmoid(conv1x1(out; wg, bg)) [P]."""
+    P, C = y.shape
+    sa = empty(P, device=y.device)
+    py, ldy = _pl(y)
+    po, ldo = _pl(out)
+    call("srpde_bn_relu_gate_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         po, ldo, P, C, wg.data_ptr(), bg.data_ptr(), sa.data_ptr(), _p(amax), stream_ptr())
+    tag_amax(out, amax)
+    return sa
+
+
 BN_RELU, BN_EVAL = 1, 2   # srpde_bn_relu_bwd flags (include/srpde.h)
 
 

@@ -182,7 +182,8 @@ def _splits_both_ways(c0, c1, cout, w, dil):
     return H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(cout, 0, c0 + c1, w, dil)
 
 
-def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False, att=None):
+def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False, att=None,
+             gate=None):
     """conv3x3 -> BatchNorm2d -> ReLU  (ConvBlock half, models.py:22-23; bridge :43-48).
 
     ``activate=False`` (train mode): stop after the BN statistics and return the conv output y
@@ -191,7 +192,8 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     ``pool``: also return the 2x2 max-pool of the activation, formed in the same pass
     (srpde_bn_relu_pool_fwd): ((a, pooled), saved).  With ``att`` (the AttentionGate that reads a)
     also its channel branch, from the same pass when possible (srpde_bn_relu_pool_att_fwd):
-    ((a, pooled, early), saved), ``early`` as _att_channel_early returns it."""
+    ((a, pooled, early), saved), ``early`` as _att_channel_early returns it.  ``gate``: the
+    AttentionGate whose gating input a is; returns ((a, sa), saved) with its spatial attention."""
     dev = x0.device
     cout = conv.out_channels
     c1 = x1.shape[1] if x1 is not None else 0
@@ -222,6 +224,13 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         y._srpde_amax = slot
         return (y, aff), saved
     a = H.empty(P, cout, device=dev)
+    if gate is not None:
+        s0 = gate.spatial_attention[0]
+        if _FUSE_SA and cout in (256, 512, 1024):
+            return (a, H.bn_relu_gate_fwd(y, mean, invstd, bn.weight, bn.bias, a, s0.weight, s0.bias,
+                                          amax=slots.take())), saved
+        H.bn_relu_fwd(y, mean, invstd, bn.weight, bn.bias, a, amax=slots.take())
+        return (a, None), saved
     if pool and _FUSE_POOL:
         pooled = H.empty(n * (h // 2) * (w // 2), cout, device=dev)
         if att is not None and _FUSE_ATT_CH and cout % 32 == 0 and cout <= 256:
@@ -445,16 +454,18 @@ def _fuse_pair(conv2, training, w, dil):
     return training and _splits_both_ways(conv2.in_channels, 0, conv2.out_channels, w, dil)
 
 
-def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False, activate=True, att=None):
+def _pair_fwd(conv1, bn1, conv2, bn2, x0, x1, n, h, w, training, dil, slots, pool=False, activate=True, att=None,
+              gate=None):
     """conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU, with the middle BN + ReLU fused into conv2's
     input transform when possible (saves a read and a write of the middle activation)."""
     if _fuse_pair(conv2, training, w, dil):
         (y1, aff), s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots, activate=False)
         a2, s2 = _cbr_fwd(conv2, bn2, y1, None, n, h, w, training, dil, slots, in_affine=aff, pool=pool,
-                          activate=activate, att=att)
+                          activate=activate, att=att, gate=gate)
         return a2, (s1, s2)
     a1, s1 = _cbr_fwd(conv1, bn1, x0, x1, n, h, w, training, dil, slots)
-    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool, activate=activate, att=att)
+    a2, s2 = _cbr_fwd(conv2, bn2, a1, None, n, h, w, training, dil, slots, pool=pool, activate=activate, att=att,
+                      gate=gate)
     return a2, (s1, s2)
 
 
@@ -568,10 +579,10 @@ def unet_forward(m, x, training, save=False):
     (e2, p2, ch2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True, att=m.att2)
     (e3, ch3), S.enc3 = _block_fwd(m.enc3, p2, None, n, h3, w3, training, slots, att=m.att3)
     # bridge (dilated)
-    b, (S.br1, S.br2) = _pair_fwd(m.bridge[0], m.bridge[1], m.bridge[3], m.bridge[4], e3, None, n, h3, w3,
-                                  training, 2, slots)
+    (b, sa3), (S.br1, S.br2) = _pair_fwd(m.bridge[0], m.bridge[1], m.bridge[3], m.bridge[4], e3, None, n, h3, w3,
+                                         training, 2, slots, gate=m.att3)
     # decoder with attention, virtual concat
-    e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3, early=ch3)
+    e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3, early=ch3, sa=sa3)
     # SRPDE_FUSE_UP=1: dec3's / dec2's output BN + ReLU applied inside the upsample that reads it
     # (train mode; d3 / d2 never written) -- measured step-neutral (33.02 vs 33.03 ms, 4 reps), off
     if training and _FUSE_UP:

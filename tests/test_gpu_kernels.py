@@ -617,3 +617,25 @@ def test_bn_relu_att_unpooled_matches_separate_passes():
     assert torch.equal(a1, a2)
     for u, v in zip(ref, got):
         assert rel(v, u) < 1e-6, rel(v, u)
+
+
+def test_bn_relu_gate_matches_separate_passes():
+    """srpde_bn_relu_gate_fwd (the bridge output's BN + ReLU with att3's spatial attention): the
+    activation bit-equal to srpde_bn_relu_fwd, sa to srpde_att_gate_fwd's within fp32 summation order."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(5)
+    n, h, w, c = 3, 10, 10, 512
+    P = n * h * w
+    y = torch.randn(P, c, generator=g).to(DEV)
+    mean, invstd = y.mean(0), 1.0 / torch.sqrt(y.var(0) + 1e-5)
+    gam, bet = (torch.rand(c, generator=g) + 0.5).to(DEV), torch.randn(c, generator=g).to(DEV)
+    wg, bg = (torch.randn(1, c, 1, 1, generator=g) * 0.05).to(DEV), torch.randn(1, generator=g).to(DEV)
+    a1, a2 = H.empty(P, c, device=DEV), H.empty(P, c, device=DEV)
+    H.bn_relu_fwd(y, mean, invstd, gam, bet, a1)
+    x = torch.randn(P, 256, generator=g).to(DEV)
+    chan = (torch.zeros(n, 256, device=DEV), torch.zeros(n, 32, device=DEV), torch.ones(n, 256, device=DEV))
+    _, (_, _, _, sa_ref) = H.att_gate_fwd(x, a1, n, h * w, chan, wg, bg)
+    sa = H.bn_relu_gate_fwd(y, mean, invstd, gam, bet, a2, wg, bg)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2)
+    assert float((sa - sa_ref).abs().max()) < 1e-6
