@@ -172,6 +172,13 @@ int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int 
 int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long long P, int C,
                             float* running_mean, float* running_var, long long* num_batches_tracked,
                             float momentum, float eps, float* mean_out, float* invstd_out, hipStream_t stream);
+/* srpde_bn_train_finalize followed by srpde_bn_affine of its mean / invstd, in one launch (the same
+ * outputs, bit for bit; amax_bound nullable, zeroed beforehand). */
+int srpde_bn_train_finalize_affine(const float* stats, int nblk, int rows_per_blk, long long P, int C,
+                                   float* running_mean, float* running_var, long long* num_batches_tracked,
+                                   float momentum, float eps, float* mean_out, float* invstd_out, const float* gamma,
+                                   const float* beta, float* scale, float* shift, unsigned* amax_bound,
+                                   hipStream_t stream);
 int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, int C, float eps, float* mean_out,
                           float* invstd_out, hipStream_t stream);
 /* amax (nullable): *amax = max(*amax, max|out|) as float bits -- the operand-scale word of the

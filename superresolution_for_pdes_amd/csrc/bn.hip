@@ -40,7 +40,10 @@ constexpr int FIN_T = 1024;
 __global__ __launch_bounds__(FIN_T) void bn_train_finalize_kernel(
     const float2* __restrict__ stats, int nblk, int rows_per_blk, long long P, int C,
     float* running_mean, float* running_var, float momentum, float eps,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches_tracked) {
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches_tracked,
+    const float* __restrict__ gamma = nullptr, const float* __restrict__ beta = nullptr,
+    float* __restrict__ scale_out = nullptr, float* __restrict__ shift_out = nullptr, unsigned* amax = nullptr,
+    float sqrt_pm1 = 0.f) {
   const int c = blockIdx.x;
   __shared__ double s1[FIN_T], s2[FIN_T], sm[FIN_T];
   const long long nfull_ll = P / rows_per_blk;
@@ -98,6 +101,12 @@ __global__ __launch_bounds__(FIN_T) void bn_train_finalize_kernel(
     if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
     if (running_var) running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)var_u;
     if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
+    if (scale_out) {   // bn_affine_kernel's outputs for this channel, from the same float mean / invstd
+      const float sc = gamma[c] * invstd_out[c];
+      scale_out[c] = sc;
+      shift_out[c] = beta[c] - mean_out[c] * sc;
+      if (amax) atomicMax(amax, __float_as_uint(fabsf(gamma[c]) * sqrt_pm1 + fabsf(beta[c])));
+    }
   }
 }
 
@@ -599,6 +608,21 @@ int srpde_bn_train_finalize(const float* stats, int nblk, int rows_per_blk, long
                      reinterpret_cast<const float2*>(stats), nblk, rows_per_blk, P, C, running_mean, running_var,
                      momentum, eps, mean_out, invstd_out, num_batches_tracked);
   SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize");
+  return 0;
+}
+
+int srpde_bn_train_finalize_affine(const float* stats, int nblk, int rows_per_blk, long long P, int C,
+                                   float* running_mean, float* running_var, long long* num_batches_tracked,
+                                   float momentum, float eps, float* mean_out, float* invstd_out, const float* gamma,
+                                   const float* beta, float* scale, float* shift, unsigned* amax_bound,
+                                   hipStream_t stream) {
+  SRPDE_CHECK_ARG(stats && mean_out && invstd_out && gamma && beta && scale && shift && C > 0 && nblk > 0 && P > 0,
+                  "srpde_bn_train_finalize_affine: bad args");
+  hipLaunchKernelGGL(bn_train_finalize_kernel, dim3(C), dim3(FIN_T), 0, stream,
+                     reinterpret_cast<const float2*>(stats), nblk, rows_per_blk, P, C, running_mean, running_var,
+                     momentum, eps, mean_out, invstd_out, num_batches_tracked, gamma, beta, scale, shift, amax_bound,
+                     (float)sqrt((double)(P - 1)));
+  SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize_affine");
   return 0;
 }
 

@@ -380,6 +380,18 @@ def bn_train_finalize(stats, nblk, rows_per_blk, P, running_mean, running_var, n
     return mean, invstd
 
 
+def bn_train_finalize_affine(stats, nblk, rows_per_blk, P, running_mean, running_var, nbt, momentum, eps, gamma,
+                             beta, amax=None):
+    """bn_train_finalize + bn_affine in one launch -> (mean, invstd, (scale, shift))."""
+    C = stats.shape[1]
+    dev = stats.device
+    mean, invstd, scale, shift = (empty(C, device=dev) for _ in range(4))
+    call("srpde_bn_train_finalize_affine", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
+         _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(amax), stream_ptr())
+    return mean, invstd, (scale, shift)
+
+
 def bn_affine(mean, invstd, gamma, beta, P, amax=None):
     """(scale, shift) with relu(y * scale + shift) == the train-mode BN + ReLU output, and a
     rigorous max|output| bound written into ``amax`` (the fused consumer's operand scale)."""

@@ -209,6 +209,18 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         assert in_affine is None or xp is not None, "a fused input needs the stored split for its wgrad"
         _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp, in_affine)
         mom = bn.momentum if bn.momentum is not None else 0.0
+        if not activate:   # the fused consumer's (scale, shift), from the same launch (SRPDE_FIN_AFFINE=0: two)
+            slot = slots.take()
+            if _FIN_AFFINE:
+                mean, invstd, aff = H.bn_train_finalize_affine(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
+                                                               bn.num_batches_tracked, mom, bn.eps, bn.weight,
+                                                               bn.bias, amax=slot)
+            else:
+                mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
+                                                   bn.num_batches_tracked, mom, bn.eps)
+                aff = H.bn_affine(mean, invstd, bn.weight, bn.bias, P, amax=slot)
+            y._srpde_amax = slot
+            return (y, aff), (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
         mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
                                            bn.num_batches_tracked, mom, bn.eps)
     else:
@@ -218,11 +230,6 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
     # the weight gradient reads the stored split
     saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
-    if not activate:
-        slot = slots.take()
-        aff = H.bn_affine(mean, invstd, bn.weight, bn.bias, P, amax=slot)
-        y._srpde_amax = slot
-        return (y, aff), saved
     a = H.empty(P, cout, device=dev)
     if gate is not None:
         s0 = gate.spatial_attention[0]
@@ -256,6 +263,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
 
 
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
+_FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
 _FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "0") == "1"
 # the gates' spatial attention formed by the upsample that produces their gating input
 # (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
