@@ -54,6 +54,59 @@ def conv_flops(cin, cout, hw):
     return 2.0 * cout * cin * 9 * hw * hw
 
 
+# whole-forward algorithmic cost per sample, SURVEY 3.4 / 8(d) [measured on the reference]:
+# 26 conv calls = 2.6753 GFLOP; unfused fp32 activation traffic (every op's inputs + outputs,
+# weights excluded) = 36.31 MB.  north_star's target: >= 60 % of the HBM roofline on this forward
+FWD_FLOP_PER_SAMPLE = 2.6753e9
+FWD_BYTES_PER_SAMPLE = 36.31e6
+HBM_PEAK = 8.0e12
+
+
+def default_traffic_json():
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
+    return files[-1] if files else None
+
+
+def time_forward(model, x, training, reps=10, warm=3):
+    """Average ms of one B-sample U-Net forward (no autograd), HIP events on the stream it runs on.
+    Train mode is the step's forward (batch statistics, running-stat update, the stored operand
+    splits the weight gradient reads); eval mode is inference (running statistics, cached weight
+    split)."""
+    was = model.training
+    model.train(training)
+    st = torch.cuda.current_stream(x.device)
+    with torch.no_grad():
+        for _ in range(warm):
+            model(x)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(reps):
+            model(x)
+        b.record(st)
+        b.synchronize()
+    model.train(was)
+    return a.elapsed_time(b) / reps
+
+
+def forward_roofline(model, x, peak_tf):
+    """roofline.forward: the north-star figure (>= 60 % of HBM roofline on the B=1024 40x40 forward,
+    i.e. forward <= 7.75 ms), with the MFMA fraction beside it."""
+    B = x.shape[0]
+    out = {"batch": B, "algorithmic_bytes": FWD_BYTES_PER_SAMPLE * B, "algorithmic_flop": FWD_FLOP_PER_SAMPLE * B,
+           "hbm_peak_gbs": HBM_PEAK / 1e9, "mfma_peak_tflops": peak_tf,
+           "target": "hbm_frac >= 0.60 (forward <= %.2f ms)" % (FWD_BYTES_PER_SAMPLE * B / (0.6 * HBM_PEAK) * 1e3)}
+    for mode, training in (("train", True), ("eval", False)):
+        ms = time_forward(model, x, training)
+        t = ms * 1e-3
+        out[mode] = {"ms": round(ms, 4), "samples_per_s": round(B / t, 1),
+                     "hbm_gbs": round(FWD_BYTES_PER_SAMPLE * B / t / 1e9, 1),
+                     "hbm_frac": round(FWD_BYTES_PER_SAMPLE * B / t / HBM_PEAK, 4),
+                     "tflops": round(FWD_FLOP_PER_SAMPLE * B / t / 1e12, 2),
+                     "mfma_frac": round(FWD_FLOP_PER_SAMPLE * B / t / 1e12 / peak_tf, 4)}
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -63,7 +116,9 @@ def parse():
     ap.add_argument("--roofline-layer", default="bridge.3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02b.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic of the roofline kernel (tools/traffic_json.py output); default: the newest "
+                         "profiles/traffic_r*.json, which round_evidence.sh measures on the tree it commits with")
     ap.add_argument("--workload", choices=("train", "poisson", "cascade"), default="train",
                     help="train = the BASELINE metric (default); poisson = config #3 CG data-gen solve; "
                          "cascade = config #5 20->640 multi-level inference")
@@ -318,9 +373,40 @@ def run_cascade(args, world, rank, dev):
     emit(rec)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """``--gpus N > 1`` without a launcher: start ``torch.distributed.run`` with N ranks (one process
+    per GPU) as a CHILD process -- this process has made no GPU call yet and makes none -- relay the
+    rank-0 JSON line on stdout and exit with the child's status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout.splitlines():
+        if line.lstrip().startswith("{"):
+            print(line, flush=True)
+    return proc.returncode
+
+
 def main():
     global _JSON_OUT
     args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if ws is not None and int(ws) != args.gpus and not (args.gpus == 1 and args.ddp):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one rank per GPU)", file=sys.stderr)
+        sys.exit(2)
     # RCCL prints its version block on fd 1 at communicator creation: keep fd 1 for the JSON line
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")
@@ -409,6 +495,14 @@ def main():
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt)
+    # after the timed region: the forward alone (every rank runs it; rank 0 reports)
+    from superresolution_for_pdes_amd import hipops as H
+    math = H.conv_math()
+    # dense MFMA peak of the instruction the kernel runs, in fp32-product units: fp32 MFMA
+    # 157.3 TF; bf16 / fp16 MFMA run at 16x that (2516.8 TF), divided by the partial
+    # products per fp32 product: 3 for h3 (838.9 TF)
+    peak = {"h3": round(157.3 * 16 / 3, 1)}.get(math, 157.3)
+    fwd_roof = forward_roofline(model, x, peak)
 
     if rank == 0:
         kern_ms = [a.elapsed_time(b) for a, b in timed]
@@ -416,17 +510,11 @@ def main():
         cin, cout, hw = next((c, o, h) for n, c, o, h in CONV3 if n == args.roofline_layer)
         flops_launch = conv_flops(cin, cout, hw) * B
         achieved = flops_launch / (kern_avg * 1e-3) / 1e12 if kern_avg > 0 else None
-        from superresolution_for_pdes_amd import hipops as H
-        math = H.conv_math()
-        # dense MFMA peak of the instruction the kernel runs, in fp32-product units: fp32 MFMA
-        # 157.3 TF; bf16 / fp16 MFMA run at 16x that (2516.8 TF), divided by the partial
-        # products per fp32 product: 6 for x6 (419.5 TF), 3 for h3 (838.9 TF)
-        peak = {"h3": round(157.3 * 16 / 3, 1), "x6": round(157.3 * 16 / 6, 1)}.get(math, 157.3)
-        kname = {"h3": "conv_fwd_h3", "x6": "conv_fwd_x6"}.get(math, "conv_fwd_v2")
-        traffic = None
-        if os.path.exists(args.traffic_json):
+        kname = {"h3": "conv_fwd_h3"}.get(math, "conv_fwd_v2")
+        traffic, tfile = None, args.traffic_json or default_traffic_json()
+        if tfile and os.path.exists(tfile):
             try:
-                traffic = json.load(open(args.traffic_json)).get(f"{math}:{args.roofline_layer}")
+                traffic = json.load(open(tfile)).get(f"{math}:{args.roofline_layer}")
             except (ValueError, OSError):
                 traffic = None
         samples = world * B * args.steps
@@ -447,8 +535,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": {"h3": "f32 (h3: fp32 products from power-of-two-scaled 2-piece fp16 splits on fp16 MFMA, "
-                            "fp32 accumulate)",
-                      "x6": "f32 (x6: fp32 products from 3-way bf16 splits on bf16 MFMA, fp32 accumulate)"}.get(math, "f32"),
+                            "fp32 accumulate)"}.get(math, "f32"),
             "data": "synthetic (x~N(0,1), theta channel=1, t~N(0,1)), resident in HBM",
             "config": {"workload": "UNet 20->40 train step, fp32, batch 1024/GPU, 40x40",
                        "global_batch": world * B, "per_gpu_batch": B, "hw": "40x40",
@@ -456,10 +543,14 @@ def main():
             "roofline": {"bound": "mfma", "kernel": f"{kname}[{args.roofline_layer}]",
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": traffic, "launch_ms": round(kern_avg, 4),
+                         "traffic": traffic,
+                         "traffic_source": (os.path.relpath(tfile, ROOT) + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                            "per launch, tools/gpu/round_evidence.sh)") if traffic else None,
+                         "launch_ms": round(kern_avg, 4),
                          "algorithmic_flop_per_launch": flops_launch,
                          "step": {"algorithmic_flop": step_flop, "achieved": round(step_ach, 2),
-                                  "frac": round(step_ach / peak, 4)}},
+                                  "frac": round(step_ach / peak, 4)},
+                         "forward": fwd_roof},
         }
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

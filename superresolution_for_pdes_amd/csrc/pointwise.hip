@@ -1199,7 +1199,8 @@ int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, cons
 
 int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho,
                                       int wo, int c, const float* wg, const float* bg, float* sa, hipStream_t stream) {
-  SRPDE_CHECK_ARG(x && out && wg && bg && sa && ldx % 4 == 0 && ldo % 4 == 0 && c % 4 == 0 && c / 4 <= 64,
+  SRPDE_CHECK_ARG(x && out && wg && bg && sa && ldx % 4 == 0 && ldo % 4 == 0 && c % 4 == 0 && c / 4 >= 1 &&
+                      c / 4 <= 64 && ((c / 4) & (c / 4 - 1)) == 0,
                   "srpde_upsample_bilinear_gate_fwd: bad args (c / 4 a power of two <= 64)");
   dim3 g, b;
   SRPDE_CHECK_ARG(px_geometry((long long)n * ho * wo, c, &g, &b), "srpde_upsample_bilinear_gate_fwd: bad geometry");

@@ -137,6 +137,12 @@ class DataParallel(torch.nn.Module):
             parts = torch.split(flat, [b.numel() for b in bufs])
             torch._foreach_copy_(bufs, [s.view_as(b) for s, b in zip(parts, bufs)])
 
+    def sync_buffers(self):
+        """Broadcast rank 0's BN buffers now (train_model calls it before validation, so every
+        rank evaluates the model rank 0 checkpoints)."""
+        if dist.get_world_size(self.pg) > 1:
+            self._sync_buffers()
+
     def forward(self, x):
         if self.broadcast_buffers and self.module.training and dist.get_world_size(self.pg) > 1:
             self._sync_buffers()

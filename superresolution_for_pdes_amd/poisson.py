@@ -30,6 +30,8 @@ def forcing_batched(k12, n: int, device="cuda"):
     """f[b] = sin(2 pi k1_b X) sin(2 pi k2_b Y) on linspace(0,1,n)^2 (data_generation.py:60-77)."""
     k = _dev_f64(k12, device).reshape(-1, 2).contiguous()
     out = torch.empty(k.shape[0], n, n, dtype=torch.float64, device=device)
+    if k.shape[0] == 0:      # an empty rank shard (shard_range with n < world): nothing to launch
+        return out
     call("srpde_forcing_batched", k.data_ptr(), k.shape[0], n, out.data_ptr(), stream_ptr())
     return out
 
@@ -50,6 +52,8 @@ def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, devic
         maxit = 20 * n * n
     u = torch.empty_like(f)
     iters = torch.empty(B, dtype=torch.int32, device=device)
+    if B == 0:               # an empty rank shard: the C entry rejects B = 0, there is nothing to solve
+        return (u, iters) if return_iters else u
     ws_bytes = int(query("srpde_poisson_workspace_size", B, n))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
     call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),

@@ -149,6 +149,11 @@ def train_model(model: nn.Module, train_loader, val_loader, criterion: nn.Module
             nb += 1
         train_loss = _global_mean(acc, nb, device)
 
+        # under data parallelism each rank's last training forward updated its BN running
+        # statistics with its own shard: validate every rank with rank 0's buffers (the state
+        # best_model.pth saves), so the reduced val loss is that model's single-process loss
+        if hasattr(model, "sync_buffers"):
+            model.sync_buffers()
         model.eval()
         vacc = torch.zeros((), dtype=torch.float64, device=device)
         vb = 0

@@ -240,13 +240,13 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         return (a, None), saved
     if pool and _FUSE_POOL:
         pooled = H.empty(n * (h // 2) * (w // 2), cout, device=dev)
-        if att is not None and _FUSE_ATT_CH and cout % 32 == 0 and cout <= 256:
+        if att is not None and _per_sample_ok(n, h, w, cout):
             c1, c3, _ = _att_params(att)
             chan = H.bn_relu_pool_att_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w,
                                           (c1.weight, c1.bias, c3.weight, c3.bias), amax=slots.take())
             return (a, pooled, (chan, None)), saved
         H.bn_relu_pool_fwd(y, mean, invstd, bn.weight, bn.bias, a, pooled, n, h, w, amax=slots.take())
-    elif (not pool and att is not None and _FUSE_ATT_CH and cout % 32 == 0 and cout <= 256
+    elif (not pool and att is not None and _per_sample_ok(n, h, w, cout)
           and a.is_cuda and not torch.cuda.is_current_stream_capturing()):
         c1, c3, _ = _att_params(att)
         chan = H.bn_relu_pool_att_fwd(y, mean, invstd, bn.weight, bn.bias, a, None, n, h, w,
@@ -271,6 +271,15 @@ _FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
 # enc1's / enc2's gate channel branch from the BN + ReLU + pool pass (srpde_bn_relu_pool_att_fwd, one
 # block per sample; SRPDE_FUSE_ATT_CH=0: a separate pass over the activation)
 _FUSE_ATT_CH = os.environ.get("SRPDE_FUSE_ATT_CH", "1") != "0"
+
+
+def _per_sample_ok(n, h, w, c):
+    """srpde_bn_relu_pool_att_fwd runs ONE workgroup per sample: take it when the batch fills the
+    chip or a sample is small (the 40x40 training / cascade tiles), not for a few large fields
+    (e.g. B = 1 at 640^2, where one CU would write the whole activation)."""
+    return _FUSE_ATT_CH and c % 32 == 0 and c <= 256 and (n >= 256 or h * w <= 4096)
+
+
 # a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
 _FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
 

@@ -42,25 +42,25 @@ def _cpu_solver(monkey_target):
     monkey_target.solve_batched = solve_batched
 
 
-def _generate(shard):
+def _generate(shard, sizes=(5, 3)):
     from superresolution_for_pdes_amd import poisson as P
     from superresolution_for_pdes_amd.enhanced_data_generation import EnhancedPoissonSolver
     _cpu_solver(P)
     s = EnhancedPoissonSolver(20, 40, 80, device="cpu")
     np.random.seed(123)
-    d1 = s.generate_dataset(n_samples=5, k_range=(0.5, 5.0), keep_on_device=True, shard=shard)
-    d2 = s.generate_subdomain_dataset(n_samples=3, k_range=(0.5, 12.0), keep_on_device=True, shard=shard)
+    d1 = s.generate_dataset(n_samples=sizes[0], k_range=(0.5, 5.0), keep_on_device=True, shard=shard)
+    d2 = s.generate_subdomain_dataset(n_samples=sizes[1], k_range=(0.5, 12.0), keep_on_device=True, shard=shard)
     after = np.random.uniform()           # the RNG stream must be where the single-process run leaves it
     return s.combine_datasets(d1, d2), after
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, sizes=(5, 3)):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        data, after = _generate(None)      # shard from the process group
-        want, want_after = _generate((0, 1))
+        data, after = _generate(None, sizes)      # shard from the process group
+        want, want_after = _generate((0, 1), sizes)
         same = set(data) == set(want) and all(
             np.array_equal(np.asarray(data[k]), np.asarray(want[k])) for k in want)
         q.put((rank, same, after == want_after, len(data["u_fine"])))
@@ -84,6 +84,24 @@ def test_sharded_datagen_equals_single_process_world2():
         assert same, rank
         assert rng_ok, rank
         assert n == 8
+
+
+def test_sharded_datagen_with_empty_shards_world3():
+    """n_samples < world: some ranks solve an empty slice and still join the gathers."""
+    world, sizes = 3, (2, 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, sizes)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, rng_ok, n in res:
+        assert same and rng_ok, rank
+        assert n == 3
 
 
 def test_shard_range_partitions():

@@ -141,3 +141,59 @@ def test_grad_reducer_unet_layout_world2():
         assert all(hi - lo == bsz for lo, hi in buckets[:-1]) and 0 < buckets[-1][1] - buckets[-1][0] <= bsz
         assert launched == (total // bsz) * bsz
     assert res[0][4] == res[1][4]                      # identical bucket boundaries on both ranks
+
+
+def _val_worker(rank, world, port, q, tmp):
+    """train_model under DataParallel: every rank validates with rank 0's BN buffers, so the
+    reduced val loss is the single-process loss of the model rank 0 checkpoints."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from superresolution_for_pdes_amd.distributed import DataParallel
+        from superresolution_for_pdes_amd.train_enhanced import train_model
+
+        class Tiny(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.lin = torch.nn.Linear(3, 4)
+                self.bn = torch.nn.BatchNorm1d(4)
+
+            def forward(self, x):
+                return self.bn(self.lin(x))
+
+        torch.manual_seed(0)
+        t = Tiny()
+        dp = DataParallel(t)
+        g = torch.Generator().manual_seed(10 + rank)      # different training shards per rank
+        train = [(torch.randn(8, 3, generator=g) * (rank + 1), torch.randn(8, 4, generator=g)) for _ in range(3)]
+        gv = torch.Generator().manual_seed(99)            # the same validation set on every rank
+        val_all = [(torch.randn(5, 3, generator=gv), torch.randn(5, 4, generator=gv)) for _ in range(4)]
+        val = val_all[rank::world]                        # single-process batches dealt round-robin
+        opt = torch.optim.SGD(t.parameters(), lr=0.0)     # parameters stay equal: only BN buffers differ
+        sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.5, patience=10)
+        hist = train_model(dp, train, val, torch.nn.MSELoss(), opt, sched, 1, "cpu", tmp, None)
+        t.eval()
+        with torch.no_grad():
+            want = sum(float(torch.nn.functional.mse_loss(t(x), y)) for x, y in val_all) / len(val_all)
+        q.put((rank, hist["val_loss"][0], want, t.bn.running_mean.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_val_loss_uses_rank0_buffers_world2(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_val_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, v0, want0, rm0), (_, v1, _, rm1) = res
+    assert rm0 == rm1                                  # rank 1 validated with rank 0's buffers
+    assert abs(v0 - want0) <= 1e-6 * max(1.0, abs(want0)), (v0, want0)
+    assert v0 == v1

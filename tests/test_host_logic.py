@@ -109,3 +109,13 @@ def test_cpu_tensors_fail_loudly():
     with pytest.raises(RuntimeError):
         PDEDataset({"u_coarse": np.zeros((1, 20, 20)), "u_fine": np.zeros((1, 40, 40)),
                     "f_fine": np.zeros((1, 40, 40)), "theta_fine": np.ones((1, 40, 40))}, device="cpu")
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py exits non-zero, before any GPU call, when WORLD_SIZE disagrees with --gpus."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "WORLD_SIZE=4" in p.stderr
