@@ -50,41 +50,12 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
 /* optional scratch for splitting the last, partially filled round of tiles over K (pass
  * NULL to disable); srpde_conv_fwd_workspace_size() bytes always suffice */
 size_t srpde_conv_fwd_workspace_size(int cout);
-/* The same convolution (same arguments, same output and statistics layout) computed as
- * fp32 products from exact 3-way bf16 splits of both operands: six partial products per
- * fp32 product on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32-accurate; see
- * DESIGN.md).  `wsplit` = srpde_split_weights() of the packed weights.  Needs c0, c1 and
- * cout multiples of 32 (srpde_conv_x6_supported). */
-int srpde_conv_x6_supported(int c0, int c1, int cout);
-int srpde_split_weights(const float* w, void* planes, long long n, hipStream_t stream);
-int srpde_conv_fwd_x6(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const void* wsplit,
-                      const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
-                      int sign, int accumulate, float* stats, void* workspace, size_t ws_bytes,
-                      hipStream_t stream);
 size_t srpde_conv_stats_blocks(int n, int h, int w, int cout);
 int srpde_conv_stats_rows_per_block(int cout);
 size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, int ksize);
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                      int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
-/* Weight gradient of a 3x3 conv on a 3-channel input (enc1.conv1, models.py:16 with the UNet's
- * in_channels = 3) whose output feeds a train-mode BN (+ReLU, flags bit 0): dy is formed on the fly
- * from the BN input y, the incoming gradient da and the per-channel m1 / m2 of srpde_bn_bwd_prepare
- * (the expressions of srpde_bn_relu_bwd's apply), so it is never written -- replaces that apply pass
- * plus srpde_conv_wgrad for the reference's conv1.weight.grad (train_enhanced.py:72 backward).
- * x: NHWC rows of ldx >= 4 floats (channels past 3 ignored); dw [cout][3][3][3]; cout 16, 32 or 64. */
-size_t srpde_conv_wgrad_bnb_c3_workspace_size(long long P, int cout);
-int srpde_conv_wgrad_bnb_c3(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
-                            const float* gamma, const float* beta, const float* m1, const float* m2, int flags,
-                            const float* x, int ldx, float* dw, int accumulate, int n, int h, int w, int cout, int dil,
-                            void* workspace, size_t ws_bytes, hipStream_t stream);
-/* activations pre-split once into three bf16 planes [3][P][c] (truncation split, exact) ... */
-int srpde_split_planes(const float* x, int ldx, int c, long long P, void* planes, hipStream_t stream);
-/* ... and the x6 convolution reading them (no split inside the GEMM loop); x0p/x1p are
- * srpde_split_planes outputs of the two input halves (c0 / c1 channels, compact) */
-int srpde_conv_fwd_x6p(const void* x0p, int c0, const void* x1p, int c1, const void* wsplit, const float* bias,
-                       float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
-                       float* stats, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* h3: the same convolution (forward / dgrad, same output and statistics layout) from
  * two-piece fp16 splits with power-of-two operand scales: three partial products per fp32
  * product on v_mfma_f32_32x32x16_f16, halo-staged activation tiles (conv_h3.hip).
@@ -98,10 +69,6 @@ int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize)
 /* Rows per BatchNorm-statistics block written by srpde_conv_fwd_h3 (stats / bn_part buffers
  * hold ceil(P / rows) blocks); the other conv families use srpde_conv_stats_rows_per_block. */
 int srpde_conv_h3_stats_rows(void);
-/* Tile choice of srpde_conv_fwd_h3: layers with at most max_chunks 32-channel chunks of input run
- * on 128-row tiles, two workgroups per CU (0: never).  Returns the previous value.  Tuning and
- * tests; the default comes from SRPDE_H3_HALF. */
-int srpde_conv_h3_set_half(int max_chunks);
 /* Kernel choice of srpde_conv_fwd_h3 for output tiles of <= 64 channels: 1 = the register-staged
  * 4-wave kernel, two workgroups per CU (default; SRPDE_H3R=0 turns it off), 0 = the 8-wave
  * kernel.  Both compute the same outputs, statistics and stored splits bit for bit (outside a
@@ -160,10 +127,6 @@ size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int ci
 int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* xp, int c0, const unsigned* amax0,
                          int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
                          int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
-/* weight gradient with the x6 arithmetic (same arguments / workspace; c0, c1, cout % 32 == 0) */
-int srpde_conv_wgrad_x6(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
-                        int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
-                        int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
 
 /* ---- BatchNorm2d + ReLU -------------------------------------------------------------
  * replaces aten::native_batch_norm / native_batch_norm_backward and relu /
@@ -281,11 +244,6 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
  * dg[q][c] += dsa[q] * wg[c] (models.py:116, srpde_att_bwd called with dg == NULL leaves dsa in
  * workspace[0, P)) folded into the upsample backward that consumes dg (models.py:89,92), so the
  * gating gradient is never written.  Needs c / 4 a power of two <= 256. */
-/* relu(y * scale + shift) (the train-mode BN + ReLU as srpde_bn_affine's per-channel affine) upsampled
- * x2 with align_corners in one pass, the activation never written (models.py:22-23 then :89,92);
- * amax (nullable, zeroed beforehand): receives max|out|. */
-int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, const float* shift, float* out, int ldo,
-                               int n, int h, int w, int ho, int wo, int c, unsigned* amax, hipStream_t stream);
 /* srpde_upsample_bilinear_fwd that also forms the spatial attention of the gate reading the result
  * (models.py:124-125, 89/92): sa[q] = sigmoid(sum_c wg[c] out[q][c] + bg[0]).  c / 4 a power of two
  * <= 64.  With srpde_att_channel_fwd's ca, srpde_att_apply_fwd then finishes the gate. */

@@ -23,9 +23,6 @@ struct ConvParams {
   // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
   int ntail, tsplit;
   int dbg;              // diagnostics (SRPDE_CONV_DBG): 1 = x6 kernel skips the per-stage DMA
-  // x6p: the inputs as pre-split bf16 planes [3][P][c0] / [3][P][c1] (srpde_split_planes)
-  const __bf16* x0p;
-  const __bf16* x1p;
   float* part;
   // optional fused BatchNorm-backward reduction (h3 dgrad): the output is the gradient of a
   // BN + ReLU output a = relu(gamma * (bn_y - mean) * invstd + beta); per (SRB-row block, channel)
@@ -558,20 +555,12 @@ int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, in
                  hipStream_t stream);
 
 // ---------------- host: K-split of the last, under-filled round of tiles ----------------
-static bool tail_split_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SRPDE_CONV_TAIL");  // tuning/diagnostics: 0 disables the split
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
-
 // tail split plan shared by the LDS-DMA forward kernels (see launch_fwd_v2)
 static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes) {
   p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
   const int nall = p.K / BK2;
   const int rem = T % slots;
-  if (tail_split_enabled() && T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
+  if (T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {
     int F = std::min(std::min(slots / rem, nall / 2), 8);
     while (F >= 2 && (size_t)rem * F * BM * BN * sizeof(float) > ws_bytes) --F;
     if (F >= 2) { p.ntail = rem; p.tsplit = F; p.part = static_cast<float*>(ws); }

@@ -463,12 +463,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ f32x4 llvm_raw_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
                                          int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
-// BNB = true: the dgrad with the BatchNorm (+ReLU) backward apply fused into the operand transform
-// (as conv_fwd_h3_kernel<..., BNB>): x0 is da (halo tile in registers), and the halo tile of the
-// BN input y is DMA'd as fp32 into S itself once S is free; the split forms dy = gamma*invstd*(dz -
-// m1 - xhat*m2) per element and overwrites its row of S in place (a row's four tasks are four lanes
-// of one wave instruction, so every read of the row precedes every write).
-template <int BN, int TPS, int NTK, int NB, bool BNB = false>
+template <int BN, int TPS, int NTK, int NB>
 __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Args h) {
   constexpr int BM = 256, WM = 4, WN = 1, NW = 4, NT = 256, SRB = 128;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -490,7 +485,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   char* const sbuf = lds + 128;
   char* const bbuf0 = sbuf + arows * 128;
   char* const sink = bbuf0 + NB * B_STAGE;
-  float* const bnbt = reinterpret_cast<float*>(sink + 1024);   // BNB: [6][32] coefficients of the chunk
   constexpr int zoff = 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -517,7 +511,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const size_t plane = (size_t)p.Cout * p.K;
   const int32x4 rsw = make_rsrc(h.wsp, (unsigned)(2 * plane * 2));
-  const int32x4 rsy = BNB ? make_rsrc(h.bnb_y, (unsigned)((size_t)p.P * h.bnb_ldy * 4)) : rs0;
   const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
 
   unsigned ab = h.amax0 ? *h.amax0 : 0u;
@@ -585,16 +578,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     pf[k][0] = llvm_raw_buffer_load_f4(rs, (int)off, 0, 0);
     pf[k][1] = llvm_raw_buffer_load_f4(rs, (int)(off + 16u), 0, 0);
   };
-  // BNB: the y halo tile of chunk `ch` into S (fp32, 16-B chunk k of row r at slot swz(r, k))
-  auto issue_y = [&](int ch) {
-    const int cb = ch * BK2;
-    for (int q = wave; q < arows / 8; q += NW) {
-      const int r = q * 8 + (lane >> 3);
-      const int pix = pix0 + r;
-      const unsigned off = (pix >= 0 && pix < p.P) ? (unsigned)((pix * h.bnb_ldy + cb + swz(r, lane & 7) * 4) * 4) : OOB;
-      dma16(rsy, off, lds_addr_of(sbuf + q * 1024));
-    }
-  };
   // the TPS taps of stage `st` of chunk `ch` into ring slot `buf`; exactly DPS DMAs per wave
   // (missing taps / rows, or ch < 0 = past the last stage: zero fills into the sink)
   auto issue_b = [&](int ch, int st, int buf) {
@@ -628,16 +611,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
       t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
     }
-    if constexpr (BNB) {   // the chunk's per-channel BN-backward terms -> an LDS table (read per task:
-                           // 48 coefficient registers held across the tasks would not fit)
-      if (t < 6 * BK2) {
-        const int q = t / BK2, c = ch * BK2 + t % BK2;
-        const float* src = q == 0 ? h.bnb_mean : q == 1 ? h.bnb_invstd : q == 2 ? h.bnb_gamma
-                         : q == 3 ? h.bnb_beta : q == 4 ? h.bnb_m1 : h.bnb_m2;
-        bnbt[t] = src[c];
-      }
-      __syncthreads();
-    }
 #pragma unroll
     for (int k = 0; k < NTK; ++k) {
       const int sg = t + NT * k;
@@ -645,36 +618,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
         const int r = sg >> 2, c8 = sg & 3;
         float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
         float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
-        if constexpr (BNB) {   // fused BN (+ReLU) backward: da and y -> dy; rows outside the tensor stay 0
-          const bool inside = pix0 + r >= 0 && pix0 + r < p.P;
-          const float4 y0 = *reinterpret_cast<const float4*>(sbuf + r * 128 + swz(r, 2 * c8) * 16);
-          const float4 y1 = *reinterpret_cast<const float4*>(sbuf + r * 128 + swz(r, 2 * c8 + 1) * 16);
-          const float yy8[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-          float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-          for (int hq = 0; hq < 2; ++hq) {   // four channels' coefficients at a time (registers)
-            int to = c8 * 8 + hq * 4;
-            asm volatile("" : "+v"(to));   // re-read per task and half (not hoisted into live registers)
-            const float4 mu = *reinterpret_cast<const float4*>(bnbt + 0 * BK2 + to);
-            const float4 is = *reinterpret_cast<const float4*>(bnbt + 1 * BK2 + to);
-            const float4 ga = *reinterpret_cast<const float4*>(bnbt + 2 * BK2 + to);
-            const float4 be = *reinterpret_cast<const float4*>(bnbt + 3 * BK2 + to);
-            const float4 m1 = *reinterpret_cast<const float4*>(bnbt + 4 * BK2 + to);
-            const float4 m2 = *reinterpret_cast<const float4*>(bnbt + 5 * BK2 + to);
-            const float cm[6][4] = {{mu.x, mu.y, mu.z, mu.w}, {is.x, is.y, is.z, is.w}, {ga.x, ga.y, ga.z, ga.w},
-                                    {be.x, be.y, be.z, be.w}, {m1.x, m1.y, m1.z, m1.w}, {m2.x, m2.y, m2.z, m2.w}};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              // the same expressions as bn_bwd_apply_kernel (bn.hip) and conv_fwd_h3_kernel<..., BNB>
-              const int e = hq * 4 + q;
-              const float xh = (yy8[e] - cm[0][q]) * cm[1][q];
-              const float dz = (!h.bnb_relu || xh * cm[2][q] + cm[3][q] > 0.f) ? vv[e] : 0.f;
-              vv[e] = inside ? (dz - cm[4][q] - xh * cm[5][q]) * (cm[2][q] * cm[1][q]) : 0.f;
-            }
-          }
-          v0 = make_float4(vv[0], vv[1], vv[2], vv[3]);
-          v1 = make_float4(vv[4], vv[5], vv[6], vv[7]);
-        }
         if (h.in_scale != nullptr) {   // rows outside the tensor stay 0
           const int pix = pix0 + r;
           const bool inside = pix >= 0 && pix < p.P;
@@ -696,7 +639,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
           }
         }
       }
-      if constexpr (BNB) __builtin_amdgcn_sched_barrier(0);   // one task's 48 coefficients live at a time
     }
   };
 
@@ -705,7 +647,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   // prologue: the first chunk's halo tile + the first NB - 1 weight stages
 #pragma unroll
   for (int k = 0; k < NTK; ++k) load_task(c_beg, k);
-  if constexpr (BNB) issue_y(c_beg);
 #pragma unroll
   for (int s = 0; s < NB - 1; ++s) {
     const int c = c_beg + s / NS;
@@ -808,11 +749,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
     if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
     if (ch + 1 < c_end) {   // every wave is past the chunk's last stage barrier: S is free
-      if constexpr (BNB) {
-        issue_y(ch + 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
       if (!(p.dbg & 4)) convert(ch + 1);   // diagnostics: 4 = no per-chunk split
       __syncthreads();
     }
@@ -1701,31 +1637,13 @@ constexpr int H3_SRB = 128;
 
 static int h3_arows(int w, int dil, int bm = H3_BM) { return (bm + 2 * (w + 1) * dil + 7) / 8 * 8; }
 
-// Layers with at most this many 32-channel chunks of K run on 128-row tiles with 4 waves and one
-// tap per stage (<= 78 KiB of LDS: two workgroups per CU), so one workgroup's prologue / epilogue
-// overlaps the other's MFMAs; deeper layers keep the 256-row, 8-wave tile (one per CU).
-// SRPDE_H3_HALF or srpde_conv_h3_set_half override the threshold (0: never).
-static std::atomic<int> g_h3_half{-1};
-static int h3_half_max() {
-  int v = g_h3_half.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("SRPDE_H3_HALF");
-    v = e ? std::max(0, atoi(e)) : 0;
-    int expect = -1;
-    g_h3_half.compare_exchange_strong(expect, v);
-    v = g_h3_half.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-
 // the K-split tail's fixup: one block per statistics sub-block of each tail tile (twice the blocks of a
-// whole-tile fixup for the same work: the tail has few tiles) unless the per-tile max|out| slot is
-// wanted (SRPDE_FIXUP_SPLIT=0: whole tiles)
+// whole-tile fixup for the same work: the tail has few tiles; 32.15 -> 32.12 ms per step) unless the
+// per-tile max|out| slot is wanted
 template <int BM, int BN, int SRB>
 static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
-  static const bool split = [] { const char* e = getenv("SRPDE_FIXUP_SPLIT"); return !(e && e[0] == '0'); }();
   if constexpr (BM > SRB) {
-    if (split && p.out_max == nullptr) {
+    if (p.out_max == nullptr) {
       hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB, SRB>), dim3(p.ntail, BM / SRB), dim3(1024), 0, st, p);
       SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
       return 0;
@@ -1739,13 +1657,9 @@ static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
 static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false) {
   return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 128 + 1024;
 }
-// taps per stage: the most (<= SRPDE_H3_TPS, default 2) whose weight double-buffer fits in LDS
+// taps per stage: two when the weight double-buffer fits in LDS (three measured within noise)
 static int h3_tps(int bn, int arows) {
-  static const int want = [] {
-    const char* e = getenv("SRPDE_H3_TPS");   // tuning/diagnostics
-    return e ? std::max(1, std::min(3, atoi(e))) : 2;
-  }();
-  int t = want;
+  int t = 2;
   while (t > 1 && h3_lds(bn, arows, t) > 160 * 1024) --t;
   return t;
 }
@@ -1780,8 +1694,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
 // h3r (register-staged halo, two workgroups per CU): LDS = S + two weight stages + the zero row
 constexpr int H3R_NTK = 6;   // halo tasks per thread: arows <= 6 * 256 / 4 = 384
 constexpr int H3R_NB = 4;    // weight ring depth (stages of one tap)
-static size_t h3r_lds(int bn, int arows, int tps) {   // zero row | S | weight ring | DMA sink | BNB table
-  return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024 + 1024;
+static size_t h3r_lds(int bn, int arows, int tps) {   // zero row | S | weight ring | DMA sink
+  return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024;
 }
 static int h3r_tps(int bn) { (void)bn; return 1; }
 static std::atomic<int> g_h3r{-1};
@@ -1802,7 +1716,7 @@ static bool h3r_fits(int bn, int arows) {
   return h3r_on() && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
 }
 
-template <int BN, int TPS, bool BNB = false>
+template <int BN, int TPS>
 static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int BM = 256, WM = 4, SRB = 128;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
@@ -1822,7 +1736,7 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB, BNB>), dim3(grid), dim3(256), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
   return 0;
@@ -1850,13 +1764,9 @@ int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigne
 
 // Cout <= 64 with K a multiple of 288 (nine taps of 32 channels: K = 576, 1728): 288-column tiles
 // of nine 64x32 / 32x32 wave tiles, so no column tile is partly empty (K = 576 filled 2.25 of three
-// 256-column tiles).  SRPDE_H3P_288=0 restores the 256-column tiles.
+// 256-column tiles)
 static bool h3p_use288(int cout, int K) {
-  static const bool on = [] {
-    const char* e = getenv("SRPDE_H3P_288");
-    return !(e && e[0] == '0');
-  }();
-  return on && cout <= 64 && K % 288 == 0;
+  return cout <= 64 && K % 288 == 0;
 }
 
 static void h3p_tiles(int cout, int K, int* bm, int* bn) {
@@ -1874,11 +1784,7 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
   // The weight gradients run on a side stream next to the dgrad chain; half the workgroups of the
   // earlier 4-round target leave CUs to the critical path and halve the split-K reduction
   // (step 34.94 / 35.06 -> 34.56 / 34.59 ms same box; 256 the same, 128: 37.1 ms).
-  // SRPDE_WGRAD_WG overrides the target (tuning).
-  static const long long target = [] {
-    const char* e = getenv("SRPDE_WGRAD_WG");
-    return e ? std::max(1LL, atoll(e)) : 512LL;
-  }();
+  constexpr long long target = 512;
   const long long want = std::max(1LL, target / tiles);
   long long c = (P + want - 1) / want;
   c = (c + 31) / 32 * 32;
@@ -1890,18 +1796,13 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
 // h3h: the input-row-ring weight gradient for the 288-column shapes (one 32-channel input chunk x
 // nine taps per tile, the same tiles and split-K slabs as h3p's 288-column kernel) whose ring of
 // H3H_CAP rows holds a stage's reach: 3 stages of H3H_PS rows + 2 (W + 1) dil + alignment.
-// SRPDE_H3H=0: h3p instead.
 // pixels per stage and ring rows (measured: 32-pixel stages 3-10% slower; a fourth ring stage of
 // 32 or 64 pixels within 1-2%)
 constexpr int H3H_PS = 64, H3H_CAP = 512;
 // (Cout >= 128 would need 9 waves x 128 x 32 accumulators with the two-level chain: 168 VGPRs
 // and 312 B of spill scratch at three waves per SIMD -- not built; those layers keep h3p)
 static bool h3h_ok(int cout, int K, int cin, int w, int dil) {
-  static const bool on = [] {
-    const char* e = getenv("SRPDE_H3H");
-    return !(e && e[0] == '0');
-  }();
-  return on && h3p_use288(cout, K) && K == 9 * cin && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP;
+  return h3p_use288(cout, K) && K == 9 * cin && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP;
 }
 
 template <int BM, int PS, int NST, int CAP>
@@ -1983,12 +1884,6 @@ extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
 
-int srpde_conv_h3_set_half(int max_chunks) {
-  const int prev = h3_half_max();
-  g_h3_half.store(std::max(0, max_chunks));
-  return prev;
-}
-
 int srpde_conv_h3r_set(int on) {
   const int prev = h3r_on() ? 1 : 0;
   g_h3r.store(on ? 1 : 0);
@@ -2050,7 +1945,6 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   ConvParams p;
   p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0;
   p.x1 = x1; p.c1 = c1; p.ldx1 = ldx1 > 0 ? ldx1 : 4;
-  p.x0p = nullptr; p.x1p = nullptr;
   p.w = nullptr; p.bias = bias; p.y = y; p.ldy = ldy;
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
@@ -2066,21 +1960,13 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   a.amax1 = c1 ? amax1 : nullptr;
   a.halo = (w + 1) * dil;
   a.arows = h3_arows(w, dil);
-  static const int relax = [] {
-    const char* e = getenv("SRPDE_H3_RELAX");   // tuning/diagnostics: 0 = wait for every DMA each stage
-    return e ? atoi(e) : 1;
-  }();
-  a.relax = relax;
+  a.relax = 1;   // a stage waits only for its weight DMA; the halo slices land later
   a.xsplit = static_cast<_Float16*>(xsplit_out);
   SRPDE_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr) && (in_scale == nullptr || c1 == 0),
                   "srpde_conv_fwd_h3: in_scale / in_shift go together and need c1 == 0");
   a.in_scale = in_scale;
   a.in_shift = in_shift;
-  static const int wide_on = [] {
-    const char* e = getenv("SRPDE_H3_WIDE");   // tuning/diagnostics: 0 = one dword store per element
-    return e ? atoi(e) : 1;
-  }();
-  a.wide = wide_on && ldy % 4 == 0 && aligned16(y);
+  a.wide = ldy % 4 == 0 && aligned16(y);
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
                                           bn_ldy % 4 == 0 && cout % 4 == 0),
                   "srpde_conv_fwd_h3: the fused BN reduction needs bn_y/mean/invstd/gamma/beta and no accumulate");
@@ -2088,23 +1974,14 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
   p.out_max = out_max;
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
-  if (p.Cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) {   // shallow K: 128-row tiles, 2 per CU
-    a.arows = h3_arows(w, dil, 128);
-    switch (h3_cfg(cout)) {
-      case 1: return launch_fwd_h3<128, 128, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
-      case 2: return launch_fwd_h3<128, 64, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
-      default: return launch_fwd_h3<128, 32, 4, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes);
-    }
-  }
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);
   }
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_)                                                                        \
-  (tps >= 3 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 3>(p, a, stream, workspace, ws_bytes) \
-   : tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
-              : launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes))
+  (tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
+            : launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 1>(p, a, stream, workspace, ws_bytes))
   switch (h3_cfg(cout)) {
     case 1: return H3_LAUNCH(128);
     case 2: return H3_LAUNCH(64);
@@ -2136,7 +2013,6 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
   ConvParams p;
   p.x0 = da; p.c0 = cout_dy; p.ldx0 = ldda;
   p.x1 = nullptr; p.c1 = 0; p.ldx1 = 4;
-  p.x0p = nullptr; p.x1p = nullptr;
   p.w = nullptr; p.bias = nullptr; p.y = dx; p.ldy = lddx;
   p.stats = nullptr;
   p.N = n; p.H = h; p.W = w; p.Cout = cin_dx; p.ksize = 3; p.dil = dil; p.sign = -1; p.accumulate = 0;
@@ -2170,17 +2046,6 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
   // one tap per stage: the second fp32 halo tile takes the second weight stage's LDS.  (The
   // 128-column tile does not fit its registers with the fused transform -- 46 VGPRs of scratch --
   // so outputs with a multiple of 128 channels keep srpde_bn_relu_bwd + srpde_conv_fwd_h3.)
-  // the register-staged kernel for the BNB dgrads: measured slower in the step (34.41 / 34.54 vs
-  // 34.05 / 34.10 ms same box) -- the 64-column instantiation spills (140 B) around its halo loads,
-  // which the compiler then serialises -- so off unless SRPDE_H3R_BNB=1 (bit-equal either way)
-  static const int bnb_r = [] {
-    const char* e = getenv("SRPDE_H3R_BNB");
-    return e ? atoi(e) : 0;
-  }();
-  if (bnb_r && h3r_fits(h3_bn(h3_cfg(cin_dx)), a.arows)) {
-    if (h3_cfg(cin_dx) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
-    return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
-  }
   if (h3_cfg(cin_dx) == 2) return launch_fwd_h3<256, 64, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
   return launch_fwd_h3<256, 32, 8, 1, H3_SRB, true, 1, true>(p, a, stream, workspace, ws_bytes);
 }
@@ -2188,7 +2053,7 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
 // Number of output tiles (= out_max slots) srpde_conv_fwd_h3 uses for this shape; 0 if unsupported.
 long long srpde_conv_h3_tiles(long long P, int cin, int cout, int w, int dil) {
   if (P <= 0 || !srpde_conv_h3_supported(cin, 0, cout, w, dil, 3)) return 0;
-  const int bm = (cin / BK2 <= h3_half_max() && h3_arows(w, dil, 128) <= 256) ? 128 : 256;
+  const int bm = H3_BM;
   const int bn = h3_bn(h3_cfg(cout));
   return ((P + bm - 1) / bm) * ((cout + bn - 1) / bn);
 }

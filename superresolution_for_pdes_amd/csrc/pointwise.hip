@@ -335,57 +335,6 @@ __global__ __launch_bounds__(256) void upsample_fwd_px_kernel(const float* __res
   *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
 }
 
-// A decoder block's output BN + ReLU and the x2 align_corners upsample that reads it (models.py:22-23
-// then :89-93), in one pass: the four source pixels of each output pixel are activated on the fly
-// (relu(y * scale + shift), the train-mode affine of srpde_bn_affine) and interpolated with
-// upsample_fwd_px_kernel's expression, so the activation is never written.  amax: max|out| (one
-// same-address atomic per block: few, long blocks).
-__global__ __launch_bounds__(256) void bn_relu_upsample_fwd_kernel(const float* __restrict__ y, int ldy,
-                                                                   const float* __restrict__ scale,
-                                                                   const float* __restrict__ shift,
-                                                                   float* __restrict__ out, int ldo, int n, int H,
-                                                                   int W, int Ho, int Wo, int C, unsigned* amax) {
-  const int C4 = C >> 2;
-  const long long total = (long long)n * Ho * Wo * C4;
-  float mx = 0.f;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const long long q = e / C4;
-    const int c = (int)(e - q * C4) * 4;
-    const int ox = (int)(q % Wo);
-    const long long t = q / Wo;
-    const int oy = (int)(t % Ho);
-    const long long nb = t / Ho;
-    const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
-    const float* base = y + (size_t)nb * H * W * ldy + c;
-    const float4 sc = *reinterpret_cast<const float4*>(scale + c);
-    const float4 sh = *reinterpret_cast<const float4*>(shift + c);
-    float4 v[4];
-    v[0] = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i0) * ldy);
-    v[1] = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i1) * ldy);
-    v[2] = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i0) * ldy);
-    v[3] = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i1) * ldy);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k].x = fmaxf(fmaf(v[k].x, sc.x, sh.x), 0.f); v[k].y = fmaxf(fmaf(v[k].y, sc.y, sh.y), 0.f);
-      v[k].z = fmaxf(fmaf(v[k].z, sc.z, sh.z), 0.f); v[k].w = fmaxf(fmaf(v[k].w, sc.w, sh.w), 0.f);
-    }
-    const float4 a = v[0], b = v[1], d = v[2], f = v[3];
-    float4 o;
-#define UP(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
-    UP(x) UP(y) UP(z) UP(w)
-#undef UP
-    *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
-    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
-  }
-  if (amax == nullptr) return;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  __shared__ float wm[4];
-  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
-}
 
 // upsample_fwd_px_kernel plus the spatial attention of the gate that reads the upsampled tensor
 // (models.py:124-125: sa = sigmoid(conv1x1(g)) with g = up(d), models.py:89,92): the block's x
@@ -594,12 +543,8 @@ static bool upsample_gather_ok(int in, int out) { return out <= 1 || in <= 1 || 
 // the row-blocked kernel: input row i's candidate rows number at most floor(2/scale) + 1 (+1 for
 // rounding) <= ROWS_NS when 2/scale < 5; C/4 a power of two <= 256; one LDS row of Wo x C floats
 static bool upsample_rows_ok(int h, int w, int ho, int wo, int c, int lddo, int lddx) {
-  static const bool off = [] {
-    const char* e = getenv("SRPDE_UPSAMPLE_BWD");   // "px": the pixel-blocked gather (A/B)
-    return e != nullptr && strcmp(e, "px") == 0;
-  }();
   const int c4 = c / 4;
-  return !off && c % 4 == 0 && c4 >= 1 && c4 <= 256 && (c4 & (c4 - 1)) == 0 && lddo % 4 == 0 && lddx % 4 == 0 &&
+  return c % 4 == 0 && c4 >= 1 && c4 <= 256 && (c4 & (c4 - 1)) == 0 && lddo % 4 == 0 && lddx % 4 == 0 &&
          h > 1 && ho > 1 && 2.0 * (ho - 1) < 5.0 * (h - 1) && upsample_gather_ok(w, wo) &&
          (size_t)wo * c * sizeof(float) <= 64 * 1024;
 }
@@ -1182,18 +1127,6 @@ int srpde_upsample_bilinear_fwd(const float* x, int ldx, float* out, int ldo, in
   hipLaunchKernelGGL(upsample_fwd_kernel, dim3(grid_for((long long)n * ho * wo * (c / 4))), dim3(256), 0, stream, x,
                      ldx, out, ldo, n, h, w, ho, wo, c);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_fwd");
-  return 0;
-}
-
-int srpde_bn_relu_upsample_fwd(const float* y, int ldy, const float* scale, const float* shift, float* out, int ldo,
-                               int n, int h, int w, int ho, int wo, int c, unsigned* amax, hipStream_t stream) {
-  SRPDE_CHECK_ARG(y && scale && shift && out && c % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0 && ho >= h && wo >= w,
-                  "srpde_bn_relu_upsample_fwd: bad args");
-  const long long total = (long long)n * ho * wo * (c / 4);
-  const int blocks = (int)std::min<long long>((total + 255) / 256, amax ? 1024 : 8192);
-  hipLaunchKernelGGL(bn_relu_upsample_fwd_kernel, dim3(blocks), dim3(256), 0, stream, y, ldy, scale, shift, out, ldo,
-                     n, h, w, ho, wo, c, amax);
-  SRPDE_LAUNCH_CHECK("srpde_bn_relu_upsample_fwd");
   return 0;
 }
 

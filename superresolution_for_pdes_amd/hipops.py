@@ -36,24 +36,17 @@ _CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "h3")
 
 
 def set_conv_math(mode: str):
-    """Pick the conv kernel family (all HIP, all fp32-accurate):
+    """Pick the conv kernel family (both HIP, both fp32-accurate):
     'h3': three fp16-split MFMA products with power-of-two operand scales, halo-staged tiles;
-    'x6': six bf16-split MFMA products; 'f32': the fp32 MFMA kernels."""
+    'f32': the fp32 MFMA kernels (also the fallback for shapes h3 does not take)."""
     global _CONV_MATH
-    if mode not in ("h3", "x6", "f32"):
+    if mode not in ("h3", "f32"):
         raise ValueError(mode)
     _CONV_MATH = mode
 
 
 def conv_math() -> str:
     return _CONV_MATH
-
-
-def split_weights(wpack):
-    """fp32 packed weights -> [3, numel] bf16 planes (hi, mid, lo) for the x6 kernels."""
-    planes = torch.empty(3, wpack.numel(), dtype=torch.bfloat16, device=wpack.device)
-    call("srpde_split_weights", wpack.data_ptr(), planes.data_ptr(), wpack.numel(), stream_ptr())
-    return planes
 
 
 def split_weights_h3(wpack, rows):
@@ -72,9 +65,8 @@ def prepare_weights_h3(desc, nlayers, total_rows):
 
 
 def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
-    """Packed fp32 weights (fwd [Cout][tap][Cin], dgrad [Cin][tap][Cout]); in x6 mode each
-    packed tensor carries its bf16 split planes as ``.x6``, in h3 mode its fp16 planes and
-    row scales as ``.h3``."""
+    """Packed fp32 weights (fwd [Cout][tap][Cin], dgrad [Cin][tap][Cout]); in h3 mode each
+    packed tensor carries its fp16 split planes and row scales as ``.h3``."""
     cout, cin_real, kh, _ = w.shape
     taps = kh * kh
     wf = empty(cout * taps * cin_pad, device=w.device) if want_fwd else None
@@ -85,11 +77,6 @@ def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
             wf.h3 = split_weights_h3(wf, cout)
         if wd is not None and cin_pad % 16 == 0 and cout % 32 == 0:
             wd.h3 = split_weights_h3(wd, cin_pad)
-    if _CONV_MATH == "x6":
-        if wf is not None and query("srpde_conv_x6_supported", cin_pad, 0, cout):
-            wf.x6 = split_weights(wf)
-        if wd is not None and query("srpde_conv_x6_supported", cout, 0, cin_pad):
-            wd.x6 = split_weights(wd)
     return wf, wd
 
 
@@ -102,12 +89,6 @@ def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
     buf = empty(nblk, cout, 2, device=device)
     buf._srpde_rows = rows
     return buf, nblk, rows
-
-
-def set_h3_half(max_chunks: int) -> int:
-    """h3 tile choice: input depth (in 32-channel chunks) up to which the 128-row, two-per-CU
-    tile runs (0: never).  Returns the previous value."""
-    return int(query("srpde_conv_h3_set_half", int(max_chunks)))
 
 
 def set_h3r(on: bool) -> bool:
@@ -155,13 +136,6 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         "planes_out / in_affine / bn_bwd / out_max need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
-    if _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout):
-        planes = getattr(wpack, "x6", None)
-        if planes is None:
-            planes = split_weights(wpack)
-        call("srpde_conv_fwd_x6", p0, x0.shape[1], ld0, p1, c1, ld1, planes.data_ptr(), _p(bias), py, ldy,
-             n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
-        return
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
 
@@ -289,28 +263,6 @@ def _scratch(nbytes, device):
     return buf
 
 
-def split_planes(x):
-    """[P, c] fp32 view -> [3, P, c] bf16 planes (hi, mid, lo; exact truncation split)."""
-    P, c = x.shape
-    px, ld = _pl(x)
-    planes = torch.empty(3, P, c, dtype=torch.bfloat16, device=x.device)
-    call("srpde_split_planes", px, ld, c, P, planes.data_ptr(), stream_ptr())
-    return planes
-
-
-def conv_fwd_x6p(x0p, x1p, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None):
-    """x6 convolution on pre-split inputs (split_planes of each input half)."""
-    c0 = x0p.shape[2]
-    c1 = x1p.shape[2] if x1p is not None else 0
-    py, ldy = _pl(y)
-    ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
-    planes = getattr(wpack, "x6", None)
-    if planes is None:
-        planes = split_weights(wpack)
-    call("srpde_conv_fwd_x6p", x0p.data_ptr(), c0, _p(x1p), c1, planes.data_ptr(), _p(bias), py, ldy,
-         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
-
-
 def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cout = dy.shape[1]
     pdy, lddy = _pl(dy)
@@ -330,24 +282,8 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
              p1, c1, ld1, _p(a1), dw.data_ptr(), cin_real, int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(),
              ws_bytes, stream_ptr())
         return
-    x6 = _CONV_MATH == "x6" and query("srpde_conv_x6_supported", x0.shape[1], c1, cout)
-    call("srpde_conv_wgrad_x6" if x6 else "srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1,
-         dw.data_ptr(), cin_real,
+    call("srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1, dw.data_ptr(), cin_real,
          int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
-
-
-def conv_wgrad_bnb_c3(y, da, mean, invstd, gamma, beta, m1, m2, x, dw, n, h, w, dil=1, relu=True, accumulate=False):
-    """srpde_conv_wgrad_bnb_c3: dW of a conv on a 3-channel input from the BN (+ReLU) backward terms
-    (m1, m2 of bn_bwd_prepare) -- dy = gamma*invstd*(dz - m1 - xhat*m2) is formed on the fly."""
-    P, cout = y.shape
-    py, ldy = _pl(y)
-    pda, ldda = _pl(da)
-    px, ldx = _pl(x)
-    ws_bytes = int(query("srpde_conv_wgrad_bnb_c3_workspace_size", P, cout))
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
-    call("srpde_conv_wgrad_bnb_c3", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
-         beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), BN_RELU if relu else 0, px, ldx, dw.data_ptr(),
-         int(accumulate), n, h, w, cout, dil, ws.data_ptr(), ws_bytes, stream_ptr())
 
 
 def split_planes_buffer(P, c, device):
@@ -529,17 +465,6 @@ def upsample_fwd(x, n, h, w, ho, wo, out=None):
     po, ldo = _pl(out)
     call("srpde_upsample_bilinear_fwd", px, ldx, po, ldo, n, h, w, ho, wo, c, stream_ptr())
     return tag_amax(out, getattr(x, "_srpde_amax", None))   # convex combinations of inputs
-
-
-def bn_relu_upsample_fwd(y, aff, n, h, w, ho, wo, amax=None):
-    """upsample_fwd(relu(y * scale + shift)) with ``aff = (scale, shift)`` (bn_affine), one pass."""
-    c = y.shape[1]
-    out = empty(n * ho * wo, c, device=y.device)
-    py, ldy = _pl(y)
-    po, ldo = _pl(out)
-    call("srpde_bn_relu_upsample_fwd", py, ldy, aff[0].data_ptr(), aff[1].data_ptr(), po, ldo, n, h, w, ho, wo, c,
-         _p(amax), stream_ptr())
-    return tag_amax(out, amax)
 
 
 def upsample_gate_fwd(x, n, h, w, ho, wo, wg, bg):

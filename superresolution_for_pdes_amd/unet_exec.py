@@ -264,7 +264,6 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
 
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
 _FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
-_FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "0") == "1"
 # the gates' spatial attention formed by the upsample that produces their gating input
 # (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
 _FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
@@ -302,8 +301,7 @@ class WgradStream:
         key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
         side = WgradStream._streams.get(key)
         if side is None:
-            frac = float(os.environ.get("SRPDE_WGRAD_CU_FRACTION", "1"))
-            side = _cu_masked_stream(dev, frac) if frac < 1 else torch.cuda.Stream(device=dev)
+            side = torch.cuda.Stream(device=dev)
             WgradStream._streams[key] = side
         self.side = side
 
@@ -317,28 +315,6 @@ class WgradStream:
 
     def join(self):
         self.main.wait_stream(self.side)
-
-
-def _cu_masked_stream(dev, frac):
-    """A HIP stream whose kernels may only use ``frac`` of the CUs (hipExtStreamCreateWithCUMask;
-    every CU index i with i % 8 < round(8 frac) kept), wrapped for torch.  Tuning knob
-    SRPDE_WGRAD_CU_FRACTION: bounds the weight-gradient side stream's CU footprint so the compute
-    stream's kernels always find free CUs."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    words = (ncu + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    keep = max(1, min(8, round(8 * frac)))
-    for i in range(ncu):
-        if i % 8 < keep:
-            mask[i // 32] |= 1 << (i % 32)
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(words), mask)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
-    return torch.cuda.ExternalStream(handle.value, device=dev)
 
 
 # weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
@@ -405,14 +381,6 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         else:
             wq.submit(fn, keep)
         return None if out_part is None else (out_part, dx_max)
-    if (_FUSE_C3 and train and dx is None and x0 is not None and x1 is None and conv.in_channels == 3
-            and x0.shape[1] >= 4 and cout in (16, 32, 64)):
-        # the network's first conv (no input gradient wanted): its BN backward apply runs inside the
-        # weight-gradient kernel, on the compute stream (nothing else is left to overlap with)
-        m1, m2, _ = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
-                                     grads[conv.bias], part=part_t, da_max=da_max)
-        H.conv_wgrad_bnb_c3(y, da, mean, invstd, bn.weight, bn.bias, m1, m2, x0, grads[conv.weight], n, h, w, dil)
-        return None
     dy = H.empty(P, cout, device=y.device)
     # eval mode: the forward normalised with the running statistics (constants), so the BN
     # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
@@ -449,17 +417,10 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
 # the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
 # (srpde_conv_dgrad_h3_bnb; SRPDE_FUSE_BN_APPLY=0: off)
 _FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
-# layers it is taken for: dgrad output channels <= _BNB_MAX_CIN, dy channels >= _BNB_MIN_COUT
-# (SRPDE_BNB_WIDE=1: also dec1.conv1's 3-tile dgrad and out_conv1's one-chunk dy)
-_BNB_WIDE = os.environ.get("SRPDE_BNB_WIDE", "0") == "1"
-_BNB_MAX_CIN, _BNB_MIN_COUT = (192, 32) if _BNB_WIDE else (64, 64)
-
-
-# the first conv's BN backward apply fused into its weight gradient (srpde_conv_wgrad_bnb_c3):
-# 362 us against 417 + 182 us for the separate passes alone, but in the step it shares the GPU with
-# enc1.conv2's concurrent weight gradient, which sets the tail either way (measured +0.06 /
-# +0.09 / -0.02 ms on three boxes), so off unless SRPDE_FUSE_C3=1
-_FUSE_C3 = os.environ.get("SRPDE_FUSE_C3", "0") == "1"
+# layers it is taken for: dgrad output channels <= _BNB_MAX_CIN (one output-column tile), dy channels
+# >= _BNB_MIN_COUT (two input chunks); wider (dec1.conv1's 3-tile dgrad, out_conv1's one-chunk dy)
+# measured +0.5 ms in the step
+_BNB_MAX_CIN, _BNB_MIN_COUT = 64, 64
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
 _FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"
@@ -530,29 +491,11 @@ def _upsample_for_gate(d, att, n, h, w, ho, wo):
     return H.upsample_fwd(d, n, h, w, ho, wo), None
 
 
-# SRPDE_ATT_EARLY=1: the attention gates' channel attention (models.py:119-121: a function of the
-# encoder output alone) runs on the side stream as soon as that output exists, beside the encoder /
-# bridge convolutions, instead of in line.  Measured step-neutral (33.26 vs 33.30 ms, 3 reps same
-# box): the convolutions it runs beside already fill the GPU, so it is off by default
-_ATT_EARLY = os.environ.get("SRPDE_ATT_EARLY", "0") == "1"
-
-
 def _att_channel_early(att, x, n, hw):
-    """Launch att's channel attention of x now; returns what _att_fwd(early=...) takes."""
+    """att's channel attention of x (models.py:119-121: a function of the encoder output alone), in
+    line; returns what _att_fwd(early=...) takes."""
     c1, c3, _ = _att_params(att)
-    args = (x, n, hw, c1.weight, c1.bias, c3.weight, c3.bias)
-    if not (_ATT_EARLY and x.is_cuda) or torch.cuda.is_current_stream_capturing():
-        return H.att_channel_fwd(*args), None
-    main = torch.cuda.current_stream(x.device)
-    side = WgradStream(x.device).side
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        chan = H.att_channel_fwd(*args)
-    for t in chan:
-        t.record_stream(main)     # allocated on the side stream, consumed on this one
-    ev = torch.cuda.Event()
-    ev.record(side)
-    return chan, ev
+    return H.att_channel_fwd(x, n, hw, c1.weight, c1.bias, c3.weight, c3.bias), None
 
 
 def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None):
@@ -589,8 +532,8 @@ def unet_forward(m, x, training, save=False):
     x4 = H.nchw_to_nhwc(x, 4)
     S.x4 = x4
     prepare_h3_weights(m)
-    # max|x| words of the 16 BN+ReLU outputs and the 2 fused upsamples (h3 operand scales)
-    slots = H.AmaxSlots(18, x.device)
+    # max|x| words of the 16 BN+ReLU outputs (h3 operand scales)
+    slots = H.AmaxSlots(16, x.device)
     # encoder
     (e1, p1, ch1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True, att=m.att1)
     (e2, p2, ch2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True, att=m.att2)
@@ -600,21 +543,11 @@ def unet_forward(m, x, training, save=False):
                                          training, 2, slots, gate=m.att3)
     # decoder with attention, virtual concat
     e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3, early=ch3, sa=sa3)
-    # SRPDE_FUSE_UP=1: dec3's / dec2's output BN + ReLU applied inside the upsample that reads it
-    # (train mode; d3 / d2 never written) -- measured step-neutral (33.02 vs 33.03 ms, 4 reps), off
-    if training and _FUSE_UP:
-        (d3y, d3aff), S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots, activate=False)
-        u3, sa2 = H.bn_relu_upsample_fwd(d3y, d3aff, n, h3, w3, h2, w2, amax=slots.take()), None
-    else:
-        d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
-        u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2)
+    d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
+    u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2)
     e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2, sa=sa2)
-    if training and _FUSE_UP:
-        (d2y, d2aff), S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots, activate=False)
-        u2, sa1 = H.bn_relu_upsample_fwd(d2y, d2aff, n, h2, w2, h, w, amax=slots.take()), None
-    else:
-        d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
-        u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w)
+    d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
+    u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1, sa=sa1)
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
     # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)

@@ -26,7 +26,7 @@ def pytest_collection_modifyitems(config, items):
 
 @pytest.fixture
 def conv_math():
-    """Restores the conv kernel family (x6 / f32) a test switched."""
+    """Restores the conv kernel family (h3 / f32) a test switched."""
     from superresolution_for_pdes_amd import hipops as H
     before = H.conv_math()
     yield before

@@ -27,6 +27,14 @@ Fixtures:
   cascade640_fixture.npz  solve_multi_resolution(40,[80..640]) + ml_multi_level_upscale to
                        320 and 640, plus the bilinear / bicubic multi-level and direct baselines
                        (resolution_comparison_enhanced.py:19-65, :355-408) and their metrics
+  init_fixture.npz     torch.manual_seed(42); UNet().apply(init_weights) as train_enhanced.main
+                       does (:187-189, :303-304): per-parameter norms, sums and strided samples
+  report_fixture.npz   compare_test_cases.generate_test_data + evaluate_dataset (:12-247) with
+                       seeded np.random, constant and varying theta: the test sets and the
+                       per-sample bilinear / ML metrics of the reference's fp32 CPU model
+  cascade20_fixture.npz  config #5 exactly (20 -> 640, five 2x applies) with bounded weights (the
+                       fixture state, final.weight x 1e-3: the residual dominates, every level stays
+                       in the physical range), strided 320^2 / 640^2 outputs and their metrics
 
 Usage: ``make_golden.py [name ...]`` (default: the four fast fixtures; ``unet_b1024`` and
 ``cascade640`` take minutes and are generated on request).
@@ -65,6 +73,7 @@ class _Writer:
 tb.SummaryWriter = _Writer
 sys.modules["torch.utils.tensorboard"] = tb
 sys.modules["seaborn"] = types.ModuleType("seaborn")
+sys.modules["seaborn"].kdeplot = lambda *a, **k: None     # plot-only (compare_test_cases.py:225-226)
 
 import models as ref_models  # noqa: E402  (reference)
 import data_generation as ref_dg  # noqa: E402
@@ -320,7 +329,81 @@ def cascade640_fixture():
     np.savez_compressed(os.path.join(HERE, "cascade640_fixture.npz"), **out)
 
 
-FIXTURES = {"unet": unet_fixture, "poisson": poisson_fixture, "datagen": datagen_fixture,
+def init_fixture():
+    """M10: the reference's seeded initialisation (models.py:209-222 applied after seed 42)."""
+    torch.manual_seed(42)
+    m = ref_models.UNet()
+    m.apply(ref_models.init_weights)
+    out = {}
+    for k, v in m.state_dict().items():
+        f = v.detach().reshape(-1).double()
+        if v.is_floating_point():
+            out[f"norm:{k}"] = np.array(float(f.norm()))
+            out[f"sum:{k}"] = np.array(float(f.sum()))
+            out[f"sample:{k}"] = f[:: max(1, f.numel() // 64)][:64].numpy()
+        else:
+            out[f"int:{k}"] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "init_fixture.npz"), **out)
+
+
+def report_fixture():
+    """compare_test_cases.py:12-247 on seeded draws (it writes data/*.npz and PNGs: run in a
+    scratch directory)."""
+    import tempfile
+    from pathlib import Path
+    import compare_test_cases as ref_ct
+    m = ref_model(torch.float32).eval()
+    out = {}
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        try:
+            for tag, const in (("const", True), ("var", False)):
+                np.random.seed(3)
+                d = ref_ct.generate_test_data((1.0, 6.0), 6, f"t_{tag}", constant_theta=const)
+                for key in ("k1", "k2", "u_fine", "u_coarse", "theta_fine", "theta_coarse", "f_fine"):
+                    out[f"{tag}:{key}"] = np.asarray(d[key])
+                metrics, avg = ref_ct.evaluate_dataset(d, m, "cpu", Path(td), f"t_{tag}")
+                out[f"{tag}:metrics"] = np.array([[mm[k] for k in ("bilinear_mae", "bilinear_rmse", "ml_mae",
+                                                                     "ml_rmse")] for mm in metrics])
+                out[f"{tag}:avg"] = np.array([avg[k] for k in ("avg_bilinear_mae", "avg_bilinear_rmse",
+                                                               "avg_ml_mae", "avg_ml_rmse")])
+        finally:
+            os.chdir(cwd)
+    np.savez_compressed(os.path.join(HERE, "report_fixture.npz"), **out)
+
+
+CASCADE20_FINAL_SCALE = 1e-3
+
+
+def cascade20_fixture():
+    """Config #5 at the physical bar: 20 -> 640 with the fixture weights, final.weight scaled by
+    1e-3 so that the residual path dominates and the cascade stays physical at every level (with
+    the raw random weights each level feeds an O(1) prediction back, resolution_comparison.py:191-226).
+    The reference hard-codes 40 as the start (:188): its 20 -> 40 level is composed from its own
+    upscale_subdomain with the level loop's GT normalisation (:196-201), as cascade640_fixture does."""
+    torch.set_num_threads(os.cpu_count())
+    m = ref_model(torch.float32).eval()
+    with torch.no_grad():
+        m.final.weight.mul_(CASCADE20_FINAL_SCALE)
+    np.random.seed(0)
+    d20 = ref_rc.solve_multi_resolution(20, [40, 80, 160, 320, 640])
+    gn = ref_rc.GlobalNormalization(d20["u"][40], d20["u"][20], d20["f"][40], d20["theta"][40])
+    u40 = ref_rc.upscale_subdomain(m, d20["u"][20], d20["f"][40], d20["theta"][40], gn, "cpu")
+    out = {"u20": d20["u"][20], "ml40": u40, "final_scale": np.array(CASCADE20_FINAL_SCALE)}
+    for tgt, (sr, sc) in ((80, (1, 1)), (160, (1, 1)), (320, (2, 3)), (640, (3, 5))):
+        d = dict(d20)
+        d["u"] = dict(d20["u"])
+        d["u"][40] = u40
+        ml = ref_rc.ml_multi_level_upscale(m, d, tgt, "cpu")
+        e = ml - d20["u"][tgt]
+        out[f"ml{tgt}"] = ml[::sr, ::sc].copy()
+        out[f"ml{tgt}_metrics"] = np.array([np.mean(np.abs(e)), np.sqrt(np.mean(e ** 2))])
+    np.savez_compressed(os.path.join(HERE, "cascade20_fixture.npz"), **out)
+
+
+FIXTURES = {"init": init_fixture, "report": report_fixture, "cascade20": cascade20_fixture,
+            "unet": unet_fixture, "poisson": poisson_fixture, "datagen": datagen_fixture,
             "cascade": cascade_fixture, "unet_b1024": unet_b1024_fixture, "cascade640": cascade640_fixture}
 
 if __name__ == "__main__":

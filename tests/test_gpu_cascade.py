@@ -176,6 +176,36 @@ def test_cascade_20_to_640_matches_reference(golden):
     assert abs(mt["mae"] - want[0]) <= 1e-3 * want[0] and abs(mt["rmse"] - want[1]) <= 1e-3 * want[1], mt
 
 
+def test_cascade_20_to_640_physical_bar():
+    """Config #5 exactly (20 -> 640, five 2x applies: 1, 4, 16, 64, 256 tiles) at the north-star
+    physical bar.  cascade20_fixture is the reference's procedure (resolution_comparison.py:183-229,
+    its 20 -> 40 level from its own upscale_subdomain) with the fixture weights and final.weight
+    x 1e-3, so every level stays in the physical range (the test above explains why the raw random
+    weights do not).  Bars: physical RMSE <= 1e-5 against the reference at 80 ... 640 (strided
+    subgrids at 320^2 / 640^2) and metrics against the 640^2 ground truth within 1e-5 relative."""
+    import os
+    from state import fixture_state_torch
+    from superresolution_for_pdes_amd.models import UNet
+    from superresolution_for_pdes_amd.resolution_comparison import cascade_metrics, ml_multi_level_upscale
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "cascade20_fixture.npz"))
+    data = _gt_640(start=20)
+    assert np.linalg.norm(data["u"][20] - z["u20"]) <= 1e-10 * np.linalg.norm(z["u20"])
+    st = fixture_state_torch()
+    st["final.weight"] = st["final.weight"] * float(z["final_scale"])
+    m = UNet()
+    m.load_state_dict(st)
+    m = m.cuda().eval()
+    for tgt, (sr, sc) in ((80, (1, 1)), (160, (1, 1)), (320, (2, 3)), (640, (3, 5))):
+        out = ml_multi_level_upscale(m, data, tgt, "cuda", start_resolution=20)
+        ref = z[f"ml{tgt}"]
+        err = _rmse(out[::sr, ::sc], ref)
+        assert err <= 1e-5, (tgt, err)
+        assert err <= 1e-5 * float(np.sqrt(np.mean(ref ** 2))), (tgt, err)   # and relative to the field
+        mt = cascade_metrics(out, data["u"][tgt])
+        want = z[f"ml{tgt}_metrics"]
+        assert abs(mt["mae"] - want[0]) <= 1e-5 * want[0] and abs(mt["rmse"] - want[1]) <= 1e-5 * want[1], (tgt, mt)
+
+
 def test_interpolation_baselines_match_reference(golden):
     """Multi-level and direct bilinear / bicubic baselines (resolution_comparison_enhanced.py:19-65,
     :371-392) on the HIP resize kernels vs the reference's F.interpolate outputs (fixture: 80^2 and

@@ -33,7 +33,7 @@ def rel(a, b):
     (3, 256, 128, 128, 20, 1), (5, 16, 0, 128, 6, 1),
     # ragged: P % 32 != 0, Cout not a tile multiple, K = 864 not a tile multiple, dil 2 on 7x7
     (3, 64, 32, 96, 7, 2), (16, 128, 0, 128, 20, 1)])
-@pytest.mark.parametrize("math", ["h3", "x6", "f32"])
+@pytest.mark.parametrize("math", ["h3", "f32"])
 def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
     from superresolution_for_pdes_amd import hipops as H
     H.set_conv_math(math)
@@ -76,10 +76,9 @@ def test_conv_fwd_dgrad_wgrad(n, cin0, cin1, cout, h, dil, math, conv_math):
 
 @pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(512, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 0, 32, 40, 1)])
 def test_conv_split_kernels_are_fp32_accurate(cin0, cin1, cout, h, dil, conv_math):
-    """The split-operand convs against fp64: the bf16 three-piece (x6) and the scaled fp16
-    two-piece (h3) kernels must sit at the fp32 kernel's error level (all far below the
-    2^-16-relative error of a 2-piece bf16 split).  Bars: < 1e-6 relative L2, and x6 within
-    2x / h3 within 3x of the fp32-MFMA kernel's own error (+1e-7)."""
+    """The split-operand conv against fp64: the scaled fp16 two-piece (h3) kernels must sit at the
+    fp32 kernel's error level (far below the 2^-16-relative error of a 2-piece bf16 split).  Bars:
+    < 1e-6 relative L2, and within 3x of the fp32-MFMA kernel's own error (+1e-7)."""
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator().manual_seed(cin0 + cout)
     n, cin = 4, cin0 + cin1
@@ -93,7 +92,7 @@ def test_conv_split_kernels_are_fp32_accurate(cin0, cin1, cout, h, dil, conv_mat
     x0, x1 = (xr[:, :cin0], xr[:, cin0:]) if cin1 else (xr, None)
     dyr = rows(dy.float()).to(DEV)
     errs = {}
-    for math in ("f32", "x6", "h3"):
+    for math in ("f32", "h3"):
         H.set_conv_math(math)
         wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
         y = H.empty(n * h * h, cout, device=DEV)
@@ -106,37 +105,8 @@ def test_conv_split_kernels_are_fp32_accurate(cin0, cin1, cout, h, dil, conv_mat
         errs[math] = (rel(unrows(y, n, h, h), y64), rel(unrows(dx, n, h, h), dx64), rel(dw, dw64))
     print(f"conv fp64 errors (fwd, dgrad, wgrad): {errs}")
     for k in range(3):
-        assert errs["x6"][k] < 1e-6, errs
-        assert errs["x6"][k] < 2.0 * errs["f32"][k] + 1e-7, errs
         assert errs["h3"][k] < 1e-6, errs
         assert errs["h3"][k] < 3.0 * errs["f32"][k] + 1e-7, errs
-
-
-@pytest.mark.parametrize("cin0,cin1,cout,h,dil", [(256, 0, 512, 10, 2), (128, 64, 64, 40, 1), (64, 32, 96, 7, 1)])
-def test_conv_x6p_equals_x6(cin0, cin1, cout, h, dil, conv_math):
-    """Pre-split planes (split_planes + conv_fwd_x6p) reproduce the in-register split
-    bit for bit: same split, same products, same accumulation order."""
-    from superresolution_for_pdes_amd import hipops as H
-    H.set_conv_math("x6")
-    g = torch.Generator().manual_seed(cin0 + 7 * cout)
-    n, cin = 3, cin0 + cin1
-    x = rows(torch.randn(n, cin, h, h, generator=g)).to(DEV)
-    x0, x1 = (x[:, :cin0], x[:, cin0:]) if cin1 else (x, None)
-    wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(DEV)
-    b = torch.randn(cout, generator=g).to(DEV)
-    wf, wd = H.pack_conv_weights(wt, cin, want_dgrad=True)
-    st1, nblk, rpb = H.conv_stats_buffer(n, h, h, cout, DEV, cin0, cin1, dil)
-    st2 = torch.empty_like(st1)
-    y1, y2 = H.empty(n * h * h, cout, device=DEV), H.empty(n * h * h, cout, device=DEV)
-    H.conv_fwd(x0, x1, wf, b, y1, n, h, h, cout, 3, dil, 1, False, st1)
-    H.conv_fwd_x6p(H.split_planes(x0), H.split_planes(x1) if x1 is not None else None, wf, b, y2, n, h, h, cout, 3,
-                   dil, 1, False, st2)
-    dy = rows(torch.randn(n, cout, h, h, generator=g)).to(DEV)
-    d1, d2 = H.empty(n * h * h, cin, device=DEV), H.empty(n * h * h, cin, device=DEV)
-    H.conv_fwd(dy, None, wd, None, d1, n, h, h, cin, 3, dil, -1, False, None)
-    H.conv_fwd_x6p(H.split_planes(dy), None, wd, None, d2, n, h, h, cin, 3, dil, -1, False, None)
-    torch.cuda.synchronize()
-    assert torch.equal(y1, y2) and torch.equal(st1, st2) and torch.equal(d1, d2)
 
 
 def test_conv_cin_pad_and_accumulate():
@@ -474,46 +444,6 @@ def test_batched_weight_prep_matches_per_layer(conv_math):
                 assert torch.equal(got.h3[0], ref[0]) and torch.equal(got.h3[1], ref[1]), name
                 checked += 1
     assert checked >= 25, checked
-
-
-@pytest.mark.parametrize("n,h,cout,dil", [(3, 40, 64, 1), (2, 13, 32, 1), (2, 9, 16, 2)])
-def test_wgrad_bnb_c3_matches_separate_pass(n, h, cout, dil):
-    """srpde_conv_wgrad_bnb_c3 (the first conv's weight gradient with its BN + ReLU backward formed
-    on the fly) equals the separate apply (srpde_bn_relu_bwd) + fp32 weight gradient to summation
-    order (<= 2e-6 relative), and both match fp64 (<= 1e-5); the input's 4th (padding) column is
-    ignored; the BN parameter / conv-bias gradients from bn_bwd_prepare equal the separate pass's."""
-    from superresolution_for_pdes_amd import hipops as H
-    g = torch.Generator().manual_seed(cout * 7 + h)
-    P = n * h * h
-    x = torch.randn(P, 4, generator=g)
-    x[:, 3] = 1e3   # padding column: must not contribute
-    y = torch.randn(P, cout, generator=g) * 2 + 0.3
-    da = torch.randn(P, cout, generator=g) * 1e-2
-    mean = y.mean(0)
-    invstd = 1.0 / torch.sqrt(y.var(0, unbiased=False) + 1e-5)
-    gam, bet = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.3
-    y, da, x, mean, invstd, gam, bet = (t.to(DEV) for t in (y, da, x, mean, invstd, gam, bet))
-    z = lambda: torch.zeros(cout, device=DEV)  # noqa: E731
-    dy = H.empty(P, cout, device=DEV)
-    dg1, db1, dc1 = z(), z(), z()
-    H.bn_relu_bwd(y, da, mean, invstd, gam, bet, dy, dg1, db1, dc1)
-    dw_ref = torch.empty(cout, 3, 3, 3, device=DEV)
-    H.conv_wgrad(dy, x, None, dw_ref, n, h, h, 3, dil)
-    dg2, db2, dc2 = z(), z(), z()
-    m1, m2, _ = H.bn_bwd_prepare(y, da, mean, invstd, gam, bet, dg2, db2, dc2)
-    dw = torch.empty(cout, 3, 3, 3, device=DEV)
-    H.conv_wgrad_bnb_c3(y, da, mean, invstd, gam, bet, m1, m2, x, dw, n, h, h, dil)
-    torch.cuda.synchronize()
-    x64 = x[:, :3].double().cpu().view(n, h, h, 3).permute(0, 3, 1, 2)
-    dy64 = dy.double().cpu().view(n, h, h, cout).permute(0, 3, 1, 2)
-    dw64 = torch.nn.grad.conv2d_weight(x64, (cout, 3, 3, 3), dy64, padding=dil, dilation=dil)
-    assert rel(dw, dw_ref) < 2e-6, rel(dw, dw_ref)
-    assert rel(dw, dw64) < 1e-5 and rel(dw_ref, dw64) < 1e-5, (rel(dw, dw64), rel(dw_ref, dw64))
-    for a, b in ((dg1, dg2), (db1, db2)):
-        assert rel(a, b) < 1e-6
-    # conv-bias gradient sum(dy) = 0 for batch statistics: both are rounding noise around it
-    scale = float(dy.abs().sum(0).max())
-    assert float(dc1.abs().max()) <= 1e-5 * scale and float(dc2.abs().max()) <= 1e-5 * scale
 
 
 @pytest.mark.parametrize("n,h,w", [(3, 40, 40), (2, 13, 7)])

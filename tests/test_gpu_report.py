@@ -1,9 +1,14 @@
-"""Evaluation report (compare_test_cases.py) against the reference's procedure.
+"""Evaluation report (compare_test_cases.py) against the reference.
 
-The reference procedure is restated here on the CPU: its test-set draws (numpy global RNG, k
+``test_report_matches_reference_fixture`` pins it to the reference itself: report_fixture.npz is
+the reference's generate_test_data + evaluate_dataset (compare_test_cases.py:12-247) run on seeded
+draws with its fp32 CPU model (tests/golden/make_golden.py report).  The older procedure test
+below restates the reference on the CPU: its test-set draws (numpy global RNG, k
 then theta, compare_test_cases.py:12-68), scipy ground truth (oracle/poisson_ref), PDEDataset
 normalisation as torch-CPU fp32 expressions (models.py:155-187), a per-sample fp64 oracle forward
 (oracle/unet_ref), torch's bilinear resize and numpy MAE / RMSE (:113-135)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -34,6 +39,36 @@ def _reference_metrics(data, st64):
                     "ml_mae": float(np.mean(np.abs(ml - fine))),
                     "ml_rmse": float(np.sqrt(np.mean((ml - fine) ** 2)))})
     return out
+
+
+@pytest.mark.parametrize("constant_theta", [True, False])
+def test_report_matches_reference_fixture(constant_theta):
+    """Same seed -> the reference's test set (k draws, theta fields exactly; u to 1e-10), and the
+    per-sample / average metrics of the HIP model equal the reference's (bilinear 1e-6, ML 1e-4)."""
+    from state import fixture_state_torch
+    from superresolution_for_pdes_amd import compare_test_cases as CT
+    from superresolution_for_pdes_amd.models import UNet
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "report_fixture.npz"))
+    tag = "const" if constant_theta else "var"
+    np.random.seed(3)
+    data = CT.generate_test_data((1.0, 6.0), 6, "t", constant_theta=constant_theta)
+    for key in ("k1", "k2", "theta_fine", "theta_coarse", "f_fine"):
+        assert np.array_equal(np.asarray(data[key]), z[f"{tag}:{key}"]), key
+    for key in ("u_fine", "u_coarse"):
+        ref = z[f"{tag}:{key}"]
+        assert np.linalg.norm(np.asarray(data[key]) - ref) <= 1e-10 * np.linalg.norm(ref), key
+    m = UNet()
+    m.load_state_dict(fixture_state_torch())
+    m = m.cuda().eval()
+    metrics, avg = CT.evaluate_dataset(data, m, "cuda")
+    got = np.array([[mm[k] for k in ("bilinear_mae", "bilinear_rmse", "ml_mae", "ml_rmse")] for mm in metrics])
+    want = z[f"{tag}:metrics"]
+    assert got.shape == want.shape
+    assert np.all(np.abs(got[:, :2] - want[:, :2]) <= 1e-6 * want[:, :2]), (got[:, :2], want[:, :2])
+    assert np.all(np.abs(got[:, 2:] - want[:, 2:]) <= 1e-4 * want[:, 2:]), (got[:, 2:], want[:, 2:])
+    wavg = z[f"{tag}:avg"]
+    gavg = np.array([avg[k] for k in ("avg_bilinear_mae", "avg_bilinear_rmse", "avg_ml_mae", "avg_ml_rmse")])
+    assert np.all(np.abs(gavg - wavg) <= 1e-4 * wavg)
 
 
 @pytest.mark.parametrize("constant_theta", [True, False])

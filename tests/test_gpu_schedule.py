@@ -2,8 +2,8 @@
 
 Every kernel on the path is deterministic (fixed-order reductions, no float atomics), so
 moving launches between streams (unet_exec.WgradStream: weight gradients on a side stream)
-or changing which workgroup computes which tile (the persistent walk of the h3 convolution,
-srpde_conv_h3_set_persistent) must not change a single bit.  Anything else is a race or a
+or changing which kernel computes a tile (the register-staged h3r kernel against the 8-wave one,
+srpde_conv_h3r_set) must not change a single bit.  Anything else is a race or a
 wrong tile, which a tolerance-based parity test could hide.
 """
 import os
@@ -126,46 +126,6 @@ def test_reducer_buckets_wait_for_their_gradients():
         assert torch.equal(a[1][n] * 3.0, p.grad), n
 
 
-@pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (6, 256, 0, 512, 10, 2),
-                                                 (4, 256, 128, 128, 20, 1), (3, 64, 0, 32, 40, 1),
-                                                 (5, 128, 64, 64, 40, 1)])
-def test_conv_h3_half_tiles_equal_full_tiles(n, c0, c1, cout, hw, dil):
-    """The 128-row, two-per-CU h3 tile computes every output element, BN partial and stored
-    split in the same order as the 256-row tile (no K-split tail at these sizes): equal bits."""
-    from superresolution_for_pdes_amd import hipops as H
-    if H.conv_math() != "h3" or not (H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, c0 + c1, hw, dil)):
-        pytest.skip("not an h3 shape")
-    g = torch.Generator(device=DEV).manual_seed(3)
-    P, cin = n * hw * hw, c0 + c1
-    x = torch.randn(P, cin, device=DEV, generator=g)
-    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
-    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
-    b = torch.randn(cout, device=DEV, generator=g)
-    wf, wd = H.pack_conv_weights(w, cin, True, True)
-    dy = torch.randn(P, cout, device=DEV, generator=g)
-    for t in (x0, x1, dy):
-        if t is not None:
-            t._srpde_amax = H.amax_of(t)
-    outs = []
-    prev = H.set_h3_half(0)
-    try:
-        for half in (0, 99):
-            H.set_h3_half(half)
-            y = torch.empty(P, cout, device=DEV)
-            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
-            xp = H.split_planes_buffer(P, cin, DEV)
-            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
-            dx = torch.empty(P, cin, device=DEV)
-            dyp = H.split_planes_buffer(P, cout, DEV)
-            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
-            torch.cuda.synchronize()
-            outs.append((y, stats, xp, dx, dyp))
-    finally:
-        H.set_h3_half(prev)
-    for k, (a, b_) in enumerate(zip(*outs)):
-        assert torch.equal(a, b_), k
-
-
 @pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [(4, 64, 0, 64, 40, 1), (5, 128, 64, 64, 40, 1), (3, 64, 0, 32, 40, 1),
                                                  (4, 32, 0, 16, 40, 1), (6, 128, 0, 64, 20, 1), (2, 64, 0, 64, 10, 2)])
 def test_conv_h3r_equals_8wave(n, c0, c1, cout, hw, dil):
@@ -221,47 +181,4 @@ def test_conv_h3r_equals_8wave(n, c0, c1, cout, hw, dil):
         H.set_h3r(prev)
     names = ("y", "stats", "xsplit", "dx", "dysplit", "bn_part", "dx_max")
     for name, a, b_ in zip(names, *outs):
-        assert torch.equal(a, b_), name
-
-
-@pytest.mark.parametrize("n,cout_dy,cin_dx,hw", [(4, 64, 64, 40), (3, 32, 64, 40), (2, 64, 192, 40), (6, 128, 64, 20)])
-def test_conv_dgrad_bnb_h3r_equals_8wave(n, cout_dy, cin_dx, hw):
-    """The fused BN-backward dgrad (srpde_conv_dgrad_h3_bnb) on the register-staged kernel (y halo
-    DMA'd into S and transformed in place) against the 8-wave kernel: dx, dy's stored split, the
-    next BN's partials and per-tile max|dx| in equal bits (same expressions, same order)."""
-    from superresolution_for_pdes_amd import hipops as H
-    if H.conv_math() != "h3" or not H.bnb_capable(cout_dy, cin_dx, hw, 1):
-        pytest.skip("not a BNB shape")
-    g = torch.Generator(device=DEV).manual_seed(9)
-    P = n * hw * hw
-    da = torch.randn(P, cout_dy, device=DEV, generator=g)
-    y = torch.randn(P, cout_dy, device=DEV, generator=g) * 2 + 0.3
-    mean, invstd = y.mean(0), y.var(0, unbiased=False).add(1e-5).rsqrt()
-    gamma = torch.randn(cout_dy, device=DEV, generator=g)
-    beta = torch.randn(cout_dy, device=DEV, generator=g) * 0.1
-    dg, db, dbias = (torch.empty(cout_dy, device=DEV) for _ in range(3))
-    m1, m2, word = H.bn_bwd_prepare(y, da, mean, invstd, gamma, beta, dg, db, dbias)
-    w = torch.randn(cout_dy, cin_dx, 3, 3, device=DEV, generator=g) * 0.05
-    wd = H.pack_conv_weights(w, cin_dx, False, True)[1]
-    by = torch.randn(P, cin_dx, device=DEV, generator=g)
-    bmean, binv = torch.randn(cin_dx, device=DEV, generator=g) * 0.1, torch.rand(cin_dx, device=DEV, generator=g) + 0.5
-    bga, bbe = torch.randn(cin_dx, device=DEV, generator=g), torch.randn(cin_dx, device=DEV, generator=g) * 0.1
-    if os.environ.get("SRPDE_H3R_BNB") != "1":
-        pytest.skip("the register-staged BNB dgrad is off (SRPDE_H3R_BNB=1 turns it on)")
-    outs = []
-    prev = H.set_h3r(True)
-    try:
-        for on in (False, True):
-            H.set_h3r(on)
-            dx = torch.empty(P, cin_dx, device=DEV)
-            dyp = H.split_planes_buffer(P, cout_dy, DEV)
-            part = H.bn_bwd_partials(n, hw, hw, cin_dx, DEV)
-            dmax = H.dx_max_slots(n, hw, hw, cin_dx, DEV)
-            H.conv_dgrad_bnb(da, y, mean, invstd, gamma, beta, m1, m2, word, wd, dx, n, hw, hw, cout_dy, cin_dx, 1,
-                             dyp, bn_bwd=(by, bmean, binv, bga, bbe, part), dx_max=dmax)
-            torch.cuda.synchronize()
-            outs.append((dx, dyp, part, dmax))
-    finally:
-        H.set_h3r(prev)
-    for name, a, b_ in zip(("dx", "dysplit", "bn_part", "dx_max"), *outs):
         assert torch.equal(a, b_), name

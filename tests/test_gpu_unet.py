@@ -323,3 +323,44 @@ def test_fused_bn_apply_matches_separate_pass():
             continue
         e = float((g - r).norm() / max(float(r.norm()), 1e-30))
         assert e < 1e-4, (n, e)
+
+
+SWITCHES = ("_FUSE_D1", "_FIN_AFFINE", "_FUSE_SA", "_FUSE_ATT_CH", "_FUSE_POOL", "_H3W_SIDE", "_FUSE_BN_BWD",
+            "_FUSE_BN_APPLY", "_WGRAD_STREAM")
+
+
+@pytest.mark.parametrize("off", [SWITCHES] + [(s,) for s in SWITCHES])
+def test_executor_switches_off_match_defaults(off):
+    """Every executor switch left in unet_exec (each fused pass against its separate passes, the
+    side-stream placements against in-line) gives the default train step's output, BN running
+    statistics and gradients to fp32 accuracy -- all off at once and each alone, so every
+    dispatchable path of the executor runs on the GPU."""
+    from superresolution_for_pdes_amd import unet_exec
+    x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(4)).to(DEV)
+    x[:, 1] = 1.0
+    saved = {k: getattr(unet_exec, k) for k in SWITCHES}
+    res = []
+    try:
+        for turn_off in ((), off):
+            for k in SWITCHES:
+                setattr(unet_exec, k, saved[k] and k not in turn_off)
+            m = make_model(True)
+            out = m(x)
+            (out ** 2).mean().backward()
+            torch.cuda.synchronize()
+            g = {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}
+            rs = {n: b.detach().double().cpu() for n, b in m.named_buffers() if "running" in n}
+            res.append((out.detach().double().cpu(), g, rs))
+    finally:
+        for k, v in saved.items():
+            setattr(unet_exec, k, v)
+    (o0, g0, r0), (o1, g1, r1) = res
+    assert float((o0 - o1).norm() / o0.norm()) <= 1e-5
+    for n in r0:
+        assert float((r0[n] - r1[n]).norm() / max(float(r0[n].norm()), 1e-30)) <= 1e-5, n
+    for n in g0:
+        if _bn_fed_conv_bias(n):
+            assert float(g1[n].norm()) <= 1e-4, n   # true gradient 0
+            continue
+        e = float((g0[n] - g1[n]).norm() / max(float(g0[n].norm()), 1e-30))
+        assert e < 1e-4, (n, e)

@@ -119,3 +119,25 @@ def test_bench_refuses_world_size_mismatch():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "WORLD_SIZE=4" in p.stderr
+
+
+def test_init_weights_matches_reference_seeded():
+    """M10: torch.manual_seed(42); UNet().apply(init_weights) -- as train_enhanced.main does
+    (:187-189, :303-304) -- builds the reference's initial tensors bit for bit (init_fixture: the
+    reference's own run, models.py:209-222; same module registration order, same RNG draws)."""
+    from superresolution_for_pdes_amd.models import UNet, init_weights
+    z = np.load(os.path.join(ROOT, "tests", "golden", "init_fixture.npz"))
+    torch.manual_seed(42)
+    m = UNet()
+    m.apply(init_weights)
+    sd = m.state_dict()
+    keys = {k.split(":", 1)[1] for k in z.files}
+    assert keys == set(sd)
+    for k, v in sd.items():
+        if not v.is_floating_point():
+            assert np.array_equal(v.numpy(), z[f"int:{k}"]), k
+            continue
+        f = v.detach().reshape(-1).double()
+        assert float(f.norm()) == float(z[f"norm:{k}"]), k
+        assert float(f.sum()) == float(z[f"sum:{k}"]), k
+        assert np.array_equal(f[:: max(1, f.numel() // 64)][:64].numpy(), z[f"sample:{k}"]), k

@@ -40,14 +40,14 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--math", default=None, choices=("h3", "x6", "f32", "x6p"), help="default: the package default (h3)")
+    ap.add_argument("--math", default=None, choices=("h3", "f32"), help="default: the package default (h3)")
     ap.add_argument("--json-out", default=None, help="per (layer, pass): ms, TF, algorithmic bytes")
     ap.add_argument("--sequence-out", default=None,
                     help="launch order of every conv call [(layer, pass)] (maps rocprofv3 dispatches to layers)")
     args = ap.parse_args()
     seq, rows = [], []
     if args.math:
-        H.set_conv_math("x6" if args.math == "x6p" else args.math)
+        H.set_conv_math(args.math)
     dev = "cuda"
     n = args.batch
     tot = {}
@@ -81,15 +81,7 @@ def main():
             seq.extend([(name, "setup"), (name, "setup")])
         for kind in args.only.split(","):
             tag = (name, kind)
-            if kind == "fwd" and args.math == "x6p":   # inputs pre-split outside the timed call
-                p0, p1 = H.split_planes(x0), (H.split_planes(x1) if x1 is not None else None)
-                ms = timeit(lambda: H.conv_fwd_x6p(p0, p1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats),
-                            args.iters, seq, tag)
-            elif kind == "dgrad" and args.math == "x6p":
-                pdy = H.split_planes(dy)
-                ms = timeit(lambda: H.conv_fwd_x6p(pdy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None),
-                            args.iters, seq, tag)
-            elif kind == "fwd":
+            if kind == "fwd":
                 ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp),
                             args.iters, seq, tag)
             elif kind == "dgrad":
