@@ -102,9 +102,15 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
                       void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                      const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
-                      hipStream_t stream);
-/* out_max (nullable): every output tile writes max|y| of its elements to out_max[tile]
+                      const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
+                      const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
+                      void* workspace, size_t ws_bytes, hipStream_t stream);
+/* ep_mean / ep_invstd / ep_gamma / ep_beta (nullable, eval mode; no stats / bn_part / accumulate):
+ * the epilogue applies the following BatchNorm with its running statistics and the ReLU,
+ * y = relu((conv + bias - mean) * invstd * gamma + beta) (srpde_bn_eval_prepare's mean / invstd),
+ * so the conv output is the activation itself (models.py:22-23 in eval mode); ep_amax (nullable,
+ * zeroed beforehand) receives max|y|, the next h3 consumer's operand-scale word.
+ * out_max (nullable): every output tile writes max|y| of its elements to out_max[tile]
  * (ceil(P/rows) x ceil(cout/cols) slots, the h3 tile of the call) -- the scale bound that
  * srpde_bn_bwd_prepare needs when y is the gradient of a BN output.
  * in_scale / in_shift (nullable, c1 == 0 only): the input is relu(x0 * in_scale[c] + in_shift[c])
@@ -158,13 +164,15 @@ int srpde_bn_relu_pool_fwd(const float* y, int ldy, const float* mean, const flo
 /* srpde_bn_relu_pool_fwd (ReLU always) with one block per sample, which also forms the channel branch
  * of the AttentionGate reading the activation (models.py:106-112, 119-121; as srpde_att_channel_fwd:
  * m [n][C], hbuf [n][C/8], ca [n][C]).  C a multiple of 32, <= 256.  pool == NULL: no pooling (the
- * activation and the channel branch only). */
+ * activation and the channel branch only).  out == NULL: the activation is not written (y already is
+ * it: pass mean 0, invstd 1, gamma 1, beta 0, an exact identity on y >= 0). */
 int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                                const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
                                int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
                                const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream);
 /* srpde_bn_relu_fwd (ReLU) that also forms the spatial attention of the gate whose gating input the
- * result is (models.py:124-125): sa[p] = sigmoid(sum_c wg[c] out[p][c] + bg[0]).  C 256, 512 or 1024. */
+ * result is (models.py:124-125): sa[p] = sigmoid(sum_c wg[c] out[p][c] + bg[0]).  C 256, 512 or 1024.
+ * out == NULL: the activation is not written (as srpde_bn_relu_pool_att_fwd). */
 int srpde_bn_relu_gate_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                            const float* beta, float* out, int ldo, long long P, int C, const float* wg,
                            const float* bg, float* sa, unsigned* amax, hipStream_t stream);

@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256) void bn_relu_pool_att_fwd_kernel(
       r.y = fmaxf((v.y - mu.y) * is.y * g.y + b.y, 0.f);
       r.z = fmaxf((v.z - mu.z) * is.z * g.z + b.z, 0.f);
       r.w = fmaxf((v.w - mu.w) * is.w * g.w + b.w, 0.f);
-      *reinterpret_cast<float4*>(out + pp[k] * ldo + c) = r;
+      if (out) *reinterpret_cast<float4*>(out + pp[k] * ldo + c) = r;
       mx = fmaxf(mx, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
       sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
       o[k] = r;
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(256) void bn_relu_gate_fwd_kernel(const float* __re
       r.y = fmaxf((v.y - mu.y) * is.y * g.y + b.y, 0.f);
       r.z = fmaxf((v.z - mu.z) * is.z * g.z + b.z, 0.f);
       r.w = fmaxf((v.w - mu.w) * is.w * g.w + b.w, 0.f);
-      *reinterpret_cast<float4*>(out + p * ldo + c) = r;
+      if (out) *reinterpret_cast<float4*>(out + p * ldo + c) = r;
       mx = fmaxf(mx, fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)));
       dot = r.x * wv.x + r.y * wv.y + r.z * wv.z + r.w * wv.w;
     }
@@ -667,8 +667,8 @@ int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const
                                const float* beta, float* out, int ldo, float* pool, int ldp, int n, int h, int w,
                                int C, unsigned* amax, const float* w1, const float* b1, const float* w2,
                                const float* b2, float* m, float* hbuf, float* ca, hipStream_t stream) {
-  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && w1 && b1 && w2 && b2 && m && hbuf && ca,
-                  "srpde_bn_relu_pool_att_fwd: null");
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && w1 && b1 && w2 && b2 && m && hbuf && ca,
+                  "srpde_bn_relu_pool_att_fwd: null");   // out nullable: the activation is not written
   SRPDE_CHECK_ARG(C % 32 == 0 && C <= 256 && 256 % (C / 4) == 0 && ldy % 4 == 0 && ldo % 4 == 0 &&
                       (pool == nullptr || (ldp % 4 == 0 && h % 2 == 0 && w % 2 == 0)),
                   "srpde_bn_relu_pool_att_fwd: C a multiple of 32 <= 256, ld multiples of 4, h and w even");
@@ -685,7 +685,7 @@ int srpde_bn_relu_pool_att_fwd(const float* y, int ldy, const float* mean, const
 int srpde_bn_relu_gate_fwd(const float* y, int ldy, const float* mean, const float* invstd, const float* gamma,
                            const float* beta, float* out, int ldo, long long P, int C, const float* wg,
                            const float* bg, float* sa, unsigned* amax, hipStream_t stream) {
-  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && out && wg && bg && sa, "srpde_bn_relu_gate_fwd: null");
+  SRPDE_CHECK_ARG(y && mean && invstd && gamma && beta && wg && bg && sa, "srpde_bn_relu_gate_fwd: null");   // out nullable
   SRPDE_CHECK_ARG((C == 256 || C == 512 || C == 1024) && ldy % 4 == 0 && ldo % 4 == 0,
                   "srpde_bn_relu_gate_fwd: C 256, 512 or 1024, ld multiples of 4");
   const long long ppb = 256 / (C / 4);

@@ -38,7 +38,20 @@ struct ConvParams {
   // the consumer reduces the [ntiles] slots) -- the operand-scale bound of the BN backward that
   // reads this output next (srpde_bn_bwd_prepare)
   float* out_max = nullptr;
+  // optional eval-mode BatchNorm + ReLU applied by the epilogue (models.py:22-23 with running
+  // statistics): out = relu((conv + bias - mean) * invstd * gamma + beta), the expression of
+  // bn_relu_fwd_kernel; ep_amax (nullable) receives max|out| (one atomicMax per workgroup)
+  const float* ep_mean = nullptr;
+  const float* ep_invstd = nullptr;
+  const float* ep_gamma = nullptr;
+  const float* ep_beta = nullptr;
+  unsigned* ep_amax = nullptr;
 };
+
+// relu((v - mean) * invstd * gamma + beta): bn_relu_fwd_kernel's expression (bn.hip)
+__device__ __forceinline__ float ep_bn_relu(float v, float mu, float is, float g, float b) {
+  return fmaxf((v - mu) * is * g + b, 0.f);
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int total) {
   // bijective: blocks that share an A row-panel land on one XCD (MI355X L2 per XCD)
@@ -126,6 +139,13 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
       a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
     }
     a.x += bias.x; a.y += bias.y; a.z += bias.z; a.w += bias.w;
+    if (p.ep_mean != nullptr && cok) {   // eval-mode BN + ReLU (see ConvParams)
+      const int c = col;
+      a.x = ep_bn_relu(a.x, p.ep_mean[c], p.ep_invstd[c], p.ep_gamma[c], p.ep_beta[c]);
+      a.y = ep_bn_relu(a.y, p.ep_mean[c + 1], p.ep_invstd[c + 1], p.ep_gamma[c + 1], p.ep_beta[c + 1]);
+      a.z = ep_bn_relu(a.z, p.ep_mean[c + 2], p.ep_invstd[c + 2], p.ep_gamma[c + 2], p.ep_beta[c + 2]);
+      a.w = ep_bn_relu(a.w, p.ep_mean[c + 3], p.ep_invstd[c + 3], p.ep_gamma[c + 3], p.ep_beta[c + 3]);
+    }
     v[i] = a;
     const int row = m0 + r;
     if (row < p.P && cok) {
@@ -139,6 +159,22 @@ __global__ __launch_bounds__(1024) void conv_tail_fixup_kernel(ConvParams p) {
     }
   }
   constexpr int IPS = RPT / NSB;      // a thread's rows per statistics sub-block
+  if (p.ep_amax != nullptr) {         // max|out| of the block's rows -> one atomicMax
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+      if (m0 + g + i * G < p.P && cok)
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+    red[g][cq] = make_float4(mx, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int k = 0; k < G; ++k)
+        for (int c = 0; c < CQ; ++c) t = fmaxf(t, red[k][c].x);
+      atomicMax(p.ep_amax, __float_as_uint(t));
+    }
+    __syncthreads();
+  }
   if (BMB == BM && p.out_max != nullptr) {   // max|out| of this tile -> its slot (whole-tile blocks only)
     float mx = 0.f;
 #pragma unroll
@@ -360,6 +396,31 @@ __device__ __forceinline__ void x6_finish_body(const ConvParams& p, floatx16 (&a
     }
     __syncthreads();
   }
+  if (p.ep_amax != nullptr) {         // max|out| of this tile -> one atomicMax per workgroup
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const bool cok = n0 + wn0 + j * 32 + lr < p.Cout;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (row_ok(row) && cok) mx = fmaxf(mx, fabsf(acc[i][j][r]));
+        }
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    __syncthreads();                  // smem may still hold the store stage's last reads
+    if (lane == 0) smem[wni * WM + wmi] = mx;
+    __syncthreads();
+    if (wmi == 0 && wni == 0 && lane == 0) {
+      float t = 0.f;
+      for (int k = 0; k < WM * WN; ++k) t = fmaxf(t, smem[k]);
+      atomicMax(p.ep_amax, __float_as_uint(t));
+    }
+    __syncthreads();
+  }
   if (p.bn_part != nullptr) {         // fused BN-backward reduction of the layer below (see ConvParams)
     float* red = smem;                // [2][WM * TI][BN]: one partial per 32-row block
     const int sb = wmi / WPS;
@@ -503,6 +564,19 @@ __device__ __forceinline__ void x6_finish(const ConvParams& p, floatx16 (&acc)[B
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_fmaf(acc[i][j][r], cs, bcol[j]);
     }
+  if (p.ep_mean != nullptr) {         // eval-mode BN + ReLU (see ConvParams)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn0 + j * 32 + lr;
+      const bool cok = col < p.Cout;
+      const float mu = cok ? p.ep_mean[col] : 0.f, is = cok ? p.ep_invstd[col] : 0.f;
+      const float ga = cok ? p.ep_gamma[col] : 0.f, be = cok ? p.ep_beta[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = ep_bn_relu(acc[i][j][r], mu, is, ga, be);
+    }
+  }
   if (m0 + BM <= p.P)
     x6_finish_body<BM, BN, WM, WN, SRB, true>(p, acc, m0, n0, wmi, wni, lane, smem, stage, bcol);
   else

@@ -1930,8 +1930,9 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate, float* stats,
                       void* xsplit_out, const float* in_scale, const float* in_shift, const float* bn_y,
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                      const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
-                      hipStream_t stream) {
+                      const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
+                      const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
+                      void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
@@ -1974,6 +1975,12 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
   p.out_max = out_max;
   SRPDE_CHECK_ARG(xsplit_out == nullptr || aligned16(xsplit_out), "srpde_conv_fwd_h3: xsplit_out must be 16-byte aligned");
+  SRPDE_CHECK_ARG(ep_mean == nullptr || (ep_invstd && ep_gamma && ep_beta && !accumulate && stats == nullptr &&
+                                         bn_part == nullptr && cout % 4 == 0),
+                  "srpde_conv_fwd_h3: the epilogue BN + ReLU needs mean/invstd/gamma/beta, no accumulate / stats / "
+                  "bn_part, cout %% 4 == 0");
+  p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
+  p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);

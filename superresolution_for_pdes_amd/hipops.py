@@ -102,12 +102,14 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
 
 
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
-             planes_out=None, in_affine=None, bn_bwd=None, out_max=None):
+             planes_out=None, in_affine=None, bn_bwd=None, out_max=None, ep_bn=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
     ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad;
     ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly;
     ``bn_bwd = (bn_y, mean, invstd, gamma, beta, part)`` (dgrad into a BN + ReLU output's
-    gradient) also writes that BN backward's reduction into ``part`` (bn_bwd_partials)."""
+    gradient) also writes that BN backward's reduction into ``part`` (bn_bwd_partials);
+    ``ep_bn = (mean, invstd, gamma, beta, amax)`` (eval mode) applies the following BatchNorm and
+    ReLU in the epilogue, so ``y`` is the activation, and writes max|y| into ``amax``."""
     p0, ld0 = _pl(x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
@@ -127,17 +129,40 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
-             *_bn_bwd_args(bn_bwd), _p(out_max), ws.data_ptr(), ws.numel(), stream_ptr())
+             *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), ws.data_ptr(), ws.numel(), stream_ptr())
+        if ep_bn is not None:
+            tag_amax(y, ep_bn[4])
         if planes_out is not None:
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert planes_out is None and in_affine is None and bn_bwd is None and out_max is None, \
-        "planes_out / in_affine / bn_bwd / out_max need the h3 kernels"
+    assert planes_out is None and in_affine is None and bn_bwd is None and out_max is None and ep_bn is None, \
+        "planes_out / in_affine / bn_bwd / out_max / ep_bn need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+def _ep_args(ep_bn):
+    if ep_bn is None:
+        return (0, 0, 0, 0, 0)
+    mean, invstd, gamma, beta, amax = ep_bn
+    return (mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _p(amax))
+
+
+_IDENT = {}
+
+
+def identity_bn(c, device):
+    """(mean 0, invstd 1, gamma 1, beta 0) for c channels: the fused BN kernels' pass-through of an
+    already activated input (relu((y - 0) * 1 * 1 + 0) == y for y >= 0, exactly)."""
+    key = (str(device), c)
+    t = _IDENT.get(key)
+    if t is None:
+        z, o = torch.zeros(c, dtype=F32, device=device), torch.ones(c, dtype=F32, device=device)
+        t = _IDENT[key] = (z, o, o, z)
+    return t
 
 
 def _bn_bwd_args(bn_bwd):
@@ -226,6 +251,7 @@ class AmaxSlots:
     def __init__(self, n, device):
         self.buf = torch.zeros(n, dtype=torch.int32, device=device)
         self.next = 0
+        self.eval_epilogue = False   # unet_forward: inference forward, BN + ReLU in the conv epilogues
 
     def take(self):
         if self.next >= self.buf.numel():
@@ -373,13 +399,14 @@ def bn_relu_pool_att_fwd(y, mean, invstd, gamma, beta, out, pool, n, h, w, att_p
     dev = y.device
     m, hb, ca = empty(n, C, device=dev), empty(n, C // 8, device=dev), empty(n, C, device=dev)
     py, ldy = _pl(y)
-    po, ldo = _pl(out)
+    po, ldo = _pl(out) if out is not None else (0, 0)
     pp, ldp = _pl(pool) if pool is not None else (0, 0)
     w1, b1, w2, b2 = att_params
     call("srpde_bn_relu_pool_att_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
          beta.data_ptr(), po, ldo, pp, ldp, n, h, w, C, _p(amax), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
          b2.data_ptr(), m.data_ptr(), hb.data_ptr(), ca.data_ptr(), stream_ptr())
-    tag_amax(out, amax)
+    if out is not None:
+        tag_amax(out, amax)
     if pool is not None:
         tag_amax(pool, amax)
     return m, hb, ca
@@ -390,10 +417,11 @@ def bn_relu_gate_fwd(y, mean, invstd, gamma, beta, out, wg, bg, amax=None):
     P, C = y.shape
     sa = empty(P, device=y.device)
     py, ldy = _pl(y)
-    po, ldo = _pl(out)
+    po, ldo = _pl(out) if out is not None else (0, 0)
     call("srpde_bn_relu_gate_fwd", py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
          po, ldo, P, C, wg.data_ptr(), bg.data_ptr(), sa.data_ptr(), _p(amax), stream_ptr())
-    tag_amax(out, amax)
+    if out is not None:
+        tag_amax(out, amax)
     return sa
 
 

@@ -225,8 +225,15 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
                                            bn.num_batches_tracked, mom, bn.eps)
     else:
         assert in_affine is None and activate
-        H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
         mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
+        if getattr(slots, "eval_epilogue", False) and _EVAL_EPI and H.h3_capable(x0.shape[1], c1, cout, w, dil):
+            # inference: the conv epilogue applies this BN (running statistics) + ReLU, so y IS the
+            # activation (nothing saved for a backward); consumers read it as is
+            slot = slots.take()
+            H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None,
+                       ep_bn=(mean, invstd, bn.weight, bn.bias, slot))
+            return _eval_consumers(y, slot, n, h, w, cout, pool, att, gate), None
+        H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
     # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
     # the weight gradient reads the stored split
     saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
@@ -262,6 +269,41 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     return (a, pooled, _att_channel_early(att, a, n, h * w)), saved
 
 
+def _eval_consumers(a, slot, n, h, w, c, pool, att, gate):
+    """_cbr_fwd's return value for an activation ``a`` the conv epilogue already formed (eval mode):
+    the pooled tensor, the gate's channel branch or its spatial attention from the fused passes with
+    an identity BN and no activation write."""
+    dev = a.device
+    ident = H.identity_bn(c, dev)
+    if gate is not None:
+        s0 = gate.spatial_attention[0]
+        if _FUSE_SA and c in (256, 512, 1024):
+            return a, H.bn_relu_gate_fwd(a, *ident, None, s0.weight, s0.bias)
+        return a, None
+    if pool:
+        pooled = H.empty(n * (h // 2) * (w // 2), c, device=dev)
+        if att is not None and _per_sample_ok(n, h, w, c) and _FUSE_POOL:
+            c1, c3, _ = _att_params(att)
+            chan = H.bn_relu_pool_att_fwd(a, *ident, None, pooled, n, h, w,
+                                          (c1.weight, c1.bias, c3.weight, c3.bias))
+            H.tag_amax(pooled, slot)
+            return a, pooled, (chan, None)
+        pooled = H.maxpool_fwd(a, n, h, w)
+        if att is None:
+            return a, pooled
+        return a, pooled, _att_channel_early(att, a, n, h * w)
+    if att is not None:
+        if _per_sample_ok(n, h, w, c) and a.is_cuda and not torch.cuda.is_current_stream_capturing():
+            c1, c3, _ = _att_params(att)
+            chan = H.bn_relu_pool_att_fwd(a, *ident, None, None, n, h, w, (c1.weight, c1.bias, c3.weight, c3.bias))
+            return a, (chan, None)
+        return a, _att_channel_early(att, a, n, h * w)
+    return a
+
+
+# inference (eval, nothing saved for a backward): BN + ReLU in the conv epilogue (SRPDE_EVAL_EPI=0: the
+# separate passes)
+_EVAL_EPI = os.environ.get("SRPDE_EVAL_EPI", "1") != "0"
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
 _FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
 # the gates' spatial attention formed by the upsample that produces their gating input
@@ -534,6 +576,7 @@ def unet_forward(m, x, training, save=False):
     prepare_h3_weights(m)
     # max|x| words of the 16 BN+ReLU outputs (h3 operand scales)
     slots = H.AmaxSlots(16, x.device)
+    slots.eval_epilogue = not training and not save   # inference: BN + ReLU in the conv epilogues
     # encoder
     (e1, p1, ch1), S.enc1 = _block_fwd(m.enc1, x4, None, n, h, w, training, slots, pool=True, att=m.att1)
     (e2, p2, ch2), S.enc2 = _block_fwd(m.enc2, p1, None, n, h2, w2, training, slots, pool=True, att=m.att2)

@@ -94,6 +94,43 @@ __global__ __launch_bounds__(512, 1) void mfma_random(float* out, int iters) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+
+// the same work as mfma_random on v_mfma_f32_16x16x32_f16 (MI355X_MICROARCH.md: the 16x16 shape holds
+// a higher clock under load on random data): per 32x32 tile-equivalent two independent 16x16
+// accumulators, each a chain of three products, per iteration (equal FLOP per iteration)
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+template <int TILES>
+__global__ __launch_bounds__(512, 1) void mfma_random16(float* out, int iters) {
+  extern __shared__ float lds_unused[];
+  if (iters < 0) lds_unused[threadIdx.x] = 0.f;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 ra, rb;
+  unsigned seed = threadIdx.x * 2654435761u + blockIdx.x * 40503u;
+  for (int k = 0; k < 4; ++k) {
+    seed = seed * 1664525u + 1013904223u; ra[k] = (seed & 0x03ff03ffu) | 0x38003800u;
+    seed = seed * 1664525u + 1013904223u; rb[k] = (seed & 0x03ff03ffu) | 0x38003800u;
+  }
+  floatx4 acc[2 * TILES];
+  for (int c = 0; c < 2 * TILES; ++c)
+    for (int r = 0; r < 4; ++r) acc[c][r] = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    const u32x4 ma = (u32x4){(unsigned)it * 0x00010001u, (unsigned)it * 0x00030003u, (unsigned)it * 0x00050005u,
+                             (unsigned)it * 0x00070007u} & 0x03ff03ffu;
+    const half8 a = __builtin_bit_cast(half8, ra ^ ma), b = __builtin_bit_cast(half8, rb ^ (ma << 1));
+    const half8 a2 = __builtin_bit_cast(half8, ra ^ (ma >> 1)), b2 = __builtin_bit_cast(half8, rb ^ (ma << 2));
+#pragma unroll
+    for (int c = 0; c < 2 * TILES; ++c) {
+      floatx4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, b, acc[c], 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b2, c0, 0, 0, 0);
+      acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+    }
+  }
+  float s = 0.f;
+  for (int c = 0; c < 2 * TILES; ++c)
+    for (int r = 0; r < 4; ++r) s += acc[c][r];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <typename K>
 static void timeit(const char* name, K kern, int blocks, float* out, int iters, double mfma_per_iter,
                    size_t lds = 0) {
@@ -146,6 +183,10 @@ int main() {
   timeit("4 chains, 1 WG/CU (2 waves/SIMD)", mfma_loop<4>, blocks, out, 5000, 4, 100 * 1024);
   timeit("random operands, 3-chains x4, 1 WG/CU", mfma_random<4>, blocks, out, 2000, 12, 100 * 1024);
   timeit("random operands, 3-chains x4, 1 WG/CU", mfma_random<4>, blocks, out, 8000, 12, 100 * 1024);
+  // flops counted in 32x32x16 units (the 16x16x32 kernel does equal work per iteration)
+  timeit("16x16x32 random, 3-chains x8, 1 WG/CU", mfma_random16<4>, blocks, out, 2000, 12, 100 * 1024);
+  timeit("16x16x32 random, 3-chains x8, 1 WG/CU", mfma_random16<4>, blocks, out, 8000, 12, 100 * 1024);
+  timeit("random operands, 3-chains x4, 1 WG/CU (again)", mfma_random<4>, blocks, out, 8000, 12, 100 * 1024);
   hipFree(out);
   return 0;
 }
