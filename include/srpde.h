@@ -95,6 +95,17 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
                             void* dysplit_out, const float* bn_y, int bn_ldy, const float* bn_mean,
                             const float* bn_invstd, const float* bn_gamma, const float* bn_beta, void* bn_part,
                             float* dx_max, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* srpde_conv_fwd_h3 (no virtual concat, no input transform) on an input that arrives as its h3
+ * split: xsplit = [2][P][c] fp16 hi / lo planes of x * 2^h3_exp(*amax) (srpde_bn_bwd_apply_split,
+ * or a stored xsplit_out).  The halo tiles go into the MFMA operand layout as fp16 pieces (no fp32
+ * tile, no split work, nothing stored for the weight gradient, which reads the same planes); same
+ * outputs, statistics, bn_part and out_max as srpde_conv_fwd_h3 on that split. */
+int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, const void* wsplit, const int* wexp,
+                               const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize,
+                               int dil, int sign, int accumulate, float* stats, const float* bn_y, int bn_ldy,
+                               const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                               const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
+                               hipStream_t stream);
 /* Output tiles (= out_max slots) of srpde_conv_fwd_h3 for P rows, cin -> cout; 0 if unsupported. */
 long long srpde_conv_h3_tiles(long long P, int cin, int cout, int w, int dil);
 int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const unsigned* amax0,
@@ -206,6 +217,14 @@ int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, con
                          int nblk_part, const float* da_max, int n_da_max, float* m1, float* m2, float* dgamma,
                          float* dbeta, float* dbias, unsigned* dy_amax, void* workspace, size_t ws_bytes,
                          hipStream_t stream);
+/* The BN (+ReLU) backward apply with srpde_bn_bwd_prepare's m1 / m2 (the expressions of
+ * srpde_bn_relu_bwd) written as the h3 operand split of dy: planes = [2][P][C] fp16 hi / lo of
+ * dy * 2^h3_exp(*dy_amax) (dy_amax = prepare's bound), the input of srpde_conv_fwd_h3_presplit and
+ * srpde_conv_wgrad_h3p.  No fp32 dy is written. */
+int srpde_bn_bwd_apply_split(const float* y, int ldy, const float* da, int ldda, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, const float* m1,
+                             const float* m2, long long P, int C, int flags, const unsigned* dy_amax, void* planes,
+                             hipStream_t stream);
 int srpde_bn_relu_bwd(const float* y, int ldy, const float* da, int ldda, const float* mean, const float* invstd,
                       const float* gamma, const float* beta, float* dy, int lddy, float* dgamma, float* dbeta,
                       float* dbias, long long P, int C, int relu, unsigned* amax, void* workspace,

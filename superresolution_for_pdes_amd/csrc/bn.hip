@@ -353,6 +353,62 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
   }
 }
 
+// The BN (+ReLU) backward apply of bn_bwd_apply_kernel (the same expressions, with the float m1 / m2
+// of bn_bwd_coef_kernel) written as the h3 operand split of dy for the dgrad and weight gradient that
+// consume it (srpde_conv_fwd_h3_presplit, srpde_conv_wgrad_h3p): dy * s = hi + lo, hi / lo fp16 planes
+// [2][P][C], s = 2^h3_exp(dy_amax) from the rigorous bound of bn_bwd_coef_kernel -- no fp32 dy is
+// written and the dgrad does no split work.  Each thread owns one channel quad of a run of rows.
+__global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __restrict__ y, int ldy,
+                                                                 const float* __restrict__ da, int ldda,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ invstd,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta,
+                                                                 const float* __restrict__ m1v,
+                                                                 const float* __restrict__ m2v, long long P, int C,
+                                                                 int rows_per_blk, int relu,
+                                                                 const unsigned* __restrict__ dy_amax,
+                                                                 _Float16* __restrict__ planes) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  int c4, r0, rs;
+  thread_rc(C, &c4, &r0, &rs);
+  if ((int)threadIdx.x >= (C >> 2) * rs) return;
+  const int c = c4 * 4;
+  const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+  const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+  const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+  const float4 b = *reinterpret_cast<const float4*>(beta + c);
+  const float4 m1 = *reinterpret_cast<const float4*>(m1v + c);
+  const float4 m2 = *reinterpret_cast<const float4*>(m2v + c);
+  const float4 k = make_float4(g.x * is.x, g.y * is.y, g.z * is.z, g.w * is.w);
+  const float s = exp2i(h3_exp(*dy_amax));
+  const size_t plane = (size_t)P * C;
+  const long long pb = (long long)blockIdx.x * rows_per_blk;
+  const long long pe = min(P, pb + rows_per_blk);
+  for (long long p = pb + r0; p < pe; p += rs) {
+    const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
+    const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+    float o[4];
+    float xh, dz;
+#define BN_APPLY_S(I, X)                                       \
+  xh = (v.X - mu.X) * is.X;                                    \
+  dz = (!(relu & 1) || xh * g.X + b.X > 0.f) ? d.X : 0.f;      \
+  o[I] = (dz - m1.X - xh * m2.X) * k.X;
+    BN_APPLY_S(0, x) BN_APPLY_S(1, y) BN_APPLY_S(2, z) BN_APPLY_S(3, w)
+#undef BN_APPLY_S
+    half4 hi, lo;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // conv_h3.hip split2h: hi = fp16(x s), lo = fp16(x s - hi)
+      const float xs = o[q] * s;
+      const _Float16 h = (_Float16)xs;
+      hi[q] = h;
+      lo[q] = (_Float16)(xs - (float)h);
+    }
+    *reinterpret_cast<half4*>(planes + (size_t)p * C + c) = hi;
+    *reinterpret_cast<half4*>(planes + plane + (size_t)p * C + c) = lo;
+  }
+}
+
 // The BN (+ReLU) backward's per-channel apply coefficients for a consumer that computes dy on the
 // fly (srpde_conv_dgrad_h3_bnb): m1 = sum(dz)/P, m2 = sum(dz*xhat)/P as float, exactly as
 // bn_bwd_apply_kernel forms them (0 in eval mode); the conv-bias gradient sum(dy) in fp64
@@ -784,6 +840,22 @@ int srpde_bn_relu_bwd_part(const float* y, int ldy, const float* da, int ldda, c
 // the (sum dz, sum dz*xhat) partials already produced by the dgrad that wrote da (nblk row blocks,
 // with that dgrad's per-tile max|da| in da_max[n_da_max]); null: one reduction pass over y and da
 // here (which also takes max|da|).  flags: SRPDE_BN_RELU | SRPDE_BN_EVAL.
+int srpde_bn_bwd_apply_split(const float* y, int ldy, const float* da, int ldda, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta, const float* m1,
+                             const float* m2, long long P, int C, int flags, const unsigned* dy_amax, void* planes,
+                             hipStream_t stream) {
+  SRPDE_CHECK_ARG(y && da && mean && invstd && gamma && beta && m1 && m2 && dy_amax && planes && P > 0,
+                  "srpde_bn_bwd_apply_split: null argument");
+  SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0 && aligned16(y) && aligned16(da) &&
+                      aligned16(planes), "srpde_bn_bwd_apply_split: C / ld multiples of 4, 16-byte aligned");
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  hipLaunchKernelGGL(bn_bwd_apply_split_kernel, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, mean, invstd,
+                     gamma, beta, m1, m2, P, C, rpb, flags & SRPDE_BN_RELU, dy_amax, static_cast<_Float16*>(planes));
+  SRPDE_LAUNCH_CHECK("srpde_bn_bwd_apply_split");
+  return 0;
+}
+
 size_t srpde_bn_bwd_prepare_workspace_size(long long P, int C) {
   int rpb;
   const int nblk = bwd_blocks(P, C, &rpb);

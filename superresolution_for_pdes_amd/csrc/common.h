@@ -60,4 +60,15 @@ inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// h3 operand scales (conv_h3.hip header): the power-of-two exponent that brings max|x| (float
+// bits) just under 2^15, and 2^e as a float.  Every producer and consumer of a split forms the
+// scale with these two, so a split written by one kernel is read back exactly by another.
+__device__ __forceinline__ int h3_exp(unsigned bits) {
+  const int e = (int)((bits >> 23) & 0xffu);
+  if (e == 0) return bits ? 100 : 0;            // zero / denormal maximum
+  if (e == 0xff) return 0;                      // inf / nan: propagate
+  return min(max(15 - (e - 126), -100), 100);   // max < 2^(e-126)
+}
+__device__ __forceinline__ float exp2i(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
+
 }  // namespace srpde

@@ -34,14 +34,6 @@ namespace srpde {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
-// power-of-two scale exponent that brings max|x| (float bits) just under 2^15
-__device__ __forceinline__ int h3_exp(unsigned bits) {
-  const int e = (int)((bits >> 23) & 0xffu);
-  if (e == 0) return bits ? 100 : 0;            // zero / denormal maximum
-  if (e == 0xff) return 0;                      // inf / nan: propagate
-  return min(max(15 - (e - 126), -100), 100);   // max < 2^(e-126)
-}
-__device__ __forceinline__ float exp2i(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
 
 __device__ __forceinline__ void split2h(const float4 a, const float4 b, float s, half8& hi, half8& lo) {
   const float v[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
@@ -53,8 +45,37 @@ __device__ __forceinline__ void split2h(const float4 a, const float4 b, float s,
   }
 }
 
-// 32-half (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ ((r >> 2) & 3)
-__device__ __forceinline__ int swzh(int r, int c) { return c ^ ((r >> 2) & 3); }
+// 32-half (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ g((r >> 2) & 3), g = (0, 2, 3, 1):
+// conflict-free for the 16x16x32 B-fragment reads (lane: row (lane & 15), chunk lane >> 4) of every
+// ds_read_b128 lane group (MI355X_MICROARCH.md, LDS table)
+__device__ __forceinline__ int swzh(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// The main loops run v_mfma_f32_16x16x32_f16 (one 32-channel chunk of a tap per instruction): at
+// equal cycles per FLOP the 16x16 shape holds a higher clock under load on random data than
+// 32x32x16 (tools/mfma_peak.hip: 2058 vs 1791-1861 TF dense, profiles/r03_mfma_shapes.txt).  The
+// epilogue (x6_finish) keeps the 32x32x16 accumulator layout; a 32x32 block is four 16x16 blocks
+// (a, b) (rows 16a.., cols 16b..), regrouped in registers by two lane swaps per dword:
+// X = (a, 0), Y = (a, 1) at one element q -> permlane16_swap -> permlane32_swap gives the 32x32
+// elements 4 (2a) + q and 4 (2a + 1) + q.
+template <int TI, int TJ>
+__device__ __forceinline__ void acc16_to_32(const floatx4 (&a16)[2 * TI][2 * TJ], floatx16 (&a32)[TI][TJ]) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto r1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a16[2 * i + a][2 * j][q]),
+                                                           __float_as_uint(a16[2 * i + a][2 * j + 1][q]), false, false);
+          const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
+          a32[i][j][8 * a + q] = __uint_as_float(r2[0]);
+          a32[i][j][8 * a + 4 + q] = __uint_as_float(r2[1]);
+        }
+}
 
 struct H3Args {
   const _Float16* wsp;     // [2][Cout][K] hi / lo planes
@@ -82,7 +103,7 @@ struct H3Args {
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
 // TPS: taps per stage (one barrier per stage; the weight stage holds TPS taps).
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false, bool PRE = false>
 __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kernel(ConvParams p, H3Args h) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -96,22 +117,28 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   constexpr int AD = BNB ? 2 : 1;               // DMAs per halo slice (BNB: the gradient and the BN input)
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
   static_assert(TPS >= 1 && TPS <= 3, "taps per stage");
+  static_assert(!(BNB && PRE), "one input transform");
   // LDS: F = fp32 halo tile (DMA target, 128-B rows) | S = its split, 128-B rows of eight 16-B
   //      chunks: hi pieces of channel group c8 in chunk c8, lo pieces in chunk 4 + c8, chunk k at
   //      slot swz(r, k) (conflict-free reads at any tap shift; a row's four fragments of one
   //      lane are XOR 32 / 64 / 96 of each other) | B = two weight stages | 128 zero bytes
   //      (the padding row, 128-B aligned so the XORs stay in it) | 1 KiB DMA sink
+  // PRE (the input arrives as its h3 split, [2][P][Cin] fp16 hi / lo planes scaled by 2^h3_exp(amax0)):
+  //      no F and no convert -- two S-layout buffers of arows + 1 rows (the last one zero), chunk c's
+  //      halo tile DMA'd straight into buffer c & 1 in S order (source-side swizzle) while the other
+  //      buffer is read | B | 1 KiB DMA sink
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int arows = h.arows;
+  const int abuf = (arows + 1) * 128;           // PRE: bytes per A buffer
   char* const fbuf = lds;
   char* const fbuf2 = fbuf + arows * ROW2;      // BNB: fp32 halo tile of the BN input y
-  const int soff = (BNB ? 2 : 1) * arows * ROW2;   // S, as a byte offset from lds
+  const int soff = PRE ? 0 : (BNB ? 2 : 1) * arows * ROW2;   // S, as a byte offset from lds
   char* const sbuf = lds + soff;
-  char* const bbuf0 = sbuf + arows * 128;
-  char* const zrow = bbuf0 + 2 * B_STAGE;
-  const int zoff = soff + arows * 128 + 2 * B_STAGE;
-  char* const sink = zrow + 128;
+  char* const bbuf0 = PRE ? lds + 2 * abuf : sbuf + arows * 128;
+  char* const zrow = PRE ? lds + arows * 128 : bbuf0 + 2 * B_STAGE;
+  const int zoff = PRE ? arows * 128 : soff + arows * 128 + 2 * B_STAGE;   // PRE: relative to the buffer
+  char* const sink = PRE ? bbuf0 + 2 * B_STAGE : zrow + 128;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,6 +159,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int HW = p.H * p.W;
 
   if (tid < 32) reinterpret_cast<float*>(zrow)[tid] = 0.f;
+  if (PRE && tid >= 32 && tid < 64) reinterpret_cast<float*>(zrow + abuf)[tid - 32] = 0.f;   // buffer 1's zero row
 
   const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
@@ -146,16 +174,18 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int ea = h3_exp(ab);
   const float sa = exp2i(ea);
 
-  // per tap: the LDS byte offset of this lane's first A fragment (hi pieces, k-group 0) of its
-  // output row shifted by the tap; the zero row for taps outside the image.  Computed once per
-  // tile, so a tap stage's A reads cost no address arithmetic beyond three XORs.
+  // per tap: the LDS byte offset of this lane's A fragment (hi pieces; lo = XOR 64) of its 16x16x32
+  // row (lane & 15 of each 16-row block, chunk lane >> 4) shifted by the tap; the zero row for taps
+  // outside the image.  Computed once per tile.
   const int lr = lane & 31, lh = lane >> 5;
+  const int l16 = lane & 15, lq = lane >> 4;
   const int wmi = wave % WM, wni = wave / WM;
   const int wm0 = wmi * TM, wn0 = wni * TN;
-  int aoff[9][TI];
+  constexpr int TI16 = 2 * TI, TJ16 = 2 * TJ;
+  int aoff[9][TI16];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const int m = m0 + wm0 + i * 32 + lr;
+  for (int i = 0; i < TI16; ++i) {
+    const int m = m0 + wm0 + i * 16 + l16;
     int yy = -(1 << 20), xx = 0;   // rows past the tensor: every tap reads the zero row
     if (m < p.P) {
       const int rem = m % HW;
@@ -166,8 +196,8 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     for (int t = 0; t < 9; ++t) {
       const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
       const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
-      const int r = wm0 + i * 32 + lr + (ky * p.W + kx) * p.dil;
-      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? soff + r * 128 + swz(r, lh) * 16 : zoff;
+      const int r = wm0 + i * 16 + l16 + (ky * p.W + kx) * p.dil;
+      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? soff + r * 128 + swz(r, lq) * 16 : zoff;
     }
   }
   // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1
@@ -188,9 +218,22 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int na = arows / 8;                   // A DMA instructions per chunk (8 rows x 128 B)
   const int pix0 = m0 - h.halo;
 
+  const size_t xplane = (size_t)p.P * p.Cin;
   // A slice `q` of chunk `ch` (8 halo rows, fp32) into F; q >= na: a zero-fill DMA into the sink,
   // so every wave issues the same number of vector-memory ops per stage (exact vmcnt counts)
   auto issue_a = [&](int ch, int q) {
+    if constexpr (PRE) {   // 8 rows x 128 B of S into buffer ch & 1: lane slot (lane & 7) holds chunk
+                           // slot ^ ((r >> 1) & 7) (swz is an involution): hi (< 4) or lo plane piece
+      const int r = q * 8 + (lane >> 3);
+      const int pix = pix0 + r;
+      const bool real = q < na;
+      const int k = (lane & 7) ^ ((r >> 1) & 7);
+      const unsigned off = (real && pix >= 0 && pix < p.P)
+                               ? (unsigned)(((k >= 4 ? xplane : 0) + (size_t)pix * p.Cin + ch * BK2 + (k & 3) * 8) * 2)
+                               : OOB;
+      dma16(rs0, off, lds_addr_of(real ? lds + (ch & 1) * abuf + q * 1024 : sink));
+      return;
+    }
     const int ch0 = ch * BK2;
     const bool second = ch0 >= p.c0;
     const int32x4 rs = second ? rs1 : rs0;
@@ -227,8 +270,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   };
   // F (fp32, landed) -> S: scale and split every halo element once per chunk
   // (the N-tile-0 workgroup of each row tile also stores its own rows' pieces to h.xsplit)
-  const bool wsplit = h.xsplit != nullptr && nt == 0;
-  const size_t xplane = (size_t)p.P * p.Cin;
+  const bool wsplit = !PRE && h.xsplit != nullptr && nt == 0;
   struct BnbCoef { float mu[8], is[8], ga[8], be[8], m1[8], m2[8]; };
   auto convert = [&](int ch) {
     BnbCoef bq;
@@ -289,18 +331,18 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     }
   };
 
-  floatx16 acc[TI][TJ];
-  floatx16 part[TWO_LEVEL ? TI : 1][TWO_LEVEL ? TJ : 1];
-  auto chain = [&](int i, int j) -> floatx16& {
+  floatx4 acc[TI16][TJ16];
+  floatx4 part[TWO_LEVEL ? TI16 : 1][TWO_LEVEL ? TJ16 : 1];
+  auto chain = [&](int i, int j) -> floatx4& {
     if constexpr (TWO_LEVEL) return part[i][j];
     else return acc[i][j];
   };
 #pragma unroll
-  for (int i = 0; i < TI; ++i)
+  for (int i = 0; i < TI16; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j)
+    for (int j = 0; j < TJ16; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
 
   // prologue: whole halo tile of the first chunk + first weight stage
   if (!(p.dbg & 32))   // diagnostics: 32 = no prologue halo DMA, 64 = no prologue convert
@@ -308,55 +350,49 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   issue_b(c_beg, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (!(p.dbg & 64)) convert(c_beg);
+  if (!PRE && !(p.dbg & 64)) convert(c_beg);
   __syncthreads();
 
   int sidx = 0;      // stage counter (B buffer parity)
-  // one tap: read its fragments up front (both 16-k groups), then the MFMAs (the second group's
-  // reads complete under the first group's MFMAs)
+  int acur = 0;      // PRE: byte offset of the current chunk's A buffer
+  // one tap: the A fragments and the first column block's B fragments, then one column block's
+  // MFMAs per further B read pair (without the schedule the compiler parks each read right before
+  // its MFMA and exposes its latency)
   auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
-    constexpr int NG = BK2 / 16;
-    half8 ah[NG][TI], al[NG][TI], bh[NG][TJ], bl[NG][TJ];
+    half8 ah[TI16], al[TI16], bh[TJ16], bl[TJ16];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {   // k-group g: XOR 32; lo pieces: XOR 64 (see the LDS layout)
-        ah[g][i] = *reinterpret_cast<const half8*>(lds + (aoff[TAP][i] ^ (32 * g)));
-        al[g][i] = *reinterpret_cast<const half8*>(lds + (aoff[TAP][i] ^ (32 * g + 64)));
-      }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn0 + j * 32 + lr;
-        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        bh[g][j] = *reinterpret_cast<const half8*>(b + o);
-        bl[g][j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
-      }
+    for (int i = 0; i < TI16; ++i) {   // lo pieces: XOR 64 (see the LDS layout)
+      const char* abase = PRE ? lds + acur : lds;
+      ah[i] = *reinterpret_cast<const half8*>(abase + aoff[TAP][i]);
+      al[i] = *reinterpret_cast<const half8*>(abase + (aoff[TAP][i] ^ 64));
     }
 #pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          floatx16 c0;
-          if (TWO_LEVEL && TAP == 0 && g == 0)   // a chunk's partial chain starts from zero
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], floatx16{}, 0, 0, 0);
-          else   // small terms first
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[g][i], bh[g][j], chain(i, j), 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bl[g][j], c0, 0, 0, 0);
-          chain(i, j) = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[g][i], bh[g][j], c0, 0, 0, 0);
-        }
-    // schedule: the first group's reads, then one MFMA per second-group read, then the rest
-    // (without this the scheduler parks each read right before its MFMA and exposes its latency)
-    constexpr int RD = 2 * (TI + TJ), MF = 3 * TI * TJ;
-    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
-#pragma unroll
-    for (int k = 0; k < RD; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    for (int j = 0; j < TJ16; ++j) {
+      const int r = wn0 + j * 16 + l16;
+      const int o = r * 64 + swzh(r, lq) * 16;
+      bh[j] = *reinterpret_cast<const half8*>(b + o);
+      bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, NG * MF - RD, 0);
+#pragma unroll
+    for (int j = 0; j < TJ16; ++j)
+#pragma unroll
+      for (int i = 0; i < TI16; ++i) {
+        floatx4 c0;
+        if (TWO_LEVEL && TAP == 0)   // a chunk's partial chain starts from zero
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], floatx4{}, 0, 0, 0);
+        else   // small terms first
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], chain(i, j), 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], c0, 0, 0, 0);
+        chain(i, j) = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], c0, 0, 0, 0);
+      }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * TI16 + 2, 0);
+#pragma unroll
+    for (int j = 1; j < TJ16; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI16, 0);
   };
   auto stage = [&](int ch, auto st_tag) {
     constexpr int ST = decltype(st_tag)::value;
@@ -386,6 +422,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     if (!(p.dbg & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
   };
   for (int ch = c_beg; ch < c_end; ++ch) {
+    if constexpr (PRE) acur = (ch & 1) * abuf;
     stage(ch, std::integral_constant<int, 0>{});
     if constexpr (NS > 1) stage(ch, std::integral_constant<int, 1>{});
     if constexpr (NS > 2) stage(ch, std::integral_constant<int, 2>{});
@@ -398,15 +435,18 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     // two-level accumulation: one partial chain per channel chunk (9 taps x 32 channels)
     if constexpr (TWO_LEVEL) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI16; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+        for (int j = 0; j < TJ16; ++j) acc[i][j] += part[i][j];
     }
-    if (ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
+    if (!PRE && ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
       convert(ch + 1);                      // (diagnostics: 4 = no per-chunk convert)
       __syncthreads();
     }
   }
+  // the 32x32x16 accumulator layout of the epilogue
+  floatx16 acc32[TI][TJ];
+  acc16_to_32<TI, TJ>(acc, acc32);
   // the scales to undo: acc * 2^-(ea + wexp[col]), exact; applied by the epilogue in the same FMA
   // as the bias.  A combined exponent outside the normal range (operands of extreme magnitude)
   // takes the activation scale here first, so no intermediate under- or overflows.
@@ -421,7 +461,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] *= ia;
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] *= ia;
       colscale[j] = exp2i(-we);
     } else {
       colscale[j] = exp2i(-e);
@@ -433,12 +473,12 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] * colscale[j] + acc[i][j][15];
+      for (int j = 0; j < TJ; ++j) t += acc32[i][j][0] * colscale[j] + acc32[i][j][15];
     if (t == 123.f) p.y[tid] = t;
     return;
   }
   // the halo buffer F is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
-  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc32, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
                                  h.wide ? smem + 2 * WM * BN : nullptr, colscale);
 }
 
@@ -463,7 +503,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ f32x4 llvm_raw_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
                                          int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
-template <int BN, int TPS, int NTK, int NB>
+// PRE: the input arrives as its h3 split ([2][P][Cin] fp16 planes, conv_fwd_h3_kernel): the halo
+// tasks load the hi / lo pieces and the convert only stores them
+template <int BN, int TPS, int NTK, int NB, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Args h) {
   constexpr int BM = 256, WM = 4, WN = 1, NW = 4, NT = 256, SRB = 128;
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
@@ -518,14 +560,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   const int ea = h3_exp(ab);
   const float sa = exp2i(ea);
 
-  const int lr = lane & 31, lh = lane >> 5;
+  const int lr = lane & 31;
+  const int l16 = lane & 15, lq = lane >> 4;
   const int wmi = wave, wni = 0;
   const int wm0 = wmi * TM, wn0 = 0;
-  static_assert(TI == 2, "two row blocks per wave: one packed offset word per tap");
-  int aoff[9][TI];
+  constexpr int TI16 = 2 * TI, TJ16 = 2 * TJ;
+  static_assert(TI16 == 4, "four 16-row blocks per wave: two packed offset words per tap");
+  // per tap and 16-row block: the LDS byte offset of this lane's 16x16x32 A fragment (hi pieces;
+  // lo = XOR 64), two blocks' offsets per 32-bit word
+  unsigned apk[9][2];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const int m = m0 + wm0 + i * 32 + lr;
+  for (int i = 0; i < TI16; ++i) {
+    const int m = m0 + wm0 + i * 16 + l16;
     int yy = -(1 << 20), xx = 0;
     if (m < p.P) {
       const int rem = m % HW;
@@ -536,13 +582,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     for (int t = 0; t < 9; ++t) {
       const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
       const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
-      const int r = wm0 + i * 32 + lr + (ky * p.W + kx) * p.dil;
-      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? 128 + r * 128 + swz(r, lh) * 16 : zoff;
+      const int r = wm0 + i * 16 + l16 + (ky * p.W + kx) * p.dil;
+      const unsigned ao = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? 128 + r * 128 + swz(r, lq) * 16 : zoff;
+      if (i % 2 == 0) apk[t][i / 2] = ao;
+      else apk[t][i / 2] |= ao << 16;
     }
   }
-  unsigned apk[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) apk[t] = (unsigned)aoff[t][0] | ((unsigned)aoff[t][1] << 16);
   int b_off[BPW];
 #pragma unroll
   for (int j = 0; j < BPW; ++j) {
@@ -574,6 +619,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     const int sg = t + NT * k;
     const int r = sg >> 2, c8 = sg & 3;
     const int pix = pix0 + r;
+    if constexpr (PRE) {
+      const unsigned off = (sg < ntask && pix >= 0 && pix < p.P) ? (unsigned)((pix * p.Cin + cb + c8 * 8) * 2) : OOB;
+      pf[k][0] = llvm_raw_buffer_load_f4(rs0, (int)off, 0, 0);
+      pf[k][1] = llvm_raw_buffer_load_f4(rs0, off == OOB ? (int)OOB : (int)(off + (unsigned)(p.P * p.Cin * 2)), 0, 0);
+      return;
+    }
     const unsigned off = (sg < ntask && pix >= 0 && pix < p.P) ? (unsigned)((pix * ld + cb + c8 * 8) * 4) : OOB;
     pf[k][0] = llvm_raw_buffer_load_f4(rs, (int)off, 0, 0);
     pf[k][1] = llvm_raw_buffer_load_f4(rs, (int)(off + 16u), 0, 0);
@@ -614,7 +665,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
 #pragma unroll
     for (int k = 0; k < NTK; ++k) {
       const int sg = t + NT * k;
-      if (sg < ntask) {
+      if (PRE && sg < ntask) {
+        const int r = sg >> 2, c8 = sg & 3;
+        *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, c8) * 16) = __builtin_bit_cast(half8, pf[k][0]);
+        *reinterpret_cast<half8*>(sbuf + r * 128 + swz(r, 4 + c8) * 16) = __builtin_bit_cast(half8, pf[k][1]);
+      } else if (sg < ntask) {
         const int r = sg >> 2, c8 = sg & 3;
         float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
         float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
@@ -642,7 +697,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     }
   };
 
-  floatx16 acc[TI][TJ], part[TI][TJ];
+  floatx4 acc[TI16][TJ16], part[TI16][TJ16];
 
   // prologue: the first chunk's halo tile + the first NB - 1 weight stages
 #pragma unroll
@@ -656,48 +711,42 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
   convert(c_beg);
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < TI; ++i)
+  for (int i = 0; i < TI16; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j)
+    for (int j = 0; j < TJ16; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
 
   int cur = 0;   // ring slot of the current stage
   auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
-    constexpr int NG = BK2 / 16;
-    unsigned pk = apk[TAP];
-    asm volatile("" : "+v"(pk));   // the four XOR'd fragment addresses per row block are formed here,
-                                    // not hoisted out of the chunk loop (72 live addresses would spill)
+    unsigned pk[2] = {apk[TAP][0], apk[TAP][1]};
+    asm volatile("" : "+v"(pk[0]), "+v"(pk[1]));   // the fragment addresses are formed here, not hoisted
+                                                    // out of the chunk loop (live addresses would spill)
+    half8 bh[TJ16], bl[TJ16];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+    for (int j = 0; j < TJ16; ++j) {
+      const int r = wn0 + j * 16 + l16;
+      const int o = r * 64 + swzh(r, lq) * 16;
+      bh[j] = *reinterpret_cast<const half8*>(b + o);
+      bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
+    }
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int ao = i == 0 ? (int)(pk & 0xffffu) : (int)(pk >> 16);
-        ah[i] = *reinterpret_cast<const half8*>(lds + (ao ^ (32 * g)));
-        al[i] = *reinterpret_cast<const half8*>(lds + (ao ^ (32 * g + 64)));
+    for (int i = 0; i < TI16; ++i) {
+      const int ao = (i % 2 == 0) ? (int)(pk[i / 2] & 0xffffu) : (int)(pk[i / 2] >> 16);
+      const half8 ah = *reinterpret_cast<const half8*>(lds + ao);
+      const half8 al = *reinterpret_cast<const half8*>(lds + (ao ^ 64));
+#pragma unroll
+      for (int j = 0; j < TJ16; ++j) {
+        floatx4 c0;
+        if (TAP == 0)
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], floatx4{}, 0, 0, 0);
+        else
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], part[i][j], 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], c0, 0, 0, 0);
+        part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], c0, 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int r = wn0 + j * 32 + lr;
-        const int o = r * 64 + swzh(r, 2 * g + lh) * 16;
-        bh[j] = *reinterpret_cast<const half8*>(b + o);
-        bl[j] = *reinterpret_cast<const half8*>(b + BP_BYTES + o);
-      }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          floatx16 c0;
-          if (TAP == 0 && g == 0)
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], floatx16{}, 0, 0, 0);
-          else
-            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], part[i][j], 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], c0, 0, 0, 0);
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], c0, 0, 0, 0);
-        }
-      // one k-group's fragments live at a time (the register budget of two workgroups per CU);
+      // one row block's A fragments live at a time (the register budget of two workgroups per CU);
       // the other workgroup's waves cover the read latency
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -721,9 +770,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       // two-level accumulation: the chunk's partial chain folds into the accumulator here, so it
       // is dead before the prefetch registers come alive
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI16; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] += part[i][j];
+        for (int j = 0; j < TJ16; ++j) acc[i][j] += part[i][j];
       // the next chunk's halo tile, after the chunk's last fragment reads; the split after the
       // chunk needs it (and every weight stage issued so far) landed
       if (more) {
@@ -753,6 +802,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       __syncthreads();
     }
   }
+  floatx16 acc32[TI][TJ];   // the 32x32x16 accumulator layout of the epilogue
+  acc16_to_32<TI, TJ>(acc, acc32);
   float colscale[TJ];
   const float ia = exp2i(-ea);
 #pragma unroll
@@ -764,7 +815,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] *= ia;
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] *= ia;
       colscale[j] = exp2i(-we);
     } else {
       colscale[j] = exp2i(-e);
@@ -776,12 +827,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) t += acc[i][j][0] * colscale[j] + acc[i][j][15];
+      for (int j = 0; j < TJ; ++j) t += acc32[i][j][0] * colscale[j] + acc32[i][j][15];
     if (t == 123.f) p.y[tid] = t;
     return;
   }
   // S is free now: reduction scratch [2][WM * TI][BN] floats, then 2 KiB per wave of store stage
-  x6_finish<BM, BN, WM, WN, SRB>(p, acc, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
+  x6_finish<BM, BN, WM, WN, SRB>(p, acc32, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,
                                  h.wide ? smem + 2 * WM * TI * BN : nullptr, colscale);
 }
 
@@ -1654,22 +1705,23 @@ static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false) {
+static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false, bool pre = false) {
+  if (pre) return (size_t)2 * (arows + 1) * 128 + (size_t)2 * tps * 2 * bn * 64 + 1024;
   return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 128 + 1024;
 }
 // taps per stage: two when the weight double-buffer fits in LDS (three measured within noise)
-static int h3_tps(int bn, int arows) {
+static int h3_tps(int bn, int arows, bool pre = false) {
   int t = 2;
-  while (t > 1 && h3_lds(bn, arows, t) > 160 * 1024) --t;
+  while (t > 1 && h3_lds(bn, arows, t, false, pre) > 160 * 1024) --t;
   return t;
 }
 
-template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false>
+template <int BM, int BN, int WM, int WN, int SRB, bool TWO_LEVEL, int TPS, bool BNB = false, bool PRE = false>
 static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int NT = WM * WN * 64;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
   const int T = nbm * nbn;
-  const size_t lds = h3_lds(BN, h.arows, TPS, BNB);
+  const size_t lds = h3_lds(BN, h.arows, TPS, BNB, PRE);
   if ((size_t)h.arows * ROW2 < (size_t)(2 * WM * BN + WM * WN * 512) * 4) h.wide = 0;   // F too small to stage
   static int slots = [&] {
     int dev = 0, cus = 0;
@@ -1684,8 +1736,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, BNB>), dim3(grid), dim3(NT), lds, st, p,
-                     h);
+  hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, BNB, PRE>), dim3(grid), dim3(NT), lds, st,
+                     p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
   return 0;
@@ -1716,7 +1768,7 @@ static bool h3r_fits(int bn, int arows) {
   return h3r_on() && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
 }
 
-template <int BN, int TPS>
+template <int BN, int TPS, bool PRE = false>
 static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   constexpr int BM = 256, WM = 4, SRB = 128;
   const int nbm = ceil_div(p.P, BM), nbn = ceil_div(p.Cout, BN);
@@ -1736,7 +1788,7 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB>), dim3(grid), dim3(256), lds, st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB, PRE>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
   return 0;
@@ -1995,6 +2047,67 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
     default: return H3_LAUNCH(32);
   }
 #undef H3_LAUNCH
+}
+
+// srpde_conv_fwd_h3 on an input that arrives as its h3 split (planes [2][P][c] fp16 hi / lo of
+// x * 2^h3_exp(*amax), e.g. srpde_bn_bwd_apply_split's dy): the halo tiles are DMA'd / loaded as
+// fp16 pieces straight into the MFMA operand layout, no fp32 tile, no split work and nothing to
+// store for the weight gradient (which reads the same planes).
+int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, const void* wsplit, const int* wexp,
+                               const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize,
+                               int dil, int sign, int accumulate, float* stats, const float* bn_y, int bn_ldy,
+                               const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                               const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
+                               hipStream_t stream) {
+  SRPDE_CHECK_ARG(xsplit && amax && wsplit && wexp && y, "srpde_conv_fwd_h3_presplit: null pointer");
+  SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0 && (sign == 1 || sign == -1), "srpde_conv_fwd_h3_presplit: bad shape");
+  SRPDE_CHECK_ARG(srpde_conv_h3_supported(c, 0, cout, w, dil, ksize),
+                  "srpde_conv_fwd_h3_presplit: unsupported shape (c=%d cout=%d w=%d dil=%d)", c, cout, w, dil);
+  SRPDE_CHECK_ARG(aligned16(xsplit) && aligned16(wsplit), "srpde_conv_fwd_h3_presplit: 16-byte alignment");
+  ConvParams p;
+  p.x0 = static_cast<const float*>(xsplit); p.c0 = c; p.ldx0 = c;   // [2][P][c] fp16 == P * c floats of bytes
+  p.x1 = nullptr; p.c1 = 0; p.ldx1 = 4;
+  p.w = nullptr; p.bias = bias; p.y = y; p.ldy = ldy;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
+  p.P = n * h * w; p.Cin = c; p.K = ksize * ksize * c;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  SRPDE_CHECK_ARG((long long)p.P * c * 4 < (1LL << 31) && 2LL * cout * p.K * 2 < (1LL << 31),
+                  "srpde_conv_fwd_h3_presplit: tensor too large");
+  SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
+                                          bn_ldy % 4 == 0 && cout % 4 == 0),
+                  "srpde_conv_fwd_h3_presplit: the fused BN reduction needs bn_y/mean/invstd/gamma/beta, no accumulate");
+  p.bn_y = bn_y; p.bn_ldy = bn_ldy; p.bn_mean = bn_mean; p.bn_invstd = bn_invstd;
+  p.bn_gamma = bn_gamma; p.bn_beta = bn_beta; p.bn_part = static_cast<float2*>(bn_part);
+  p.out_max = out_max;
+  H3Args a{};
+  a.wsp = static_cast<const _Float16*>(wsplit);
+  a.wexp = wexp;
+  a.amax0 = amax;
+  a.amax1 = nullptr;
+  a.halo = (w + 1) * dil;
+  a.arows = h3_arows(w, dil);
+  a.relax = 1;
+  a.xsplit = nullptr;
+  a.in_scale = nullptr; a.in_shift = nullptr;
+  a.wide = ldy % 4 == 0 && aligned16(y);
+  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
+    if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
+    return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
+  }
+  const int bn = h3_bn(h3_cfg(cout));
+  SRPDE_CHECK_ARG(h3_lds(bn, a.arows, 1, false, true) <= 160 * 1024, "srpde_conv_fwd_h3_presplit: LDS (w=%d dil=%d)", w,
+                  dil);
+  const int tps = h3_tps(bn, a.arows, true);
+#define H3P_LAUNCH(BN_)                                                                                   \
+  (tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2, false, true>(p, a, stream, workspace, ws_bytes) \
+            : launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 1, false, true>(p, a, stream, workspace, ws_bytes))
+  switch (h3_cfg(cout)) {
+    case 1: return H3P_LAUNCH(128);
+    case 2: return H3P_LAUNCH(64);
+    default: return H3P_LAUNCH(32);
+  }
+#undef H3P_LAUNCH
 }
 
 // dgrad with the BatchNorm (+ReLU) backward apply fused into the operand transform (BNB kernels):

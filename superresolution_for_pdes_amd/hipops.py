@@ -144,6 +144,37 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
 
 
+def conv_fwd_presplit(xp, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
+                      bn_bwd=None, out_max=None):
+    """conv_fwd on an input given as its h3 split ``xp`` ([2, P, c] fp16 carrying its max|.| word as
+    ``_srpde_amax``: bn_bwd_apply_split's dy, or a stored planes_out) -- srpde_conv_fwd_h3_presplit."""
+    c = xp.shape[2]
+    planes, wexp = wpack.h3
+    py, ldy = _pl(y)
+    for buf in (stats, bn_bwd[5] if bn_bwd is not None else None):
+        if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
+            raise ValueError("statistics buffer not laid out for the h3 kernel")
+    ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
+    call("srpde_conv_fwd_h3_presplit", xp.data_ptr(), c, xp._srpde_amax.data_ptr(), planes.data_ptr(), wexp.data_ptr(),
+         _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), *_bn_bwd_args(bn_bwd),
+         _p(out_max), ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+def bn_bwd_apply_split(y, da, mean, invstd, gamma, beta, m1, m2, dy_amax, out=None, relu=True):
+    """The BN (+ReLU) backward apply (bn_bwd_prepare's m1 / m2) written as the h3 split of dy:
+    [2, P, C] fp16 planes scaled by 2^h3_exp(dy_amax), tagged with that word (srpde_bn_bwd_apply_split)."""
+    P, C = y.shape
+    py, ldy = _pl(y)
+    pda, ldda = _pl(da)
+    if out is None:
+        out = split_planes_buffer(P, C, y.device)
+    call("srpde_bn_bwd_apply_split", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), P, C, BN_RELU if relu else 0, dy_amax.data_ptr(),
+         out.data_ptr(), stream_ptr())
+    out._srpde_amax = dy_amax
+    return out
+
+
 def _ep_args(ep_bn):
     if ep_bn is None:
         return (0, 0, 0, 0, 0)

@@ -423,6 +423,31 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         else:
             wq.submit(fn, keep)
         return None if out_part is None else (out_part, dx_max)
+    if (_PRESPLIT_BWD and train and dx is not None and xp is not None and H.h3_capable(cout, 0, cin, w, dil)):
+        # the BN backward apply writes dy as its h3 split (scale from bn_bwd_prepare's rigorous bound);
+        # the dgrad reads the fp16 pieces straight into its operand tiles and the weight gradient
+        # reads the same planes: no fp32 dy, no split work or split store in the dgrad
+        m1, m2, dyw = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
+                                       grads[conv.bias], part=part_t, da_max=da_max)
+        dyp = H.bn_bwd_apply_split(y, da, mean, invstd, bn.weight, bn.bias, m1, m2, dyw)
+        if DEBUG_TAPS is not None:
+            _tap("dyp:" + getattr(conv, "_srpde_name", "?"), dyp)
+        wd = _dgrad_weights(conv, cin, w, dil)
+        bn_bwd, dx_max = None, None
+        if below is not None and not dx_accumulate and _FUSE_BN_BWD:
+            bnb, sb = below
+            out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
+            bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
+            if _FUSE_BN_APPLY:   # max|dx| slots for the layer below's BN backward bound
+                dx_max = H.out_max_slots(n, h, w, cout, cin, dil, y.device)
+        H.conv_fwd_presplit(dyp, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, bn_bwd=bn_bwd,
+                            out_max=dx_max)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
+        if wq is None:
+            fn()
+        else:
+            wq.submit(fn, keep)
+        return None if out_part is None else (out_part, dx_max)
     dy = H.empty(P, cout, device=y.device)
     # eval mode: the forward normalised with the running statistics (constants), so the BN
     # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
@@ -463,6 +488,10 @@ _FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
 # >= _BNB_MIN_COUT (two input chunks); wider (dec1.conv1's 3-tile dgrad, out_conv1's one-chunk dy)
 # measured +0.5 ms in the step
 _BNB_MAX_CIN, _BNB_MIN_COUT = 64, 64
+
+# the BN backward apply writes dy as its h3 split for a presplit dgrad (SRPDE_PRESPLIT_BWD=0: fp32 dy,
+# split inside the dgrad)
+_PRESPLIT_BWD = os.environ.get("SRPDE_PRESPLIT_BWD", "1") != "0"
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
 _FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"

@@ -569,3 +569,67 @@ def test_bn_relu_gate_matches_separate_passes():
     torch.cuda.synchronize()
     assert torch.equal(a1, a2)
     assert float((sa - sa_ref).abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("n,c,cout,hw,dil,sign", [(4, 64, 64, 40, 1, -1), (3, 128, 64, 20, 1, -1),
+                                                  (2, 256, 512, 10, 2, -1), (4, 512, 256, 10, 1, -1),
+                                                  (3, 64, 32, 40, 1, 1), (5, 128, 128, 20, 1, 1)])
+def test_conv_presplit_equals_inline_split(n, c, cout, hw, dil, sign):
+    """srpde_conv_fwd_h3_presplit on the split the inline kernel stored (planes_out) computes every
+    output element, BN partial, fused BN-backward partial and per-tile max in equal bits: the same
+    fp16 operands in the same MFMA order (8-wave kernel for >64 output channels, h3r below)."""
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("h3")
+    g = torch.Generator(device=DEV).manual_seed(c + cout + hw)
+    P = n * hw * hw
+    x = torch.randn(P, c, device=DEV, generator=g)
+    x._srpde_amax = H.amax_of(x)
+    w = torch.randn(cout, c, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g) if sign > 0 else None
+    wf, _ = H.pack_conv_weights(w, c, True, False)   # [cout][tap][c] rows: either pass's layout
+    by = torch.randn(P, cout, device=DEV, generator=g)
+    bmean, binv = torch.randn(cout, device=DEV, generator=g) * 0.1, torch.rand(cout, device=DEV, generator=g) + 0.5
+    bga, bbe = torch.randn(cout, device=DEV, generator=g), torch.randn(cout, device=DEV, generator=g) * 0.1
+    outs = []
+    xp = H.split_planes_buffer(P, c, DEV)
+    for pre in (False, True):
+        y = torch.empty(P, cout, device=DEV)
+        part = H.bn_bwd_partials(n, hw, hw, cout, DEV)
+        omax = H.out_max_slots(n, hw, hw, c, cout, dil, DEV)
+        bnb = (by, bmean, binv, bga, bbe, part)
+        if not pre:
+            H.conv_fwd(x, None, wf, b, y, n, hw, hw, cout, 3, dil, sign, False, None, xp, bn_bwd=bnb, out_max=omax)
+            xp._srpde_amax = x._srpde_amax
+        else:
+            H.conv_fwd_presplit(xp, wf, b, y, n, hw, hw, cout, 3, dil, sign, False, None, bn_bwd=bnb, out_max=omax)
+        torch.cuda.synchronize()
+        outs.append((y.clone(), part.clone(), omax.clone()))
+    for name, a, b_ in zip(("y", "bn_part", "out_max"), *outs):
+        assert torch.equal(a, b_), name
+
+
+@pytest.mark.parametrize("P,C", [(1024 * 100, 256), (3 * 1600, 64), (777, 32)])
+def test_bn_bwd_apply_split_matches_fp32_apply(P, C):
+    """srpde_bn_bwd_apply_split's planes hold bn_relu_bwd's dy: (hi + lo) / s equals the fp32 apply
+    to the split's representation error (2^-22 of the scale), and the scale word is a bound."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator(device=DEV).manual_seed(P + C)
+    y = torch.randn(P, C, device=DEV, generator=g) * 2 + 0.5
+    da = torch.randn(P, C, device=DEV, generator=g)
+    mean, invstd = y.mean(0), y.var(0, unbiased=False).add(1e-5).rsqrt()
+    gamma = torch.randn(C, device=DEV, generator=g)
+    beta = torch.randn(C, device=DEV, generator=g) * 0.1
+    d1, d2, d3 = (torch.empty(C, device=DEV) for _ in range(3))
+    m1, m2, word = H.bn_bwd_prepare(y, da, mean, invstd, gamma, beta, d1, d2, d3)
+    planes = H.bn_bwd_apply_split(y, da, mean, invstd, gamma, beta, m1, m2, word)
+    dy = torch.empty(P, C, device=DEV)
+    e1, e2, e3 = (torch.empty(C, device=DEV) for _ in range(3))
+    H.bn_relu_bwd(y, da, mean, invstd, gamma, beta, dy, e1, e2, e3)
+    torch.cuda.synchronize()
+    bound = float(word.view(torch.float32))
+    assert bound >= float(dy.abs().max())
+    e = int(np.floor(np.log2(bound))) + 1           # h3_exp: max < 2^e -> scale 2^(15 - e)
+    s = 2.0 ** (15 - e)
+    deq = (planes[0].double() + planes[1].double()) / s
+    err = float((deq - dy.double()).abs().max())
+    assert err <= 2.0 ** -22 * (2.0 ** 15 / s) + 1e-30, (err, bound)
