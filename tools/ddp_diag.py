@@ -1,23 +1,49 @@
-import os, sys, json, torch, torch.distributed as dist
-sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
-rank = int(os.environ["RANK"]); dev = torch.device("cuda", 0); torch.cuda.set_device(dev)
+"""Diagnostic: two ranks on one GPU over gloo -- per-tensor comparison of the DataParallel step's
+all-reduced gradients with the mean of each rank's single-process gradient (tests/test_gpu_ddp.py)."""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dev = torch.device("cuda", 0); torch.cuda.set_device(dev)
 dist.init_process_group("gloo")
 from superresolution_for_pdes_amd.functional import mse_loss
 from superresolution_for_pdes_amd.models import UNet, init_weights
+from superresolution_for_pdes_amd.distributed import DataParallel
 torch.manual_seed(42); m = UNet(); m.apply(init_weights); m = m.to(dev).train(); m.flatten_parameters_()
 g = torch.Generator(device=dev).manual_seed(1000 + rank)
-x = torch.randn(64, 3, 40, 40, device=dev, generator=g); x[:, 1] = 1.0
-t = torch.randn(64, 1, 40, 40, device=dev, generator=g)
-res = []
-for k in range(4):
+B = int(os.environ.get("DIAG_B", "64"))
+x = torch.randn(B, 3, 40, 40, device=dev, generator=g); x[:, 1] = 1.0
+t = torch.randn(B, 1, 40, 40, device=dev, generator=g)
+flat = lambda: torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu()  # noqa: E731
+for p in m.parameters(): p.grad = None
+out0 = m(x); l0 = mse_loss(out0, t); l0.backward(); torch.cuda.synchronize()
+out0 = out0.detach().cpu()
+loc = flat()
+x_ref = x.detach().cpu().clone()
+p_ref = torch.cat([q.detach().reshape(-1) for q in m.parameters()]).cpu()
+parts = [torch.empty_like(loc) for _ in range(world)]
+dist.all_gather(parts, loc)
+want = sum(parts) / world
+if os.environ.get("DIAG_NODP") == "1":   # no reducer: each rank repeats its own plain step
+    net, want = m, parts[rank]
+else:
+    net = DataParallel(m, bucket_bytes=int(os.environ.get("DIAG_BUCKET", str(8 << 20))),
+                       broadcast_buffers=os.environ.get("DIAG_BCAST", "1") == "1")
+for k in range(int(os.environ.get("DIAG_STEPS", "6"))):
     for p in m.parameters(): p.grad = None
-    out = m(x); mse_loss(out, t).backward(); torch.cuda.synchronize()
-    res.append((out.detach().cpu().clone(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu()))
-names = [n for n, _ in m.named_parameters()]
-offs = []; o = 0
-for _, p in m.named_parameters(): offs.append((o, p.numel())); o += p.numel()
-for k in range(1, 4):
-    do = float((res[k][0] - res[0][0]).abs().max()); dg = float((res[k][1] - res[0][1]).norm() / res[0][1].norm())
-    bad = [names[i] for i, (a, n) in enumerate(offs) if not torch.equal(res[k][1][a:a+n], res[0][1][a:a+n])]
-    print(f"rank {rank} step {k}: out maxdiff {do:.3e} grad rel {dg:.3e} differing {len(bad)}: {bad[:6]}", flush=True)
+    xs = torch.equal(x.detach().cpu(), x_ref)
+    ps = torch.equal(torch.cat([q.detach().reshape(-1) for q in m.parameters()]).cpu(), p_ref)
+    if not (xs and ps):
+        print(f"rank {rank} dp step {k}: INPUT CHANGED x {xs} params {ps}", flush=True)
+    out1 = net(x); l1 = mse_loss(out1, t)
+    torch.cuda.synchronize()
+    print(f"rank {rank} dp step {k}: out equal {torch.equal(out1.detach().cpu(), out0)} loss {float(l0):.8f} vs {float(l1):.8f}", flush=True)
+    l1.backward(); torch.cuda.synchronize()
+    red = flat()
+    o = 0; bad = []
+    for n, p in m.named_parameters():
+        a, b = red[o:o + p.numel()], want[o:o + p.numel()]
+        if not torch.equal(a, b):
+            bad.append((n, float((a - b).norm() / max(float(b.norm()), 1e-30)), float((a - parts[rank][o:o+p.numel()]).norm() / max(float(b.norm()), 1e-30))))
+        o += p.numel()
+    print(f"rank {rank} dp step {k}: {len(bad)} differ; first: {bad[:5]}", flush=True)
 dist.barrier(); dist.destroy_process_group()
