@@ -10,7 +10,8 @@
  *
  * Conventions
  *  - All tensor arguments are caller-owned DEVICE pointers; the library never allocates,
- *    frees or synchronises the host (one exception: srpde_poisson_cg_batched for n > 128).  Scratch is passed in as (workspace, ws_bytes), its
+ *    frees or synchronises the host (one exception: srpde_poisson_cg_batched for a single problem
+ *    too large for one cooperative grid, n > ~1400).  Scratch is passed in as (workspace, ws_bytes), its
  *    size queried with the matching *_workspace_size() function.
  *  - Activations are NHWC fp32 ("channels-last").  A view is (pointer, ld): ld = floats
  *    between consecutive pixels, so channel slices of a wider tensor (virtual concat) need
@@ -341,12 +342,15 @@ int srpde_forcing_batched(const double* k12, int B, int n, double* out, hipStrea
 size_t srpde_poisson_workspace_size(int B, int n);
 /* The batched solve in one call (replaces spsolve(diag(theta) @ L, f), data_generation.py:79-104,
  * for B problems at once): f, theta, u are [B][n][n] fp64 device arrays, iters_out [B] int32
- * (nullable).  n <= srpde_poisson_lds_max_n(): one stream-ordered launch, no workspace.  Larger n:
- * grid CG with workspace (srpde_poisson_workspace_size bytes); the call polls convergence every
- * 128 iterations and therefore synchronises `stream` -- the one entry of this library that blocks
- * the host.  The split entry points below are the same solve, for callers that poll themselves. */
+ * (nullable; -1 marks a problem whose cooperative launch aborted at a stuck grid barrier).
+ * n <= srpde_poisson_lds_max_n(): one stream-ordered launch, no workspace.  Larger n: grid CG with
+ * workspace (srpde_poisson_workspace_size bytes), run as cooperative launches of
+ * srpde_poisson_coop_problems(n) problems each -- stream-ordered, the host never waits.  Only when
+ * that count is 0 (one problem larger than the co-resident grid) the call drives the split entry
+ * points below and polls convergence every 128 iterations, synchronising `stream`. */
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+int srpde_poisson_coop_problems(int n);
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream);
 int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,

@@ -120,7 +120,14 @@ __global__ void maxpool2_bwd_kernel(const float* __restrict__ x, int ldx, const 
 struct Lerp { int i0, i1; float l0, l1; };
 __device__ __forceinline__ Lerp lerp_index(int o, int in, int out) {
   const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-  const float src = scale * (float)o;
+  // rounded product, as aten's area_pixel_compute_source_index: with contraction on, the compiler
+  // may fuse src - i0 below into fma(scale, o, -i0) (it did once packed-FP32 ops were disabled), which
+  // moves the weights by up to an ulp of src (~2e-6 at src ~ 19) and the interpolated values with them
+  float src;
+  {
+#pragma clang fp contract(off)
+    src = scale * (float)o;
+  }
   Lerp r;
   r.i0 = (int)src;
   r.i1 = r.i0 + (r.i0 < in - 1 ? 1 : 0);

@@ -256,6 +256,147 @@ __global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restr
   if (blockIdx.x == 0 && threadIdx.x == 0 && iters) iters[b] = g.done[b] ? g.iters[b] : maxit;
 }
 
+// ---------------- grid CG in ONE cooperative launch (n > 128, stream-ordered) ----------------
+// The same iteration as gcg_a / gcg_b (same per-block partial sums, same re-reduction order, same
+// expressions: bit-identical iterates) with the two launch boundaries of an iteration replaced by
+// two grid barriers, so the solve is one launch and the host never polls.  Every block owns GCG_PTS
+// points of one problem; x, r, p and q of its points stay in registers, r and p are also written to
+// HBM for the neighbours' stencils (p double-buffered by parity).  All blocks co-reside
+// (hipLaunchCooperativeKernel checks it); a problem that converges keeps its blocks at the barriers
+// until every problem of the launch has (ctl[0] counts them), and every block leaves the loop at the
+// same barrier.  A barrier that waits longer than ~1 s sets ctl[1] (abort), which releases every
+// waiter: the launch then ends with iters = -1 instead of hanging the queue.
+struct GridCoop {
+  double *r, *p0, *p1;          // [B][N2]
+  double *rrp, *pqp;            // [B][nb] per-block partials
+  unsigned long long* bar;      // barrier arrivals (monotonic; zeroed before the launch)
+  unsigned* ctl;                // [0] problems converged, [1] abort
+  int n, nb, B;
+  double rtol;
+};
+
+__device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long target, int* sflag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();   // release this block's r / p / partial stores to the other XCDs
+    __hip_atomic_fetch_add(g.bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    int ab = 0;
+    for (unsigned spins = 0;; ++spins) {
+      if (__hip_atomic_load(g.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(g.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
+      if (spins > (1u << 24)) {
+        __hip_atomic_store(g.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ab = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence();   // acquire
+    *sflag = ab;
+  }
+  __syncthreads();
+  return *sflag == 0;
+}
+
+__global__ __launch_bounds__(GCG_T) void gcg_coop_kernel(const double* __restrict__ f,
+                                                         const double* __restrict__ theta, double* __restrict__ u,
+                                                         int* __restrict__ iters, GridCoop g, int maxit) {
+  __shared__ double sh[8];
+  __shared__ int sflag;
+  const int b = blockIdx.x / g.nb, j = blockIdx.x - b * g.nb;
+  const int n = g.n, N2 = n * n;
+  const size_t off = (size_t)b * N2;
+  const unsigned long long nblk = gridDim.x;
+  unsigned long long epoch = 0;
+  const double inv_h2 = (double)(n - 1) * (double)(n - 1);
+  const double* rpart = g.rrp + (size_t)b * g.nb;
+  const double* qpart = g.pqp + (size_t)b * g.nb;
+  double* rv = g.r + off;
+  double x[GCG_NPT], r[GCG_NPT], p[GCG_NPT], q[GCG_NPT];
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < GCG_NPT; ++k) {
+    const int i = j * GCG_PTS + k * GCG_T + threadIdx.x;
+    x[k] = 0.0; p[k] = 0.0; q[k] = 0.0; r[k] = 0.0;
+    if (i < N2) {
+      r[k] = -f[off + i] / theta[off + i];
+      rv[i] = r[k];
+      g.p0[off + i] = 0.0;
+      s += r[k] * r[k];
+    }
+  }
+  write_part(s, sh, g.rrp + (size_t)b * g.nb + j);
+  bool ok = coop_sync(g, ++epoch * nblk, &sflag);
+  const double bb = sum_parts(rpart, g.nb, sh);
+  double rr = bb, rr_old = 1.0;
+  bool done = false;
+  int it_done = maxit;
+  for (int k = 0; ok; ++k) {
+    // A (gcg_a_kernel): convergence, beta, p <- r + beta p, q = A p, <p, q> partials
+    if (!done && (rr <= g.rtol * g.rtol * bb || k >= maxit)) {
+      done = true;
+      it_done = k;
+      if (j == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(g.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!done) {
+      const double beta = k == 0 ? 0.0 : rr / rr_old;
+      const double* po = ((k & 1) ? g.p1 : g.p0) + off;
+      double* pn = ((k & 1) ? g.p0 : g.p1) + off;
+      s = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < GCG_NPT; ++kk) {
+        const int i = j * GCG_PTS + kk * GCG_T + threadIdx.x;
+        if (i < N2) {
+          const int yy = i / n, xx = i - yy * n;
+          auto pv = [&](int jj) { return rv[jj] + beta * po[jj]; };
+          const double pc = r[kk] + beta * p[kk];
+          double nb = 0.0;
+          if (xx > 0) nb += pv(i - 1);
+          if (xx < n - 1) nb += pv(i + 1);
+          if (yy > 0) nb += pv(i - n);
+          if (yy < n - 1) nb += pv(i + n);
+          q[kk] = (4.0 * pc - nb) * inv_h2;
+          p[kk] = pc;
+          pn[i] = pc;
+          s += pc * q[kk];
+        }
+      }
+      write_part(s, sh, g.pqp + (size_t)b * g.nb + j);
+    }
+    ok = coop_sync(g, ++epoch * nblk, &sflag);
+    // every increment of ctl[0] precedes this barrier and the next one follows these reads: all
+    // blocks read the same count and leave together
+    if (!ok || __hip_atomic_load(g.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)g.B) break;
+    // B (gcg_b_kernel): alpha, x += alpha p, r -= alpha q, <r, r> partials
+    if (!done) {
+      const double alpha = rr / sum_parts(qpart, g.nb, sh);
+      s = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < GCG_NPT; ++kk) {
+        const int i = j * GCG_PTS + kk * GCG_T + threadIdx.x;
+        if (i < N2) {
+          x[kk] += alpha * p[kk];
+          r[kk] = r[kk] - alpha * q[kk];
+          rv[i] = r[kk];
+          s += r[kk] * r[kk];
+        }
+      }
+      write_part(s, sh, g.rrp + (size_t)b * g.nb + j);
+    }
+    ok = coop_sync(g, ++epoch * nblk, &sflag);
+    if (!done) {
+      rr_old = rr;
+      rr = sum_parts(rpart, g.nb, sh);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GCG_NPT; ++k) {
+    const int i = j * GCG_PTS + k * GCG_T + threadIdx.x;
+    if (i < N2) u[off + i] = x[k];
+  }
+  if (j == 0 && threadIdx.x == 0 && iters) iters[b] = ok ? it_done : -1;
+}
+
 static GridCG carve(void* ws, int B, int n) {
   GridCG g;
   const size_t N2 = (size_t)n * n;
@@ -377,15 +518,75 @@ int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit,
   return 0;
 }
 
-// One entry for any n (SURVEY 8(b)'s srpde_poisson_cg_batched): n <= 128 is one stream-ordered
-// launch (LDS-resident CG); n > 128 runs the grid CG from the host in chunks of kCheckEvery
-// iterations and polls the device done flags after each chunk -- the only call of the library that
-// synchronises `stream` (it must know when to stop issuing iterations).  ws: srpde_poisson_workspace_size.
+// co-resident blocks of gcg_coop_kernel on this device (0: no cooperative launch)
+static int coop_capacity() {
+  static const int cap = [] {
+    int dev = 0, cus = 0, per = 0, coop = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&gcg_coop_kernel), GCG_T, 0) !=
+        hipSuccess)
+      return 0;
+    return coop ? per * cus : 0;
+  }();
+  return cap;
+}
+
+// Problems per cooperative launch at this n (0: one problem does not fit the co-resident grid)
+int srpde_poisson_coop_problems(int n) {
+  const long long nb = ceil_div((long long)n * n, GCG_PTS);
+  return nb <= coop_capacity() ? (int)(coop_capacity() / nb) : 0;
+}
+
+// the whole grid CG of problems [b0, b0 + cnt) in one cooperative launch (workspace carved for B)
+static int coop_solve(const double* f, const double* theta, double* u, int* iters, int b0, int cnt, int B, int n,
+                      double rtol, int maxit, void* ws, hipStream_t stream) {
+  const GridCG c = carve(ws, B, n);
+  const size_t N2 = (size_t)n * n;
+  GridCoop g;
+  g.r = c.r + b0 * N2; g.p0 = c.p0 + b0 * N2; g.p1 = c.p1 + b0 * N2;
+  g.rrp = c.rrp0 + (size_t)b0 * c.nb; g.pqp = c.pqp + (size_t)b0 * c.nb;
+  g.bar = reinterpret_cast<unsigned long long*>(c.bbp);   // B * nb >= 2 doubles for n > 128
+  g.ctl = reinterpret_cast<unsigned*>(c.bbp + 1);
+  g.n = n; g.nb = c.nb; g.B = cnt; g.rtol = rtol;
+  hipError_t e = hipMemsetAsync(c.bbp, 0, 2 * sizeof(double), stream);
+  if (e != hipSuccess) { set_error("srpde_poisson_cg_batched: memset: %s", hipGetErrorString(e)); return (int)e; }
+  const double* fb = f + b0 * N2;
+  const double* tb = theta + b0 * N2;
+  double* ub = u + b0 * N2;
+  int* ib = iters ? iters + b0 : nullptr;
+  void* args[] = {&fb, &tb, &ub, &ib, &g, &maxit};
+  e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&gcg_coop_kernel), dim3(cnt * c.nb), dim3(GCG_T), args,
+                                 0, stream);
+  if (e != hipSuccess) {
+    set_error("srpde_poisson_cg_batched: cooperative launch failed: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+
+// One entry for any n (SURVEY 8(b)'s srpde_poisson_cg_batched), stream-ordered: n <= 128 is one
+// launch of the LDS-resident CG; n > 128 runs the grid CG as cooperative launches (one per group of
+// srpde_poisson_coop_problems(n) problems), whose grid barriers replace the launch boundaries and
+// whose device-side convergence count ends the loop -- nothing returns to the host.  Only a single
+// problem too large for the co-resident grid (n > ~1400 on MI355X) still runs the launch-per-iteration
+// grid CG polled from the host every 128 iterations (that case synchronises `stream`).
+// ws: srpde_poisson_workspace_size.
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(f && theta && u && B > 0 && n >= 2 && maxit >= 0, "srpde_poisson_cg_batched: bad args");
   if (n <= srpde_poisson_lds_max_n())
     return srpde_poisson_cg_lds(f, theta, u, B, n, rtol, maxit, iters_out, nullptr, stream);
+  SRPDE_CHECK_ARG(workspace && ws_bytes >= grid_ws_bytes(B, n), "srpde_poisson_cg_batched: workspace too small");
+  const int per = srpde_poisson_coop_problems(n);
+  if (per > 0) {
+    for (int b0 = 0; b0 < B; b0 += per) {
+      const int rc = coop_solve(f, theta, u, iters_out, b0, std::min(per, B - b0), B, n, rtol, maxit, workspace, stream);
+      if (rc != 0) return rc;
+    }
+    return 0;
+  }
   constexpr int kCheckEvery = 128;
   int rc = srpde_poisson_cg_grid_init(f, theta, B, n, workspace, ws_bytes, stream);
   if (rc != 0) return rc;

@@ -34,7 +34,13 @@ __global__ __launch_bounds__(256) void resize_bicubic_ac_kernel(const float* __r
     const long long pl = e / ((long long)ho * wo);
     const int rem = (int)(e - pl * ho * wo);
     const int oy = rem / wo, ox = rem - oy * wo;
-    const float ry = sy * (float)oy, rx = sx * (float)ox;
+    // rounded products (no contraction into the fractional parts below), as aten computes them
+    float ry, rx;
+    {
+#pragma clang fp contract(off)
+      ry = sy * (float)oy;
+      rx = sx * (float)ox;
+    }
     const int iy = (int)floorf(ry), ix = (int)floorf(rx);
     float cy[4], cx[4];
     cubic_coeffs(ry - (float)iy, cy);

@@ -5,8 +5,9 @@ operator (reference src/data_generation.py:35-104, src/enhanced_data_generation.
 (h = 1/(n-1), all n^2 nodes unknown, zero ghost ring -- exactly diag(theta) @ L of the
 reference) as the SPD system (-L) u = -f/theta by matrix-free CG in fp64:
   * n <= 128 : one workgroup per problem, direction vector in LDS (one launch);
-  * n  > 128 : grid CG, two launches per iteration; the host polls a device `done` flag
-               every 128 iterations (the only host sync of the path).
+  * n  > 128 : grid CG as cooperative launches (srpde_poisson_coop_problems(n) problems each):
+               two grid barriers per iteration instead of two launches, convergence decided on
+               the device -- stream-ordered, no host sync.
 Both go through the single C entry ``srpde_poisson_cg_batched`` (include/srpde.h), which a
 non-Python caller binds the same way.
 """

@@ -23,13 +23,14 @@ _BLOCKS = ["enc1", "enc2", "enc3", "dec3", "dec2", "dec1"]
 
 def hip_step(model, x, t, want_dx=True):
     """One forward (save=True) + MSE backward through the executor, weight gradients on the side
-    stream as in training.  Returns (out, {param name: grad}, dx or None, S)."""
+    stream as in training (unless unet_exec._WGRAD_STREAM is off).  Returns (out, {param name: grad},
+    dx or None, S)."""
     out, S = X.unet_forward(model, x, model.training, save=True)
     dout = (2.0 / out.numel()) * (out - t)
     layout = model._flat_layout()
     flat = torch.empty(layout[-1][2] + layout[-1][3], device=x.device)
     views = {p: flat[o:o + n].view_as(p) for _, p, o, n in layout}
-    wq = X.WgradStream(x.device)
+    wq = X.WgradStream(x.device) if X._WGRAD_STREAM else None
     dx = X.unet_backward(model, S, dout.reshape(-1), views, wq=wq, want_dx=want_dx)
     torch.cuda.synchronize()
     names = {p: n for n, p in model.named_parameters()}

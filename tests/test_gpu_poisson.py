@@ -62,6 +62,60 @@ def test_batched_large_against_oracle():
         assert rel(un[b], R.solve(fn[b], tn[b])) < 1e-10
 
 
+def _polled_grid_cg(f, th, rtol, maxit):
+    """The launch-per-iteration grid CG driven from the host through the split entry points
+    (srpde_poisson_cg_grid_init / _iterate / _finish), polling the done flags every 64 iterations."""
+    from superresolution_for_pdes_amd._lib import call, query, stream_ptr
+    B, n, _ = f.shape
+    ws_bytes = int(query("srpde_poisson_workspace_size", B, n))
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=f.device)
+    done_at = int(query("srpde_poisson_cg_grid_done_offset", B, n))
+    done = ws[done_at:done_at + 4 * B].view(torch.int32)
+    u = torch.empty_like(f)
+    it = torch.empty(B, dtype=torch.int32, device=f.device)
+    sp = stream_ptr()
+    call("srpde_poisson_cg_grid_init", f.data_ptr(), th.data_ptr(), B, n, ws.data_ptr(), ws_bytes, sp)
+    k = 0
+    while k <= maxit:
+        cnt = min(64, maxit + 1 - k)
+        call("srpde_poisson_cg_grid_iterate", B, n, float(rtol), k, cnt, int(maxit), ws.data_ptr(), ws_bytes, sp)
+        k += cnt
+        if bool((done != 0).all()):
+            break
+    call("srpde_poisson_cg_grid_finish", u.data_ptr(), it.data_ptr(), B, n, int(maxit), ws.data_ptr(), ws_bytes, sp)
+    return u, it
+
+
+@pytest.mark.parametrize("n,B", [(129, 3), (320, 0), (200, 5)])
+def test_cooperative_grid_cg_equals_polled(n, B):
+    """n > 128: srpde_poisson_cg_batched runs the grid CG as cooperative launches whose grid barriers
+    replace the launch boundaries (stream-ordered, no host poll).  Same partial sums, reduction order
+    and expressions as the launch-per-iteration kernels: u and the iteration counts are bit-identical
+    to the polled split entries, per problem, across launch groups (B = 0 here means one more problem
+    than fit one cooperative launch at this n) and with a problem that converges at once (zero forcing)
+    and one stopped by maxit."""
+    from superresolution_for_pdes_amd import poisson as P
+    from superresolution_for_pdes_amd._lib import query
+    per = int(query("srpde_poisson_coop_problems", n))
+    assert per >= 1
+    if B == 0:
+        B = per + 1
+    rng = np.random.default_rng(n + B)
+    f = P.forcing_batched(rng.uniform(0.5, 8.0, (B, 2)), n)
+    f[B // 2] = 0.0
+    th = torch.from_numpy(rng.uniform(0.5, 2.0, (B, n, n))).cuda()
+    for maxit in (20 * n * n, 37):
+        u, it = P.solve_batched(f, th, maxit=maxit, return_iters=True)
+        u2, it2 = _polled_grid_cg(f, th, P.DEFAULT_RTOL, maxit)
+        assert torch.equal(it, it2), (it.tolist(), it2.tolist())
+        assert torch.equal(u, u2)
+        assert int(it[B // 2]) == 0 and float(u[B // 2].abs().max()) == 0.0
+        if maxit == 37:
+            assert int(it.max()) == 37
+        else:
+            assert int(it.max()) < 10 * n
+
+
 def test_edge_cases():
     from superresolution_for_pdes_amd import poisson as P
     from oracle import poisson_ref as R

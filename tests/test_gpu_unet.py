@@ -330,16 +330,36 @@ SWITCHES = ("_FUSE_D1", "_FIN_AFFINE", "_FUSE_SA", "_FUSE_ATT_CH", "_FUSE_POOL",
 
 
 @pytest.mark.parametrize("off", [SWITCHES] + [(s,) for s in SWITCHES])
-def test_executor_switches_off_match_defaults(off):
+def test_executor_switches_off_match_fp64(off):
     """Every executor switch left in unet_exec (each fused pass against its separate passes, the
-    side-stream placements against in-line) gives the default train step's output, BN running
-    statistics and gradients to fp32 accuracy -- all off at once and each alone, so every
-    dispatchable path of the executor runs on the GPU.  Gradient bar 5e-4: a fused pass rounds
-    differently, and a ReLU-mask / max-pool decision that flips moves a layer's weight gradient by
-    ~1e-4 at this batch (measured 1.5e-4 on enc1.conv1 with all switches off); a wrong path is O(1)."""
+    side-stream placements against in-line), all off at once and each alone, so every dispatchable
+    path of the executor runs on the GPU.  Each path's train step is held to the fp64 oracle evaluated
+    on that path's OWN branch (its ReLU masks and max-pool argmaxes, tests/golden/branch.py): every
+    gradient and the input gradient to max(1e-4, 3x the oracle's own fp32 error on that branch) -- a
+    scalar such as a spatial-attention bias gradient is a sum of cancelling terms whose fp32 error
+    alone reaches ~1e-4 -- and the output to 3e-5 of its std.  Two paths are not compared with each other gradient by
+    gradient: they round differently, so a few ReLU-mask / max-pool decisions within rounding of the
+    threshold flip, and one flip moves a layer's weight gradient by ~1e-3 at B = 16 (measured 1.7e-3 on
+    enc1.conv1 with every switch off), which says nothing about the path.  The output and the BN
+    running statistics, which flips barely move, are also held to the default path's (1e-5)."""
+    from branch import hip_decisions, hip_step
+    from oracle.unet_ref import clone_state, unet_forward as ref_fwd, trainable_names
     from superresolution_for_pdes_amd import unet_exec
-    x = torch.randn(16, 3, 40, 40, generator=torch.Generator().manual_seed(4)).to(DEV)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(16, 3, 40, 40, generator=g)
     x[:, 1] = 1.0
+    t = torch.randn(16, 1, 40, 40, generator=g)
+    names = trainable_names()
+
+    def oracle_step(dec, dtype):
+        st = clone_state(fixture_state_torch(dtype))
+        for n_ in names:
+            st[n_].requires_grad_(True)
+        xr = x.to(dtype).detach().clone().requires_grad_(True)
+        out = ref_fwd(st, xr, True, decisions=dec)
+        torch.nn.functional.mse_loss(out, t.to(dtype)).backward()
+        return out.detach().double(), {n_: st[n_].grad.double() for n_ in names}, xr.grad.double()
+
     saved = {k: getattr(unet_exec, k) for k in SWITCHES}
     res = []
     try:
@@ -347,25 +367,33 @@ def test_executor_switches_off_match_defaults(off):
             for k in SWITCHES:
                 setattr(unet_exec, k, saved[k] and k not in turn_off)
             m = make_model(True)
-            out = m(x)
-            (out ** 2).mean().backward()
-            torch.cuda.synchronize()
-            g = {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}
+            m.flatten_parameters_()
+            out, grads, dx, S = hip_step(m, x.to(DEV), t.to(DEV))
+            dec = hip_decisions(m, S)
             rs = {n: b.detach().double().cpu() for n, b in m.named_buffers() if "running" in n}
-            res.append((out.detach().double().cpu(), g, rs))
+            res.append((out.detach().double().cpu(), rs))
+            o64, g64, dx64 = oracle_step(dec, torch.float64)
+            _, g32, dx32 = oracle_step(dec, torch.float32)
+            assert rmse(out.detach().cpu(), o64) <= 3e-5 * float(o64.std()), turn_off
+            bad = []
+            for n_ in names:
+                if _bn_fed_conv_bias(n_):
+                    assert float(grads[n_].norm()) <= 1e-4, (turn_off, n_)   # true gradient 0
+                    continue
+                e = float((grads[n_].double().cpu() - g64[n_]).norm() / g64[n_].norm())
+                e32 = float((g32[n_] - g64[n_]).norm() / g64[n_].norm())
+                if e > max(1e-4, 3 * e32):
+                    bad.append((n_, e, e32))
+            assert not bad, (turn_off, bad[:4])
+            egx = float((dx.double().cpu() - dx64).norm() / dx64.norm())
+            assert egx <= max(1e-4, 3 * float((dx32 - dx64).norm() / dx64.norm())), (turn_off, egx)
     finally:
         for k, v in saved.items():
             setattr(unet_exec, k, v)
-    (o0, g0, r0), (o1, g1, r1) = res
+    (o0, r0), (o1, r1) = res
     assert float((o0 - o1).norm() / o0.norm()) <= 1e-5
     for n in r0:
         assert float((r0[n] - r1[n]).norm() / max(float(r0[n].norm()), 1e-30)) <= 1e-5, n
-    for n in g0:
-        if _bn_fed_conv_bias(n):
-            assert float(g1[n].norm()) <= 1e-4, n   # true gradient 0
-            continue
-        e = float((g0[n] - g1[n]).norm() / max(float(g0[n].norm()), 1e-30))
-        assert e < 5e-4, (n, e)
 
 
 @pytest.mark.parametrize("B", [3, 64])
