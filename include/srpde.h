@@ -78,8 +78,9 @@ int srpde_conv_h3r_set(int on);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]
- * weights: desc = device int64 [nlayers][9] = {w, cout, cin_real, cin_pad, planes_f, exp_f,
- * planes_d, exp_d, first row}; a layer owns cout forward rows then cin_pad dgrad rows */
+ * weights: desc = device int64 [nlayers][10] = {w, cout, cin_real, cin_pad, planes_f, exp_f,
+ * planes_d, exp_d, first row, cout_pad}; a layer owns cout forward rows then cin_pad dgrad rows of
+ * K = 9 * cout_pad (k = tap * cout_pad + n, zero for n >= cout) */
 int srpde_prepare_weights_h3(const long long* desc, int nlayers, int total_rows, hipStream_t stream);
 /* dgrad (conv^T) with the BatchNorm (+ReLU) backward apply of the layer fused into the operand
  * transform: dy = gamma*invstd*(dz - m1 - xhat*m2) is formed per halo element from da (the BN
@@ -139,8 +140,9 @@ int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, cons
                         int cin_real, int accumulate, int n, int h, int w, int cout, int ksize, int dil,
                         void* workspace, size_t ws_bytes, hipStream_t stream);
 /* h3 weight gradient from pre-split operands: dyp = the xsplit_out of the dgrad call (sign -1,
- * [2][P][cout]) and xp = the xsplit_out of the forward call ([2][P][c0+c1]), with the max|.| words
- * those calls used.  No split work inside; workspace: srpde_conv_wgrad_h3p_workspace_size. */
+ * [2][P][cout]) or srpde_bn_bwd_apply_split's planes ([2][P][cout rounded up to 32]: cout = 16 reads
+ * 32-channel planes), and xp = the xsplit_out of the forward call ([2][P][c0+c1]), with the max|.|
+ * words those calls used.  No split work inside; workspace: srpde_conv_wgrad_h3p_workspace_size. */
 size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int cin, int ksize);
 int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* xp, int c0, const unsigned* amax0,
                          int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
@@ -219,8 +221,9 @@ int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, con
                          float* dbeta, float* dbias, unsigned* dy_amax, void* workspace, size_t ws_bytes,
                          hipStream_t stream);
 /* The BN (+ReLU) backward apply with srpde_bn_bwd_prepare's m1 / m2 (the expressions of
- * srpde_bn_relu_bwd) written as the h3 operand split of dy: planes = [2][P][C] fp16 hi / lo of
- * dy * 2^h3_exp(*dy_amax) (dy_amax = prepare's bound), the input of srpde_conv_fwd_h3_presplit and
+ * srpde_bn_relu_bwd) written as the h3 operand split of dy: planes = [2][P][Cp] fp16 hi / lo of
+ * dy * 2^h3_exp(*dy_amax) (dy_amax = prepare's bound), Cp = C rounded up to a multiple of 32 with
+ * channels C..Cp-1 zero (out_bn2's C = 16), the input of srpde_conv_fwd_h3_presplit (c = Cp) and
  * srpde_conv_wgrad_h3p.  No fp32 dy is written. */
 int srpde_bn_bwd_apply_split(const float* y, int ldy, const float* da, int ldda, const float* mean,
                              const float* invstd, const float* gamma, const float* beta, const float* m1,

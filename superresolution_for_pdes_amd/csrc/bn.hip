@@ -356,8 +356,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 // The BN (+ReLU) backward apply of bn_bwd_apply_kernel (the same expressions, with the float m1 / m2
 // of bn_bwd_coef_kernel) written as the h3 operand split of dy for the dgrad and weight gradient that
 // consume it (srpde_conv_fwd_h3_presplit, srpde_conv_wgrad_h3p): dy * s = hi + lo, hi / lo fp16 planes
-// [2][P][C], s = 2^h3_exp(dy_amax) from the rigorous bound of bn_bwd_coef_kernel -- no fp32 dy is
-// written and the dgrad does no split work.  Each thread owns one channel quad of a run of rows.
+// [2][P][Cp], s = 2^h3_exp(dy_amax) from the rigorous bound of bn_bwd_coef_kernel -- no fp32 dy is
+// written and the dgrad does no split work.  Cp = C rounded up to the 32-channel h3 chunk, channels
+// C..Cp-1 zero (out_bn2's 16 channels: its dgrad and weight gradient then run on the h3 kernels).
+// Each thread owns one channel quad of a run of rows.
 __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __restrict__ y, int ldy,
                                                                  const float* __restrict__ da, int ldda,
                                                                  const float* __restrict__ mean,
@@ -366,14 +368,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __
                                                                  const float* __restrict__ beta,
                                                                  const float* __restrict__ m1v,
                                                                  const float* __restrict__ m2v, long long P, int C,
-                                                                 int rows_per_blk, int relu,
+                                                                 int Cp, int rows_per_blk, int relu,
                                                                  const unsigned* __restrict__ dy_amax,
                                                                  _Float16* __restrict__ planes) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   int c4, r0, rs;
-  thread_rc(C, &c4, &r0, &rs);
-  if ((int)threadIdx.x >= (C >> 2) * rs) return;
+  thread_rc(Cp, &c4, &r0, &rs);
+  if ((int)threadIdx.x >= (Cp >> 2) * rs) return;
   const int c = c4 * 4;
+  const size_t plane = (size_t)P * Cp;
+  const long long pb = (long long)blockIdx.x * rows_per_blk;
+  const long long pe = min(P, pb + rows_per_blk);
+  if (c >= C) {   // the zero channels padding the planes to Cp (a multiple of 32, the h3 chunk)
+    const half4 z = {0, 0, 0, 0};
+    for (long long p = pb + r0; p < pe; p += rs) {
+      *reinterpret_cast<half4*>(planes + (size_t)p * Cp + c) = z;
+      *reinterpret_cast<half4*>(planes + plane + (size_t)p * Cp + c) = z;
+    }
+    return;
+  }
   const float4 mu = *reinterpret_cast<const float4*>(mean + c);
   const float4 is = *reinterpret_cast<const float4*>(invstd + c);
   const float4 g = *reinterpret_cast<const float4*>(gamma + c);
@@ -382,9 +395,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __
   const float4 m2 = *reinterpret_cast<const float4*>(m2v + c);
   const float4 k = make_float4(g.x * is.x, g.y * is.y, g.z * is.z, g.w * is.w);
   const float s = exp2i(h3_exp(*dy_amax));
-  const size_t plane = (size_t)P * C;
-  const long long pb = (long long)blockIdx.x * rows_per_blk;
-  const long long pe = min(P, pb + rows_per_blk);
   for (long long p = pb + r0; p < pe; p += rs) {
     const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
     const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
@@ -404,8 +414,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __
       hi[q] = h;
       lo[q] = (_Float16)(xs - (float)h);
     }
-    *reinterpret_cast<half4*>(planes + (size_t)p * C + c) = hi;
-    *reinterpret_cast<half4*>(planes + plane + (size_t)p * C + c) = lo;
+    *reinterpret_cast<half4*>(planes + (size_t)p * Cp + c) = hi;
+    *reinterpret_cast<half4*>(planes + plane + (size_t)p * Cp + c) = lo;
   }
 }
 
@@ -848,10 +858,11 @@ int srpde_bn_bwd_apply_split(const float* y, int ldy, const float* da, int ldda,
                   "srpde_bn_bwd_apply_split: null argument");
   SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ldda % 4 == 0 && aligned16(y) && aligned16(da) &&
                       aligned16(planes), "srpde_bn_bwd_apply_split: C / ld multiples of 4, 16-byte aligned");
+  const int Cp = (C + 31) / 32 * 32;
   int rpb;
-  const int nblk = bwd_blocks(P, C, &rpb);
+  const int nblk = bwd_blocks(P, Cp, &rpb);
   hipLaunchKernelGGL(bn_bwd_apply_split_kernel, dim3(nblk), dim3(256), 0, stream, y, ldy, da, ldda, mean, invstd,
-                     gamma, beta, m1, m2, P, C, rpb, flags & SRPDE_BN_RELU, dy_amax, static_cast<_Float16*>(planes));
+                     gamma, beta, m1, m2, P, C, Cp, rpb, flags & SRPDE_BN_RELU, dy_amax, static_cast<_Float16*>(planes));
   SRPDE_LAUNCH_CHECK("srpde_bn_bwd_apply_split");
   return 0;
 }

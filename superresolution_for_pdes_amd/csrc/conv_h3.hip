@@ -1133,16 +1133,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
   const int nsteps = (pend - pbeg + PS - 1) / PS;
   const int kc = p.ksize >> 1;
 
-  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.Cout * 2));
+  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.lddy * 2));
   const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
-  const size_t aplane = (size_t)p.P * p.Cout * 2, bplane = (size_t)p.P * p.Cin * 2;   // bytes
+  const size_t aplane = (size_t)p.P * p.lddy * 2, bplane = (size_t)p.P * p.Cin * 2;   // bytes
 
   // this wave's DMA ops: A op j is A instruction wave + j*NW, B op j is B instruction wave + j*NW
   // (past NA / NB: a spare zero-fill into the sink).  LDS destinations are wave-uniform; per lane: a
   // running byte offset (advanced by one stage of pixels per issue) and, for B, the image
   // coordinates of its pixel.
   const int psy = PS / p.W, psx = PS - psy * p.W;       // one stage of pixels in image rows / columns
-  const unsigned astep = (unsigned)(PS * p.Cout * 2), bstep = (unsigned)(PS * p.Cin * 2);
+  const unsigned astep = (unsigned)(PS * p.lddy * 2), bstep = (unsigned)(PS * p.Cin * 2);
   int a_row[DA];
   unsigned a_off[DA];
   bool a_ok[DA];
@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
     const int m = m0 + 8 * (slot ^ wx_swz<RA>(row));
     a_row[j] = row;
     a_ok[j] = m < p.Cout && wave + j * NW < NA;
-    a_off[j] = (unsigned)(pl * aplane + ((size_t)(pbeg + row) * p.Cout + m) * 2);
+    a_off[j] = (unsigned)(pl * aplane + ((size_t)(pbeg + row) * p.lddy + m) * 2);
   }
   int b_row[DB], b_dy[DB], b_dx[DB], b_y[DB], b_x[DB];
   unsigned b_off[DB];
@@ -1345,9 +1345,9 @@ __global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H
   if (threadIdx.x < 8)
     reinterpret_cast<float4*>(zrow + (threadIdx.x >> 2) * RING)[threadIdx.x & 3] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.Cout * 2));
+  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.lddy * 2));
   const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
-  const unsigned aplane = (unsigned)((size_t)p.P * p.Cout * 2), bplane = (unsigned)((size_t)p.P * p.Cin * 2);
+  const unsigned aplane = (unsigned)((size_t)p.P * p.lddy * 2), bplane = (unsigned)((size_t)p.P * p.Cin * 2);
 
   // B piece of rows [r, r + 16) of plane pl: lane -> row r + lane / 4, 16-B chunk lane % 4
   auto bpiece = [&](int r, int pl) {
@@ -1371,7 +1371,7 @@ __global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H
         const int row = byte / RA, sl = (byte - row * RA) >> 4;
         const int m = m0 + 8 * (sl ^ wx_swz<RA>(row));
         const bool ok = m < p.Cout && (full || p0 + row < pend);
-        dma16(rsa, ok ? pl * aplane + (unsigned)(((size_t)(p0 + row) * p.Cout + m) * 2) : OOB,
+        dma16(rsa, ok ? pl * aplane + (unsigned)(((size_t)(p0 + row) * p.lddy + m) * 2) : OOB,
               lds_addr_of(abuf + (slot * 2 + pl) * IMG_A + idx * 1024));
       } else {
         const int v = u - NA, pl = v / NBP, g = v - pl * NBP;
@@ -1538,9 +1538,11 @@ __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __re
 // forward rows  n in [0, Cout):   k = tap*Cin_pad + c  ->  W[n][c][tap]   (c >= Cin_real: 0)
 // dgrad rows    c in [0, Cin_pad): k = tap*Cout + n    ->  W[n][c][tap]
 // one wave per row: max|row| -> power-of-two scale -> hi / lo fp16 planes.  desc (device int64,
-// H3W_DESC per layer): w, cout, cin_real, cin_pad, planes_f, exp_f, planes_d, exp_d, row_begin
-// (rows of a layer: Cout forward rows then Cin_pad dgrad rows; planes_f / planes_d may be 0).
-constexpr int H3W_DESC = 9;
+// H3W_DESC per layer): w, cout, cin_real, cin_pad, planes_f, exp_f, planes_d, exp_d, row_begin,
+// cout_pad (rows of a layer: Cout forward rows then Cin_pad dgrad rows; planes_f / planes_d may be 0;
+// dgrad rows hold k = tap*cout_pad + n, zero for n >= cout: out_conv2's 16 channels as a 32-channel
+// dgrad input, matching srpde_bn_bwd_apply_split's padded planes).
+constexpr int H3W_DESC = 10;
 constexpr int H3W_TMAX = 512;   // dgrad rows of layers with cout <= this stage their source through LDS
 
 __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long* __restrict__ desc, int nlayers,
@@ -1553,14 +1555,14 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
   while (l + 1 < nlayers && desc[(l + 1) * H3W_DESC + 8] <= row) ++l;
   const long long* d = desc + l * H3W_DESC;
   const float* w = reinterpret_cast<const float*>(d[0]);
-  const int cout = (int)d[1], cin_real = (int)d[2], cin_pad = (int)d[3];
+  const int cout = (int)d[1], cin_real = (int)d[2], cin_pad = (int)d[3], cout_pad = (int)d[9];
   int r = row - (int)d[8];
   const bool fwd = r < cout;
   if (!fwd) r -= cout;
   _Float16* planes = reinterpret_cast<_Float16*>(fwd ? d[4] : d[6]);
   int* wexp = reinterpret_cast<int*>(fwd ? d[5] : d[7]);
   if (planes == nullptr) return;   // uniform over the block: its 4 rows are of one layer and kind
-  const int inner = fwd ? cin_pad : cout;          // k = tap * inner + i
+  const int inner = fwd ? cin_pad : cout_pad;      // k = tap * inner + i
   const int K = 9 * inner;
   const int rows = fwd ? cout : cin_pad;
   if (fwd && 4 * cin_real * 9 <= H3W_TMAX * 37 && cin_pad % 8 == 0) {
@@ -1597,20 +1599,20 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
     if (lane == 0) wexp[r] = e;
     return;
   }
-  if (!fwd && cout <= H3W_TMAX) {
+  if (!fwd && cout_pad <= H3W_TMAX) {
     // dgrad rows c0..c0+3 of this block: the source W[n][c0..c0+3][0..8] is 36 contiguous floats
     // per n -- staged through LDS once by the block, so HBM / L2 reads are row-contiguous (a wave
     // walking k = tap * cout + n directly reads one scattered 4-B word per cache line, 18 times)
     const int c0 = r - (threadIdx.x >> 6);
-    for (int e = threadIdx.x; e < cout * 36; e += 256) {
+    for (int e = threadIdx.x; e < cout_pad * 36; e += 256) {
       const int n = e / 36, q = e - n * 36;
-      T[n * 37 + q] = c0 + q / 9 < cin_real ? w[((size_t)n * cin_real + c0) * 9 + q] : 0.f;
+      T[n * 37 + q] = (n < cout && c0 + q / 9 < cin_real) ? w[((size_t)n * cin_real + c0) * 9 + q] : 0.f;
     }
     __syncthreads();
     const int cq = (threadIdx.x >> 6) * 9;   // this wave's row within the staged columns
     float m = 0.f;
     for (int k = lane; k < K; k += 64) {
-      const int tap = k / cout, n = k - tap * cout;
+      const int tap = k / cout_pad, n = k - tap * cout_pad;
       m = fmaxf(m, fabsf(T[n * 37 + cq + tap]));
     }
 #pragma unroll
@@ -1619,8 +1621,8 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
     const float sc = exp2i(e);
     _Float16* hi = planes + (size_t)r * K;
     _Float16* lo = planes + (size_t)rows * K + (size_t)r * K;
-    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k (same tap: cout % 8 == 0) per lane
-      const int tap = k0 / cout, n = k0 - tap * cout;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k (same tap: cout_pad % 8 == 0) per lane
+      const int tap = k0 / cout_pad, n = k0 - tap * cout_pad;
       half8 hv, lv;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -1638,7 +1640,7 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
   auto val = [&](int k) -> float {
     const int tap = k / inner, i = k - tap * inner;
     const int n = fwd ? r : i, c = fwd ? i : r;
-    return c < cin_real ? w[((size_t)n * cin_real + c) * 9 + tap] : 0.f;
+    return (c < cin_real && n < cout) ? w[((size_t)n * cin_real + c) * 9 + tap] : 0.f;
   };
   float m = 0.f;
   for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(val(k)));
@@ -1898,11 +1900,13 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
                          int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(dyp && xp && dw && workspace && amax_dy && amax0 && (c1 == 0 || amax1),
                   "srpde_conv_wgrad_h3p: null pointer");
-  SRPDE_CHECK_ARG(cout % 32 == 0 && (c0 + c1) % 8 == 0 && ksize == 3 && cin_real <= c0 + c1,
-                  "srpde_conv_wgrad_h3p: needs cout %% 32 == 0, cin %% 8 == 0, ksize 3 (cout=%d cin=%d)", cout, c0 + c1);
+  SRPDE_CHECK_ARG(cout % 16 == 0 && (c0 + c1) % 8 == 0 && ksize == 3 && cin_real <= c0 + c1,
+                  "srpde_conv_wgrad_h3p: needs cout %% 16 == 0, cin %% 8 == 0, ksize 3 (cout=%d cin=%d)", cout, c0 + c1);
   SRPDE_CHECK_ARG(aligned16(dyp) && aligned16(xp), "srpde_conv_wgrad_h3p: planes must be 16-byte aligned");
   WgradParams p;
-  p.dy = nullptr; p.lddy = cout; p.x0 = nullptr; p.c0 = c0; p.ldx0 = c0 + c1; p.x1 = nullptr; p.c1 = c1;
+  // dyp planes hold cout rounded up to the 32-channel chunk (srpde_bn_bwd_apply_split's padding); rows of
+  // dw: cout (the padded rows are zero-filled by the DMA range check, their products never stored)
+  p.dy = nullptr; p.lddy = (cout + 31) / 32 * 32; p.x0 = nullptr; p.c0 = c0; p.ldx0 = c0 + c1; p.x1 = nullptr; p.c1 = c1;
   p.ldx1 = c0 + c1;
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;

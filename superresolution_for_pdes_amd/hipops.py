@@ -77,7 +77,22 @@ def pack_conv_weights(w, cin_pad, want_fwd=True, want_dgrad=False):
             wf.h3 = split_weights_h3(wf, cout)
         if wd is not None and cin_pad % 16 == 0 and cout % 32 == 0:
             wd.h3 = split_weights_h3(wd, cin_pad)
+        elif wd is not None and cin_pad % 16 == 0 and cout % 16 == 0:
+            # out_conv2 (16 channels): the h3 dgrad reads dy as 32-channel planes (bn_bwd_apply_split pads
+            # them), so its split is of the [Cin][tap][32] packing with zero weights for the padded
+            # channels; the fp32 packing stays [Cin][tap][16] for the fp32 kernels on a 16-channel dy
+            wpad = torch.zeros(cpad32(cout), cin_real, kh, kh, device=w.device)
+            wpad[:cout] = w
+            wdp = empty(wpad.shape[0] * taps * cin_pad, device=w.device)
+            call("srpde_pack_conv_weights", wpad.data_ptr(), 0, wdp.data_ptr(), wpad.shape[0], cin_pad, cin_real, kh,
+                 stream_ptr())
+            wd.h3 = split_weights_h3(wdp, cin_pad)
     return wf, wd
+
+
+def cpad32(c):
+    """c rounded up to the 32-channel h3 chunk: the channel count of a dy split (bn_bwd_apply_split)."""
+    return -(-c // 32) * 32
 
 
 def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
@@ -167,7 +182,7 @@ def bn_bwd_apply_split(y, da, mean, invstd, gamma, beta, m1, m2, dy_amax, out=No
     py, ldy = _pl(y)
     pda, ldda = _pl(da)
     if out is None:
-        out = split_planes_buffer(P, C, y.device)
+        out = split_planes_buffer(P, cpad32(C), y.device)
     call("srpde_bn_bwd_apply_split", py, ldy, pda, ldda, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
          beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), P, C, BN_RELU if relu else 0, dy_amax.data_ptr(),
          out.data_ptr(), stream_ptr())
@@ -349,9 +364,11 @@ def split_planes_buffer(P, c, device):
 
 
 def conv_wgrad_h3p(dyp, xp, dw, n, h, w, ksize=3, dil=1, accumulate=False):
-    """Weight gradient from the stored splits: ``dyp`` from the dgrad conv_fwd(planes_out=...),
-    ``xp`` from the forward conv_fwd(planes_out=...), each carrying its max|.| word(s)."""
-    cout, cin = dyp.shape[2], xp.shape[2]
+    """Weight gradient from the stored splits: ``dyp`` from the dgrad conv_fwd(planes_out=...) or
+    bn_bwd_apply_split (its channels padded to 32: out_conv2's 16), ``xp`` from the forward
+    conv_fwd(planes_out=...), each carrying its max|.| word(s); ``dw`` [Cout, Cin, k, k]."""
+    cout, cin = dw.shape[0], xp.shape[2]
+    assert dyp.shape[2] == cpad32(cout), "dy planes must hold cout rounded up to 32 channels"
     ax = xp._srpde_amax
     a0, a1 = (ax, None) if not isinstance(ax, tuple) else ax
     c1 = 0 if a1 is None else cin - xp._srpde_c0

@@ -109,15 +109,16 @@ def prepare_h3_weights(m):
             if cin % 32 == 0 and cout % 16 == 0:
                 pf = torch.empty(2, cout * 9 * cin, dtype=torch.float16, device=dev)
                 ef = torch.empty(cout, dtype=torch.int32, device=dev)
-            if cout % 32 == 0 and cin % 16 == 0:
-                pd = torch.empty(2, cin * 9 * cout, dtype=torch.float16, device=dev)
+            if cout % 16 == 0 and cin % 16 == 0:   # dgrad rows k = tap * cpad32(cout) + n (out_conv2: 16 -> 32)
+                pd = torch.empty(2, cin * 9 * H.cpad32(cout), dtype=torch.float16, device=dev)
                 ed = torch.empty(cin, dtype=torch.int32, device=dev)
             c._srpde_h3f = _Planes(pf, ef) if pf is not None else None
             c._srpde_h3d = _Planes(pd, ed) if pd is not None else None
             if pf is None and pd is None:
                 continue
             # a layer owns cout forward rows then cin dgrad rows (rows of a missing packing idle)
-            desc.append([c.weight.data_ptr(), cout, cin, cin, H._p(pf), H._p(ef), H._p(pd), H._p(ed), rows])
+            desc.append([c.weight.data_ptr(), cout, cin, cin, H._p(pf), H._p(ef), H._p(pd), H._p(ed), rows,
+                         H.cpad32(cout)])
             rows += cout + cin
             keep += [t for t in (pf, ef, pd, ed) if t is not None]
         cache = (sig, torch.tensor(desc, dtype=torch.int64, device=dev), len(desc), rows, keep)
@@ -169,17 +170,24 @@ def _fwd_weights(conv, cin, c0, c1, w, dil):
     return H.pack_conv_weights(conv.weight, cin)[0]
 
 
-def _dgrad_weights(conv, cin, w, dil):
+def _dgrad_weights(conv, cin, w, dil, cdy=None):
+    """The dgrad's packed weights for a dy operand of ``cdy`` channels (default: the layer's output
+    channels).  The cached h3 planes hold cpad32(cout) dy channels (out_conv2: 16 padded to 32, the
+    planes of bn_bwd_apply_split); a 16-channel fp32 dy takes the fp32 packing instead."""
+    cdy = conv.out_channels if cdy is None else cdy
     wp = getattr(conv, "_srpde_h3d", None)
-    if wp is not None and H.h3_capable(conv.out_channels, 0, cin, w, dil):
+    if wp is not None and cdy == H.cpad32(conv.out_channels) and H.h3_capable(cdy, 0, cin, w, dil):
         _h3w_ready(conv.weight.device)
         return wp
     return H.pack_conv_weights(conv.weight, cin, want_fwd=False, want_dgrad=True)[1]
 
 
 def _splits_both_ways(c0, c1, cout, w, dil):
-    """The layer's forward and dgrad both run on h3, so its weight gradient reads stored splits."""
-    return H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(cout, 0, c0 + c1, w, dil)
+    """The layer's forward and dgrad both run on h3, so its weight gradient reads stored splits (the
+    dgrad reads dy as planes of cpad32(cout) channels: out_conv2's 16 padded to 32, which only the
+    pre-split BN backward apply produces)."""
+    return (H.h3_capable(c0, c1, cout, w, dil) and H.h3_capable(H.cpad32(cout), 0, c0 + c1, w, dil)
+            and (cout % 32 == 0 or _PRESPLIT_BWD))
 
 
 def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, activate=True, pool=False, att=None,
@@ -423,7 +431,8 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         else:
             wq.submit(fn, keep)
         return None if out_part is None else (out_part, dx_max)
-    if (_PRESPLIT_BWD and train and dx is not None and xp is not None and H.h3_capable(cout, 0, cin, w, dil)):
+    if (_PRESPLIT_BWD and train and dx is not None and xp is not None
+            and H.h3_capable(H.cpad32(cout), 0, cin, w, dil)):
         # the BN backward apply writes dy as its h3 split (scale from bn_bwd_prepare's rigorous bound);
         # the dgrad reads the fp16 pieces straight into its operand tiles and the weight gradient
         # reads the same planes: no fp32 dy, no split work or split store in the dgrad
@@ -432,14 +441,14 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         dyp = H.bn_bwd_apply_split(y, da, mean, invstd, bn.weight, bn.bias, m1, m2, dyw)
         if DEBUG_TAPS is not None:
             _tap("dyp:" + getattr(conv, "_srpde_name", "?"), dyp)
-        wd = _dgrad_weights(conv, cin, w, dil)
+        wd = _dgrad_weights(conv, cin, w, dil, cdy=H.cpad32(cout))
         bn_bwd, dx_max = None, None
         if below is not None and not dx_accumulate and _FUSE_BN_BWD:
             bnb, sb = below
             out_part = H.bn_bwd_partials(n, h, w, cin, y.device)
             bn_bwd = (sb[2], sb[3], sb[4], bnb.weight, bnb.bias, out_part)
             if _FUSE_BN_APPLY:   # max|dx| slots for the layer below's BN backward bound
-                dx_max = H.out_max_slots(n, h, w, cout, cin, dil, y.device)
+                dx_max = H.out_max_slots(n, h, w, H.cpad32(cout), cin, dil, y.device)
         H.conv_fwd_presplit(dyp, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, bn_bwd=bn_bwd,
                             out_max=dx_max)
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
@@ -624,12 +633,20 @@ def unet_forward(m, x, training, save=False):
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
     # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)
     if _FUSE_D1 and _fuse_pair(m.out_conv1, training, w, 1):
-        (d1y, d1aff), S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots, activate=False)
-        o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1y, None, n, h, w, training, 1, slots, in_affine=d1aff)
+        (d1, d1aff), S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots, activate=False)
     else:
         d1, S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots)
-        o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots)
-    o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots)
+        d1aff = None
+    # out_conv1 -> BN -> ReLU -> out_conv2 as a ConvBlock pair: out_bn1's BN + ReLU applied inside
+    # out_conv2's input transform (train mode; out_conv2's dgrad and weight gradient run on h3 from
+    # 32-channel-padded dy planes, so it keeps its input split)
+    if _fuse_pair(m.out_conv2, training, w, 1):
+        (o1, o1aff), S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots, in_affine=d1aff,
+                                       activate=False)
+        o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots, in_affine=o1aff)
+    else:
+        o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots, in_affine=d1aff)
+        o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots)
     out = H.head_fwd(o2, m.final.weight, m.final.bias, x, n, hw1)
     if not save:
         return out.view(n, 1, h, w), None

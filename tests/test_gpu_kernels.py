@@ -385,11 +385,14 @@ def test_amax_words_match_outputs():
 @pytest.mark.parametrize("n,cin0,cin1,cout,h,dil", [
     (4, 512, 0, 512, 10, 2), (3, 512, 256, 256, 10, 1), (2, 256, 128, 128, 20, 1), (2, 128, 64, 64, 40, 1),
     (2, 64, 0, 32, 40, 1), (3, 64, 32, 96, 7, 2), (5, 128, 0, 128, 6, 1), (3, 64, 0, 64, 40, 1),
-    (3, 64, 0, 64, 13, 2), (2, 64, 32, 32, 20, 1)])
+    (3, 64, 0, 64, 13, 2), (2, 64, 32, 32, 20, 1), (3, 32, 0, 16, 40, 1), (2, 32, 0, 16, 9, 1)])
 def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
     """h3p: the forward and dgrad kernels store their operand splits (planes_out) and the weight
     gradient consumes them (no split work of its own).  Against fp64: within 3x the fp32-MFMA
-    kernel's error (+1e-7) and < 1e-6 relative L2; ragged P, Cout not a tile multiple, dil 2 on 7x7."""
+    kernel's error (+1e-7) and < 1e-6 relative L2; ragged P, Cout not a tile multiple, dil 2 on 7x7.
+    Cout = 16 (out_conv2): dy enters as 32-channel planes (zero channels 16..31, as
+    srpde_bn_bwd_apply_split pads them) against the zero-padded dgrad weights; the dgrad is checked
+    too."""
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator().manual_seed(n * 31 + cout + cin0)
     cin = cin0 + cin1
@@ -402,13 +405,18 @@ def test_conv_wgrad_from_stored_splits(n, cin0, cin1, cout, h, dil, conv_math):
     dyr = rows(dy.float()).to(DEV)
     P = n * h * h
     H.set_conv_math("h3")
-    assert H.h3_capable(cin0, cin1, cout, h, dil) and H.h3_capable(cout, 0, cin, h, dil)
+    cp = H.cpad32(cout)
+    assert H.h3_capable(cin0, cin1, cout, h, dil) and H.h3_capable(cp, 0, cin, h, dil)
     wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
-    xp, dyp = H.split_planes_buffer(P, cin, DEV), H.split_planes_buffer(P, cout, DEV)
+    xp, dyp = H.split_planes_buffer(P, cin, DEV), H.split_planes_buffer(P, cp, DEV)
     y = H.empty(P, cout, device=DEV)
     H.conv_fwd(x0, x1, wf, None, y, n, h, h, cout, 3, dil, 1, False, None, xp)
     dx = H.empty(P, cin, device=DEV)
-    H.conv_fwd(dyr, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None, dyp)
+    dyin = dyr if cp == cout else torch.cat([dyr, torch.zeros(P, cp - cout, device=DEV)], 1)
+    H.conv_fwd(dyin, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None, dyp)
+    if cp != cout:
+        dx64 = torch.nn.grad.conv2d_input(x.shape, wt, dy, padding=dil, dilation=dil)
+        assert rel(dx.view(n, h, h, cin).permute(0, 3, 1, 2).cpu(), dx64) < 1e-6
     dw = torch.empty(cout, cin, 3, 3, device=DEV)
     H.conv_wgrad_h3p(dyp, xp, dw, n, h, h, 3, dil)
     H.set_conv_math("f32")
@@ -608,10 +616,11 @@ def test_conv_presplit_equals_inline_split(n, c, cout, hw, dil, sign):
         assert torch.equal(a, b_), name
 
 
-@pytest.mark.parametrize("P,C", [(1024 * 100, 256), (3 * 1600, 64), (777, 32)])
+@pytest.mark.parametrize("P,C", [(1024 * 100, 256), (3 * 1600, 64), (777, 32), (2 * 1600 + 5, 16)])
 def test_bn_bwd_apply_split_matches_fp32_apply(P, C):
     """srpde_bn_bwd_apply_split's planes hold bn_relu_bwd's dy: (hi + lo) / s equals the fp32 apply
-    to the split's representation error (2^-22 of the scale), and the scale word is a bound."""
+    to the split's representation error (2^-22 of the scale), and the scale word is a bound.  C = 16
+    (out_bn2): the planes are 32 channels wide, channels 16..31 exactly zero."""
     from superresolution_for_pdes_amd import hipops as H
     g = torch.Generator(device=DEV).manual_seed(P + C)
     y = torch.randn(P, C, device=DEV, generator=g) * 2 + 0.5
@@ -630,6 +639,8 @@ def test_bn_bwd_apply_split_matches_fp32_apply(P, C):
     assert bound >= float(dy.abs().max())
     e = int(np.floor(np.log2(bound))) + 1           # h3_exp: max < 2^e -> scale 2^(15 - e)
     s = 2.0 ** (15 - e)
-    deq = (planes[0].double() + planes[1].double()) / s
+    assert planes.shape == (2, P, H.cpad32(C))
+    assert not bool(planes[:, :, C:].any())
+    deq = (planes[0, :, :C].double() + planes[1, :, :C].double()) / s
     err = float((deq - dy.double()).abs().max())
     assert err <= 2.0 ** -22 * (2.0 ** 15 / s) + 1e-30, (err, bound)

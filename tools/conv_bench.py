@@ -71,22 +71,29 @@ def main():
         dx = torch.empty(P, cin, device=dev)
         dw = torch.empty_like(w)
         line = f"{name:11s}"
-        # h3 as training runs it: forward and dgrad store their operand splits, wgrad reads them
-        h3p = H.conv_math() == "h3" and H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cout, 0, cin, hw, dil)
+        # h3 as training runs it: the forward stores its input split, the dgrad reads dy as split planes
+        # (bn_bwd_apply_split's output, 32-channel padded for out_conv2) and the wgrad reads both
+        cp = H.cpad32(cout)
+        h3p = H.conv_math() == "h3" and H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cp, 0, cin, hw, dil)
         xp = H.split_planes_buffer(P, cin, dev) if h3p else None
-        dyp = H.split_planes_buffer(P, cout, dev) if h3p else None
+        dyp = H.split_planes_buffer(P, cp, dev) if h3p else None
         if h3p:
+            dyin = dy if cp == cout else torch.cat([dy, torch.zeros(P, cp - cout, device=dev)], 1)
+            dyin._srpde_amax = dy._srpde_amax
             H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
-            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
+            H.conv_fwd(dyin, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
             seq.extend([(name, "setup"), (name, "setup")])
         for kind in args.only.split(","):
             tag = (name, kind)
             if kind == "fwd":
                 ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp),
                             args.iters, seq, tag)
+            elif kind == "dgrad" and h3p:
+                ms = timeit(lambda: H.conv_fwd_presplit(dyp, wd, None, dx, n, hw, hw, cin, 3, dil, -1), args.iters,
+                            seq, tag)
             elif kind == "dgrad":
-                ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp),
-                            args.iters, seq, tag)
+                ms = timeit(lambda: H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1), args.iters, seq,
+                            tag)
             elif h3p:
                 ms = timeit(lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, hw, hw, 3, dil), args.iters, seq, tag)
             else:
@@ -98,8 +105,8 @@ def main():
             wb = 4 * cout * cin * 9
             if kind == "fwd":
                 ab = 4 * P * cin + wb + 4 * P * cout + (4 * P * cin if h3p else 0)
-            elif kind == "dgrad":
-                ab = 4 * P * cout + wb + 4 * P * cin + (4 * P * cout if h3p else 0)
+            elif kind == "dgrad":   # h3: dy arrives as its stored split (4 B/elem), nothing else stored
+                ab = 4 * P * cout + wb + 4 * P * cin
             else:
                 ab = 4 * P * (cin + cout) + wb
             rows.append({"layer": name, "pass": kind, "ms": round(ms, 4), "tflops": round(tf, 1), "flop": flops,
