@@ -7,9 +7,10 @@
 //           (-L) u = -f / theta
 // which is solved here by CG on a matrix-free stencil, for B independent problems at once.
 //
-// * n <= 128  : one workgroup per problem; the search direction p (with its zero ghost
-//               ring) lives in LDS, x / r / q stay in registers (NPT points per lane);
-//               3 barriers per iteration, deterministic fixed-order block reductions.
+// * n <= 128  : one workgroup per problem, Chronopoulos-Gear CG: the residual r (with its zero
+//               ghost ring) lives in LDS, x / r / p / s / w stay in registers (NPT points per
+//               lane); 2 barriers per iteration (one fused two-value reduction on the DPP network),
+//               deterministic fixed-order block reductions.
 // * n  > 128  : grid CG, 2 launches per iteration (A: beta, p <- r + beta p, q = A p, <p,q>
 //               partials;  B: alpha, x += alpha p, r -= alpha A p, <r,r> partials); every
 //               block re-reduces the previous launch's partials in the same order, so all
@@ -23,17 +24,44 @@ namespace srpde {
 
 constexpr int CG_MAXT = 1024;
 
-__device__ __forceinline__ double block_sum_uniform(double v, double* slots) {
-  // every thread returns the same value (fixed reduction order)
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  if ((threadIdx.x & 63) == 0) slots[w] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int k = 0; k < nw; ++k) s += slots[k];
-  return s;
+// fp64 wave reduction on the DPP network (no LDS round trips): butterfly within quads, rotations
+// within 16-lane rows, then the GFX9 row broadcasts fold the four rows into lane 63, read back as a
+// wave-uniform value.  Fixed order: every wave of every block sums identically.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, ROWS, 0xf, false),
+                          __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x124, 0xf>(v);   // row_ror:4
+  v += dpp_f64<0x128, 0xf>(v);   // row_ror:8   (every lane: its row's sum)
+  v += dpp_f64<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3 (lane 63: the wave's sum)
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63), hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
 }
 
+// (a, b) summed over the block, the same values in every thread: per-wave DPP sums into `slots`
+// ([2][16] doubles), one barrier, then each wave re-reduces the nw wave sums in lane order.
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* slots) {
+  a = wave_sum_dpp(a);
+  b = wave_sum_dpp(b);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
+  if (lane == 0) { slots[w] = a; slots[16 + w] = b; }
+  __syncthreads();
+  a = wave_sum_dpp(lane < nw ? slots[lane] : 0.0);
+  b = wave_sum_dpp(lane < nw ? slots[16 + lane] : 0.0);
+}
+
+// Chronopoulos-Gear CG (the same Krylov iterates as textbook CG, rearranged so that both inner
+// products of an iteration, gamma = <r, r> and delta = <A r, r>, come from ONE block reduction):
+//   w = A r;  gamma, delta;  beta = gamma / gamma_old;  alpha = gamma / (delta - beta * gamma / alpha_old)
+//   p = r + beta p;  s = w + beta s  (= A p);  x += alpha p;  r -= alpha s
+// Two barriers per iteration (r visible for the stencil; the reduction) against textbook CG's three;
+// r lives in LDS with its zero ghost ring, x / r / p / s / w in registers (NPT points per lane).
 template <int NPT>
 __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restrict__ f,
                                                          const double* __restrict__ theta, double* __restrict__ u,
@@ -41,21 +69,19 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
                                                          double* __restrict__ resid) {
   extern __shared__ double sp[];
   const int N2 = n * n, ld = n + 2;
-  double* pl = sp;                       // (n+2)^2
-  double* slotA = sp + ld * ld;          // 16
-  double* slotB = slotA + 16;            // 16
+  double* rl = sp;                       // (n+2)^2
+  double* slots = sp + ld * ld;          // [2][2][16]: reduction parity x (gamma, delta) x wave
   const size_t off = (size_t)blockIdx.x * N2;
   const double inv_h2 = (double)(n - 1) * (double)(n - 1);
   const int T = blockDim.x;
 
-  for (int e = threadIdx.x; e < ld * ld; e += T) pl[e] = 0.0;
-  double x[NPT], r[NPT], p[NPT], q[NPT];
+  for (int e = threadIdx.x; e < ld * ld; e += T) rl[e] = 0.0;
+  double x[NPT], r[NPT], p[NPT], s[NPT], w[NPT];
   int li[NPT];
-  double rr_l = 0.0;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int i = threadIdx.x + k * T;
-    x[k] = 0.0; q[k] = 0.0;
+    x[k] = 0.0; p[k] = 0.0; s[k] = 0.0; w[k] = 0.0;
     if (i < N2) {
       const int yy = i / n, xx = i - yy * n;
       li[k] = (yy + 1) * ld + xx + 1;
@@ -64,45 +90,56 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
       li[k] = -1;
       r[k] = 0.0;
     }
-    p[k] = r[k];
-    rr_l += r[k] * r[k];
   }
   __syncthreads();  // ghost ring zeroed before interior writes
-#pragma unroll
-  for (int k = 0; k < NPT; ++k)
-    if (li[k] >= 0) pl[li[k]] = p[k];
-  double rr = block_sum_uniform(rr_l, slotB);  // includes a barrier: p visible
-  const double stop = rtol * rtol * rr;
-  int it = 0;
-  while (rr > stop && it < maxit) {
-    double pq_l = 0.0;
+  int par = 0;
+  // w = A r and (gamma, delta) of the current r (r already written to rl, one barrier passed)
+  auto apply_reduce = [&](double& gamma, double& delta) {
+    double g = 0.0, d = 0.0;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       if (li[k] >= 0) {
         const int c = li[k];
-        q[k] = (4.0 * p[k] - pl[c - 1] - pl[c + 1] - pl[c - ld] - pl[c + ld]) * inv_h2;
-        pq_l += p[k] * q[k];
+        w[k] = (4.0 * r[k] - rl[c - 1] - rl[c + 1] - rl[c - ld] - rl[c + ld]) * inv_h2;
+        g += r[k] * r[k];
+        d += w[k] * r[k];
       }
+      // two points' neighbour loads in flight at a time: hoisting all of them spills the five
+      // register vectors (the block's other waves hide the LDS latency)
+      if (k & 1) __builtin_amdgcn_sched_barrier(0);
     }
-    const double pq = block_sum_uniform(pq_l, slotA);
-    const double alpha = rr / pq;
-    double rr_n = 0.0;
+    block_sum2(g, d, slots + 32 * par);
+    par ^= 1;
+    gamma = g;
+    delta = d;
+  };
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      x[k] += alpha * p[k];
-      r[k] -= alpha * q[k];
-      rr_n += r[k] * r[k];
-    }
-    const double rrn = block_sum_uniform(rr_n, slotB);
-    const double beta = rrn / rr;
-    rr = rrn;
+  for (int k = 0; k < NPT; ++k)
+    if (li[k] >= 0) rl[li[k]] = r[k];
+  __syncthreads();
+  double gamma, delta;
+  apply_reduce(gamma, delta);
+  const double stop = rtol * rtol * gamma;
+  const double g0 = gamma;
+  double alpha = gamma / delta, beta = 0.0;
+  int it = 0;
+  while (gamma > stop && it < maxit) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       p[k] = r[k] + beta * p[k];
-      if (li[k] >= 0) pl[li[k]] = p[k];
+      s[k] = w[k] + beta * s[k];
+      x[k] += alpha * p[k];
+      r[k] -= alpha * s[k];
+      if (li[k] >= 0) rl[li[k]] = r[k];
     }
-    __syncthreads();
     ++it;
+    __syncthreads();   // r visible to the neighbours' stencils (all reads of the old r are done:
+                       // they precede the reduction barrier every thread has passed)
+    double gn, dn;
+    apply_reduce(gn, dn);
+    beta = gn / gamma;
+    alpha = gn / (dn - beta * gn / alpha);
+    gamma = gn;
   }
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -111,7 +148,7 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
   }
   if (threadIdx.x == 0) {
     if (iters) iters[blockIdx.x] = it;
-    if (resid) resid[blockIdx.x] = sqrt(rr / (stop > 0.0 ? stop / (rtol * rtol) : 1.0));
+    if (resid) resid[blockIdx.x] = sqrt(gamma / (g0 > 0.0 ? g0 : 1.0));
   }
 }
 
@@ -125,7 +162,8 @@ struct GridCG {
   double rtol;
 };
 
-constexpr int GCG_T = 256, GCG_NPT = 4, GCG_PTS = GCG_T * GCG_NPT;
+// 512 threads x 4 points: 2048 points per block (a 640^2 problem is 200 blocks; 143 VGPRs, no spill)
+constexpr int GCG_T = 512, GCG_NPT = 4, GCG_PTS = GCG_T * GCG_NPT;
 
 __device__ __forceinline__ double sum_parts(const double* part, int nb, double* sh) {
   double s = 0.0;
@@ -260,29 +298,76 @@ __global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restr
 // The same iteration as gcg_a / gcg_b (same per-block partial sums, same re-reduction order, same
 // expressions: bit-identical iterates) with the two launch boundaries of an iteration replaced by
 // two grid barriers, so the solve is one launch and the host never polls.  Every block owns GCG_PTS
-// points of one problem; x, r, p and q of its points stay in registers, r and p are also written to
-// HBM for the neighbours' stencils (p double-buffered by parity).  All blocks co-reside
+// consecutive points of one problem; x, r, p and q of its points stay in registers, the new p also in
+// LDS for the in-block stencil, and only the first / last n points' r and p (p double-buffered by
+// parity) go to global memory for the neighbouring blocks.  All blocks co-reside
 // (hipLaunchCooperativeKernel checks it); a problem that converges keeps its blocks at the barriers
 // until every problem of the launch has (ctl[0] counts them), and every block leaves the loop at the
 // same barrier.  A barrier that waits longer than ~1 s sets ctl[1] (abort), which releases every
 // waiter: the launch then ends with iters = -1 instead of hanging the queue.
+// The grid barrier is a two-level tree of monotonic arrival counters (zeroed before the launch):
+// bar[1 + g] counts the arrivals of block group g (COOP_GRP consecutive blocks), the last arriver of
+// a group bumps bar[0], and every block waits for bar[0] to reach epoch x groups -- COOP_GRP + groups
+// serialised atomics per barrier instead of one per block on a single address.
+constexpr int COOP_GRP = 16;
 struct GridCoop {
   double *r, *p0, *p1;          // [B][N2]
   double *rrp, *pqp;            // [B][nb] per-block partials
-  unsigned long long* bar;      // barrier arrivals (monotonic; zeroed before the launch)
+  unsigned long long* bar;      // [0] groups arrived, [1 + g] blocks of group g arrived
   unsigned* ctl;                // [0] problems converged, [1] abort
-  int n, nb, B;
+  int n, nb, B, ngrp;
   double rtol;
 };
 
-__device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long target, int* sflag) {
+// Everything one block writes and another reads (r, p, the partials) goes through agent-scope
+// relaxed atomic stores / loads, which bypass the XCD-private L2 (the sc1 bit) -- so a barrier needs
+// no cache maintenance: each thread drains its stores (vmcnt) before the block arrives, and the loads
+// after the barrier fetch from the coherent level.  (An agent-scope fence per block and barrier
+// instead writes back and invalidates the whole L2 of its XCD: measured 14x slower at n = 640.)
+__device__ __forceinline__ void st_ag(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_ag(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double sum_parts_ag(const double* part, int nb, double* sh) {
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) s += ld_ag(part + k);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double t = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ void write_part_ag(double v, double* sh, double* dst) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();   // release this block's r / p / partial stores to the other XCDs
-    __hip_atomic_fetch_add(g.bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    double t = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+    st_ag(dst, t);
+  }
+}
+
+// epoch `epoch` (1, 2, ...) of the grid barrier; false on abort (a wait past ~1 s)
+__device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long epoch, int* sflag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int grp = blockIdx.x / COOP_GRP;
+    const unsigned long long gsz = min(COOP_GRP, (int)gridDim.x - grp * COOP_GRP);
+    const unsigned long long old = __hip_atomic_fetch_add(g.bar + 1 + grp, 1ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == epoch * gsz) __hip_atomic_fetch_add(g.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = epoch * (unsigned long long)g.ngrp;
     int ab = 0;
     for (unsigned spins = 0;; ++spins) {
-      if (__hip_atomic_load(g.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(g.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
       if (__hip_atomic_load(g.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
       if (spins > (1u << 24)) {
         __hip_atomic_store(g.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -291,10 +376,10 @@ __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long 
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __threadfence();   // acquire
     *sflag = ab;
   }
   __syncthreads();
+  asm volatile("" ::: "memory");   // no load of the next phase is hoisted above the barrier
   return *sflag == 0;
 }
 
@@ -303,10 +388,14 @@ __global__ __launch_bounds__(GCG_T) void gcg_coop_kernel(const double* __restric
                                                          int* __restrict__ iters, GridCoop g, int maxit) {
   __shared__ double sh[8];
   __shared__ int sflag;
+  __shared__ double pl[GCG_PTS];   // this block's new search direction (the in-block stencil reads)
   const int b = blockIdx.x / g.nb, j = blockIdx.x - b * g.nb;
   const int n = g.n, N2 = n * n;
   const size_t off = (size_t)b * N2;
-  const unsigned long long nblk = gridDim.x;
+  const int lo = j * GCG_PTS, hi = min(N2, lo + GCG_PTS);
+  // r and p of the block's first / last n points are what the neighbouring blocks' stencils read:
+  // only those are written to (and read from) the coherent global copies
+  auto edge = [&](int i) { return i < lo + n || i >= hi - n; };
   unsigned long long epoch = 0;
   const double inv_h2 = (double)(n - 1) * (double)(n - 1);
   const double* rpart = g.rrp + (size_t)b * g.nb;
@@ -316,18 +405,20 @@ __global__ __launch_bounds__(GCG_T) void gcg_coop_kernel(const double* __restric
   double s = 0.0;
 #pragma unroll
   for (int k = 0; k < GCG_NPT; ++k) {
-    const int i = j * GCG_PTS + k * GCG_T + threadIdx.x;
+    const int i = lo + k * GCG_T + threadIdx.x;
     x[k] = 0.0; p[k] = 0.0; q[k] = 0.0; r[k] = 0.0;
-    if (i < N2) {
+    if (i < hi) {
       r[k] = -f[off + i] / theta[off + i];
-      rv[i] = r[k];
-      g.p0[off + i] = 0.0;
+      if (edge(i)) {
+        st_ag(rv + i, r[k]);
+        st_ag(g.p0 + off + i, 0.0);
+      }
       s += r[k] * r[k];
     }
   }
-  write_part(s, sh, g.rrp + (size_t)b * g.nb + j);
-  bool ok = coop_sync(g, ++epoch * nblk, &sflag);
-  const double bb = sum_parts(rpart, g.nb, sh);
+  write_part_ag(s, sh, g.rrp + (size_t)b * g.nb + j);
+  bool ok = coop_sync(g, ++epoch, &sflag);
+  const double bb = sum_parts_ag(rpart, g.nb, sh);
   double rr = bb, rr_old = 1.0;
   bool done = false;
   int it_done = maxit;
@@ -342,57 +433,67 @@ __global__ __launch_bounds__(GCG_T) void gcg_coop_kernel(const double* __restric
       const double beta = k == 0 ? 0.0 : rr / rr_old;
       const double* po = ((k & 1) ? g.p1 : g.p0) + off;
       double* pn = ((k & 1) ? g.p0 : g.p1) + off;
+#pragma unroll
+      for (int kk = 0; kk < GCG_NPT; ++kk) {
+        const int i = lo + kk * GCG_T + threadIdx.x;
+        if (i < hi) {
+          const double pc = r[kk] + beta * p[kk];
+          p[kk] = pc;
+          pl[i - lo] = pc;
+          if (edge(i)) st_ag(pn + i, pc);
+        }
+      }
+      __syncthreads();
+      // a neighbour in another block: its p = r + beta p_old from that block's stored copies (the
+      // same expression on the same values, so the same bits as its owner holds)
+      auto pv = [&](int jj) { return (jj >= lo && jj < hi) ? pl[jj - lo] : ld_ag(rv + jj) + beta * ld_ag(po + jj); };
       s = 0.0;
 #pragma unroll
       for (int kk = 0; kk < GCG_NPT; ++kk) {
-        const int i = j * GCG_PTS + kk * GCG_T + threadIdx.x;
-        if (i < N2) {
+        const int i = lo + kk * GCG_T + threadIdx.x;
+        if (i < hi) {
           const int yy = i / n, xx = i - yy * n;
-          auto pv = [&](int jj) { return rv[jj] + beta * po[jj]; };
-          const double pc = r[kk] + beta * p[kk];
           double nb = 0.0;
           if (xx > 0) nb += pv(i - 1);
           if (xx < n - 1) nb += pv(i + 1);
           if (yy > 0) nb += pv(i - n);
           if (yy < n - 1) nb += pv(i + n);
-          q[kk] = (4.0 * pc - nb) * inv_h2;
-          p[kk] = pc;
-          pn[i] = pc;
-          s += pc * q[kk];
+          q[kk] = (4.0 * p[kk] - nb) * inv_h2;
+          s += p[kk] * q[kk];
         }
       }
-      write_part(s, sh, g.pqp + (size_t)b * g.nb + j);
+      write_part_ag(s, sh, g.pqp + (size_t)b * g.nb + j);
     }
-    ok = coop_sync(g, ++epoch * nblk, &sflag);
+    ok = coop_sync(g, ++epoch, &sflag);
     // every increment of ctl[0] precedes this barrier and the next one follows these reads: all
     // blocks read the same count and leave together
     if (!ok || __hip_atomic_load(g.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)g.B) break;
     // B (gcg_b_kernel): alpha, x += alpha p, r -= alpha q, <r, r> partials
     if (!done) {
-      const double alpha = rr / sum_parts(qpart, g.nb, sh);
+      const double alpha = rr / sum_parts_ag(qpart, g.nb, sh);
       s = 0.0;
 #pragma unroll
       for (int kk = 0; kk < GCG_NPT; ++kk) {
-        const int i = j * GCG_PTS + kk * GCG_T + threadIdx.x;
-        if (i < N2) {
+        const int i = lo + kk * GCG_T + threadIdx.x;
+        if (i < hi) {
           x[kk] += alpha * p[kk];
           r[kk] = r[kk] - alpha * q[kk];
-          rv[i] = r[kk];
+          if (edge(i)) st_ag(rv + i, r[kk]);
           s += r[kk] * r[kk];
         }
       }
-      write_part(s, sh, g.rrp + (size_t)b * g.nb + j);
+      write_part_ag(s, sh, g.rrp + (size_t)b * g.nb + j);
     }
-    ok = coop_sync(g, ++epoch * nblk, &sflag);
+    ok = coop_sync(g, ++epoch, &sflag);
     if (!done) {
       rr_old = rr;
-      rr = sum_parts(rpart, g.nb, sh);
+      rr = sum_parts_ag(rpart, g.nb, sh);
     }
   }
 #pragma unroll
   for (int k = 0; k < GCG_NPT; ++k) {
-    const int i = j * GCG_PTS + k * GCG_T + threadIdx.x;
-    if (i < N2) u[off + i] = x[k];
+    const int i = lo + k * GCG_T + threadIdx.x;
+    if (i < hi) u[off + i] = x[k];
   }
   if (j == 0 && threadIdx.x == 0 && iters) iters[b] = ok ? it_done : -1;
 }
@@ -416,13 +517,25 @@ static GridCG carve(void* ws, int B, int n) {
   return g;
 }
 
+static size_t coop_ctl_bytes(int B, int n) {   // the cooperative launches' barrier counters + ctl words
+  const size_t nb = ((size_t)n * n + GCG_PTS - 1) / GCG_PTS;
+  return ((B * nb + COOP_GRP - 1) / COOP_GRP + 2) * sizeof(unsigned long long);
+}
 static size_t grid_ws_bytes(int B, int n) {
   const size_t N2 = (size_t)n * n;
   const size_t nb = (N2 + GCG_PTS - 1) / GCG_PTS;
-  return (4 * B * N2 + 4 * (size_t)B * nb) * sizeof(double) + 2 * (size_t)B * sizeof(int) + 64;
+  return (4 * B * N2 + 4 * (size_t)B * nb) * sizeof(double) + 2 * (size_t)B * sizeof(int) + 64 +
+         coop_ctl_bytes(B, n);
+}
+// past carve()'s last array (iters), 8-byte aligned
+static unsigned long long* coop_ctl(void* ws, int B, int n) {
+  const uintptr_t end = reinterpret_cast<uintptr_t>(carve(ws, B, n).iters + B);
+  return reinterpret_cast<unsigned long long*>((end + 7) & ~uintptr_t(7));
 }
 
-static int lds_npt(int n) { return n <= 24 ? 4 : (n <= 80 ? 8 : 16); }
+// points per lane (lanes <= 1024): 4 up to n = 24, 7 up to n = 84 (config #3's 40 and 80: 4 and 15
+// waves per problem, 128 VGPRs), 16 up to n = 128 (spills part of its five vectors to scratch)
+static int lds_npt(int n) { return n <= 24 ? 4 : (n <= 84 ? 7 : 16); }
 
 // f[b][i][j] = sin(2 pi k1_b x_j) sin(2 pi k2_b y_i) on linspace(0,1,n)  (generate_forcing_term,
 // data_generation.py:60-77: meshgrid(x, y) -> X varies along columns, Y along rows)
@@ -469,10 +582,10 @@ int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B,
   int T = ceil_div((long long)n * n, npt);
   T = (T + 63) / 64 * 64;
   SRPDE_CHECK_ARG(T <= CG_MAXT, "srpde_poisson_cg_lds: n too large");
-  const size_t lds = ((size_t)(n + 2) * (n + 2) + 32) * sizeof(double);
+  const size_t lds = ((size_t)(n + 2) * (n + 2) + 64) * sizeof(double);
   switch (npt) {
     case 4: hipLaunchKernelGGL(cg_lds_kernel<4>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
-    case 8: hipLaunchKernelGGL(cg_lds_kernel<8>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
+    case 7: hipLaunchKernelGGL(cg_lds_kernel<7>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
     default: hipLaunchKernelGGL(cg_lds_kernel<16>, dim3(B), dim3(T), lds, stream, f, theta, u, n, rtol, maxit, iters, resid); break;
   }
   SRPDE_LAUNCH_CHECK("srpde_poisson_cg_lds");
@@ -547,10 +660,11 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   GridCoop g;
   g.r = c.r + b0 * N2; g.p0 = c.p0 + b0 * N2; g.p1 = c.p1 + b0 * N2;
   g.rrp = c.rrp0 + (size_t)b0 * c.nb; g.pqp = c.pqp + (size_t)b0 * c.nb;
-  g.bar = reinterpret_cast<unsigned long long*>(c.bbp);   // B * nb >= 2 doubles for n > 128
-  g.ctl = reinterpret_cast<unsigned*>(c.bbp + 1);
   g.n = n; g.nb = c.nb; g.B = cnt; g.rtol = rtol;
-  hipError_t e = hipMemsetAsync(c.bbp, 0, 2 * sizeof(double), stream);
+  g.ngrp = ceil_div((long long)cnt * c.nb, COOP_GRP);
+  g.bar = coop_ctl(ws, B, n);
+  g.ctl = reinterpret_cast<unsigned*>(g.bar + 1 + g.ngrp);
+  hipError_t e = hipMemsetAsync(g.bar, 0, (g.ngrp + 2) * sizeof(unsigned long long), stream);
   if (e != hipSuccess) { set_error("srpde_poisson_cg_batched: memset: %s", hipGetErrorString(e)); return (int)e; }
   const double* fb = f + b0 * N2;
   const double* tb = theta + b0 * N2;
