@@ -182,7 +182,9 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   const int wmi = wave % WM, wni = wave / WM;
   const int wm0 = wmi * TM, wn0 = wni * TN;
   constexpr int TI16 = 2 * TI, TJ16 = 2 * TJ;
-  int aoff[9][TI16];
+  // (the image row / column of each of this lane's rows; the nine tap offsets are formed per tap from
+  // them -- a [9][TI16] table held 18 VGPRs through the loop)
+  int ayy[TI16], axx[TI16];
 #pragma unroll
   for (int i = 0; i < TI16; ++i) {
     const int m = m0 + wm0 + i * 16 + l16;
@@ -192,14 +194,16 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
       yy = rem / p.W;
       xx = rem - yy * p.W;
     }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
-      const int iy = yy + (t / 3 - 1) * p.dil * p.sign, ix = xx + (t % 3 - 1) * p.dil * p.sign;
-      const int r = wm0 + i * 16 + l16 + (ky * p.W + kx) * p.dil;
-      aoff[t][i] = (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? soff + r * 128 + swz(r, lq) * 16 : zoff;
-    }
+    ayy[i] = yy;
+    axx[i] = xx;
   }
+  auto aoff_of = [&](auto tap_tag, int i) -> int {
+    constexpr int t = decltype(tap_tag)::value;
+    const int ky = p.sign > 0 ? t / 3 : 2 - t / 3, kx = p.sign > 0 ? t % 3 : 2 - t % 3;
+    const int iy = ayy[i] + (t / 3 - 1) * p.dil * p.sign, ix = axx[i] + (t % 3 - 1) * p.dil * p.sign;
+    const int r = wm0 + i * 16 + l16 + (ky * p.W + kx) * p.dil;
+    return (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) ? soff + r * 128 + swz(r, lq) * 16 : zoff;
+  };
   // B: instruction q = plane * (BN/16) + 16-row block; lane -> (row, slot), fetches chunk swzh^-1
   int b_off[BPW];
 #pragma unroll
@@ -358,14 +362,26 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   // one tap: the A fragments and the first column block's B fragments, then one column block's
   // MFMAs per further B read pair (without the schedule the compiler parks each read right before
   // its MFMA and exposes its latency)
+  // A fragments of the next tap, read during the current tap's last MFMA group (within a chunk the
+  // A tile does not change, so they stay valid across the stage barrier); tap 0 of a chunk reads its own.
+  // Pre-split inputs only: the convert path's registers leave no room for them in the other kernels
+  // (48 B of scratch, forward +3 %; presplit dgrad -2.4 %, tools/gpu/lib_ab.sh)
+  constexpr bool PF = PRE;
+  half8 pah[TI16], pal[TI16];
   auto tap_body = [&](const char* b, auto tap_tag) {
     constexpr int TAP = decltype(tap_tag)::value;
     half8 ah[TI16], al[TI16], bh[TJ16], bl[TJ16];
+    const char* abase = PRE ? lds + acur : lds;
 #pragma unroll
     for (int i = 0; i < TI16; ++i) {   // lo pieces: XOR 64 (see the LDS layout)
-      const char* abase = PRE ? lds + acur : lds;
-      ah[i] = *reinterpret_cast<const half8*>(abase + aoff[TAP][i]);
-      al[i] = *reinterpret_cast<const half8*>(abase + (aoff[TAP][i] ^ 64));
+      if constexpr (TAP == 0 || !PF) {
+        const int o = aoff_of(std::integral_constant<int, TAP>{}, i);
+        ah[i] = *reinterpret_cast<const half8*>(abase + o);
+        al[i] = *reinterpret_cast<const half8*>(abase + (o ^ 64));
+      } else {
+        ah[i] = pah[i];
+        al[i] = pal[i];
+      }
     }
 #pragma unroll
     for (int j = 0; j < TJ16; ++j) {
@@ -386,12 +402,21 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], c0, 0, 0, 0);
         chain(i, j) = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], c0, 0, 0, 0);
       }
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * TI16 + 2, 0);
+    if constexpr (PF && TAP < 8) {
+#pragma unroll
+      for (int i = 0; i < TI16; ++i) {
+        const int o = aoff_of(std::integral_constant<int, (TAP < 8 ? TAP + 1 : 8)>{}, i);
+        pah[i] = *reinterpret_cast<const half8*>(abase + o);
+        pal[i] = *reinterpret_cast<const half8*>(abase + (o ^ 64));
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, (TAP == 0 || !PF) ? 2 * TI16 + 2 : 2, 0);
 #pragma unroll
     for (int j = 1; j < TJ16; ++j) {
       __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI16, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
+    if constexpr (PF && TAP < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2 * TI16, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 3 * TI16, 0);
   };
   auto stage = [&](int ch, auto st_tag) {
@@ -400,17 +425,33 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     // the current chunk was converted to S before its first stage)
     const bool more = ch + 1 < c_end;
     const bool dma = !(p.dbg & 1);   // diagnostics (SRPDE_CONV_DBG, results wrong): 1 = no DMA in the loop
-    if (dma && ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
-    else if (dma && more) issue_b(ch + 1, 0, (sidx + 1) & 1);
-    if (dma && ST < NS - 1 && more) {
+    // waves 4..7 issue the stage's LDS-DMA pieces between its two taps, waves 0..3 before them: the two
+    // waves of a SIMD issue out of phase, each under the other's MFMAs (fwd -1.7 %, dgrad -0.6 % on the
+    // deep layers, tools/gpu/dma_ab.sh)
+    const bool late_b = wave >= 4 && TPS > 1;
+    const bool late_a = late_b;
+    auto dma_b = [&]() {
+      if (dma && ST < NS - 1) issue_b(ch, ST + 1, (sidx + 1) & 1);
+      else if (dma && more) issue_b(ch + 1, 0, (sidx + 1) & 1);
+    };
+    auto dma_a = [&]() {
+      if (dma && ST < NS - 1 && more) {
 #pragma unroll
-      for (int u = 0; u < AQ; ++u) issue_a(ch + 1, wave + (ST * AQ + u) * NW);
-    }
+        for (int u = 0; u < AQ; ++u) issue_a(ch + 1, wave + (ST * AQ + u) * NW);
+      }
+    };
+    if (!late_b) dma_b();
+    if (!late_a) dma_a();
     const char* b = bbuf0 + (sidx & 1) * B_STAGE;
     if (!(p.dbg & 128)) {   // diagnostics: 128 = no MFMA work
       tap_body(b, std::integral_constant<int, ST * TPS>{});
+      if (late_b) dma_b();
+      if (late_a) dma_a();
       if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
       if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
+    } else {
+      if (late_b) dma_b();
+      if (late_a) dma_a();
     }
     ++sidx;
     // the next stage's weights must have landed; the halo slices issued after them may still be
@@ -1725,12 +1766,14 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   const int T = nbm * nbn;
   const size_t lds = h3_lds(BN, h.arows, TPS, BNB, PRE);
   if ((size_t)h.arows * ROW2 < (size_t)(2 * WM * BN + WM * WN * 512) * 4) h.wide = 0;   // F too small to stage
-  static int slots = [&] {
-    int dev = 0, cus = 0;
+  static const int cus = [] {
+    int dev = 0, c = 0;
     (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max(1, cus) * (8 / (WM * WN));   // resident workgroups: one (8 waves) or two (4) per CU
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, c);
   }();
+  // resident workgroups: by waves (8 per CU) and by LDS
+  const int slots = cus * std::max(1, std::min(8 / (WM * WN), (int)((160 * 1024) / lds)));
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
   static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
   p.dbg = dbg;   // diagnostics only (timing experiments; results wrong when non-zero)
