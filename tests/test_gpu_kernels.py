@@ -362,6 +362,38 @@ def test_conv_h3_scale_invariance(scale, conv_math):
     assert e_exact < 1e-6 and rel(unrows(y2, n, h, h), y64) < 1e-6, (e_exact, scale)
 
 
+@pytest.mark.parametrize("log2_ratio", [6, 12, 18, 24])
+def test_conv_h3_outlier_channel(log2_ratio, conv_math):
+    """The h3 operand scale is per tensor: one channel 2^k larger than the rest sets it for all.
+    Outputs that read only the small channels keep fp32-class accuracy while those channels sit
+    within 2^-18 of the tensor's max (k <= 18: < 2e-6 relative); past that each small element keeps
+    an absolute error <= 2^-40 of the max, i.e. a relative error growing as 2^(k-40)
+    (k = 24: measured against that bound, not fp32's).  Outputs that read the outlier channel are
+    dominated by it and stay exact to fp32 rounding."""
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("h3")
+    g = torch.Generator().manual_seed(17 + log2_ratio)
+    n, cin, cout, h = 2, 64, 64, 20
+    x = torch.randn(n, cin, h, h, generator=g, dtype=torch.float64)
+    x[:, 0] *= 2.0 ** log2_ratio
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * 0.05
+    wt[: cout // 2, 0] = 0.0          # the first half of the outputs never reads the outlier channel
+    y64 = F.conv2d(x, wt, None, padding=1)
+    xr = rows(x.float()).to(DEV)
+    wf, _ = H.pack_conv_weights(wt.float().to(DEV), cin)
+    y = H.empty(n * h * h, cout, device=DEV)
+    H.conv_fwd(xr, None, wf, None, y, n, h, h, cout, 3, 1, 1, False, None)
+    torch.cuda.synchronize()
+    yc = unrows(y, n, h, h)
+    e_small = rel(yc[:, : cout // 2], y64[:, : cout // 2])
+    e_big = rel(yc[:, cout // 2:], y64[:, cout // 2:])
+    assert e_big < 2e-6, e_big
+    if log2_ratio <= 18:
+        assert e_small < 2e-6, e_small
+    else:
+        assert e_small < 4 * 2.0 ** (log2_ratio - 40) + 2e-6, e_small
+
+
 def test_amax_words_match_outputs():
     """bn_relu_fwd / bn_relu_bwd write max|out| (float bits) into the word they are given."""
     from superresolution_for_pdes_amd import hipops as H
