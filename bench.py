@@ -116,6 +116,9 @@ def parse():
     ap.add_argument("--roofline-layer", default="bridge.3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="skip the two rocprofv3 PMC passes that measure the roofline kernel's HBM bytes for this "
+                         "line (N=1 train only) and take them from --traffic-json / the newest profiles file")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic of the roofline kernel (tools/traffic_json.py output); default: the newest "
                          "profiles/traffic_r*.json, which round_evidence.sh measures on the tree it commits with")
@@ -382,6 +385,42 @@ def _free_port():
     return port
 
 
+def measure_traffic_live(layer):
+    """HBM bytes per launch of the roofline kernel, measured now on this build: two rocprofv3 PMC
+    passes (FETCH_SIZE, WRITE_SIZE -- separate runs, --kernel-trace only) over tools/conv_bench.py
+    running that layer's forward, reduced by tools/traffic_json.py (FETCH_SIZE x2, the guide's gfx950
+    correction).  Child processes, each under a hard time limit, started before this process touches
+    the GPU.  -> (bytes or None, source note)."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="srpde_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", c, "--kernel-trace", "--output-format", "csv",
+                   "-d", d, "-o", f"p{i}", "--", sys.executable, os.path.join(ROOT, "tools", "conv_bench.py"),
+                   "--layers", layer, "--only", "fwd", "--iters", "3"]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            if r.returncode != 0:
+                return None, f"PMC pass {c} failed (rc {r.returncode})"
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "traffic_json.py"), d, layer],
+                           capture_output=True, text=True, timeout=120)
+        rec = json.loads(r.stdout.strip().splitlines()[-1])
+        val = rec.get(f"h3:{layer}")
+        det = rec.get(f"h3:{layer}_detail", {})
+        return (val if val else None,
+                f"measured by this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over tools/conv_bench.py {layer} fwd "
+                f"(read {det.get('read_bytes')} B x2-corrected, written {det.get('write_bytes')} B per launch)")
+    except Exception as e:   # noqa: BLE001 -- the bench line must not depend on the profiler
+        return None, f"PMC measurement failed: {e}"
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def launch_ranks(args):
     """``--gpus N > 1`` without a launcher: start ``torch.distributed.run`` with N ranks (one process
     per GPU) as a CHILD process -- this process has made no GPU call yet and makes none -- relay the
@@ -407,6 +446,10 @@ def main():
     if ws is not None and int(ws) != args.gpus and not (args.gpus == 1 and args.ddp):
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one rank per GPU)", file=sys.stderr)
         sys.exit(2)
+    live_traffic = None
+    if (ws is None and args.workload == "train" and not args.no_live_traffic and args.traffic_json is None
+            and not args.ddp):
+        live_traffic = measure_traffic_live(args.roofline_layer)   # before this process touches the GPU
     # RCCL prints its version block on fd 1 at communicator creation: keep fd 1 for the JSON line
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")
@@ -511,12 +554,18 @@ def main():
         flops_launch = conv_flops(cin, cout, hw) * B
         achieved = flops_launch / (kern_avg * 1e-3) / 1e12 if kern_avg > 0 else None
         kname = {"h3": "conv_fwd_h3"}.get(math, "conv_fwd_v2")
-        traffic, tfile = None, args.traffic_json or default_traffic_json()
-        if tfile and os.path.exists(tfile):
+        traffic, tfile, tsource = None, args.traffic_json or default_traffic_json(), None
+        if live_traffic is not None and live_traffic[0] and math == "h3":
+            traffic, tsource = live_traffic
+        elif tfile and os.path.exists(tfile):
             try:
                 traffic = json.load(open(tfile)).get(f"{math}:{args.roofline_layer}")
             except (ValueError, OSError):
                 traffic = None
+            if traffic:
+                tsource = (os.path.relpath(tfile, ROOT) + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                           "tools/gpu/round_evidence.sh)" +
+                           (f"; live measurement unavailable: {live_traffic[1]}" if live_traffic else ""))
         samples = world * B * args.steps
         # whole-step fraction: algorithmic FLOP of every 3x3 conv pass the step runs (forward,
         # dgrad except enc1.conv1's, whose input needs no gradient, and wgrad) at batch B, over the
@@ -544,8 +593,7 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                          "traffic": traffic,
-                         "traffic_source": (os.path.relpath(tfile, ROOT) + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
-                                            "per launch, tools/gpu/round_evidence.sh)") if traffic else None,
+                         "traffic_source": tsource,
                          "launch_ms": round(kern_avg, 4),
                          "algorithmic_flop_per_launch": flops_launch,
                          "step": {"algorithmic_flop": step_flop, "achieved": round(step_ach, 2),

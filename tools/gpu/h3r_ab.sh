@@ -18,6 +18,6 @@ for rep in 1 2; do
 done
 for v in 0 1 0 1; do
   if [ $v = e ]; then export SRPDE_H3R=1 SRPDE_H3R_EARLY=1; else export SRPDE_H3R=$v SRPDE_H3R_EARLY=0; fi
-  timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/h3r_bench_${T}_$v.json 2> gpurun_out/h3r_bench_${T}_$v.err || { echo "bench $v failed"; tail gpurun_out/h3r_bench_${T}_$v.err; exit 1; }
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-live-traffic --steps 20 > gpurun_out/h3r_bench_${T}_$v.json 2> gpurun_out/h3r_bench_${T}_$v.err || { echo "bench $v failed"; tail gpurun_out/h3r_bench_${T}_$v.err; exit 1; }
   echo "H3R=$v $(python -c "import json,sys; d=json.load(open('gpurun_out/h3r_bench_${T}_$v.json')); print(d['ms_per_step'], d['value'])")"
 done

@@ -13,7 +13,7 @@ for rep in $(seq 1 $N); do
   i=0
   for cfg in "$@"; do
     i=$((i+1))
-    env $cfg timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/knob_${T}_${i}_$rep.json 2> gpurun_out/knob_${T}_${i}_$rep.err || { echo "bench [$cfg] failed"; tail gpurun_out/knob_${T}_${i}_$rep.err; exit 1; }
+    env $cfg timeout -k 10 200 python bench.py --no-cpu-baseline --no-live-traffic --steps 20 > gpurun_out/knob_${T}_${i}_$rep.json 2> gpurun_out/knob_${T}_${i}_$rep.err || { echo "bench [$cfg] failed"; tail gpurun_out/knob_${T}_${i}_$rep.err; exit 1; }
     echo "[$cfg] $rep $(python -c "import json; d=json.load(open('gpurun_out/knob_${T}_${i}_$rep.json')); print(d['ms_per_step'], d['value'])")"
   done
 done

@@ -15,7 +15,7 @@ fi
 for rep in $(seq 1 $N); do
   for v in base new; do
     if [ $v = base ]; then export SRPDE_LIB=$R/superresolution_for_pdes_amd/lib/ab/libsrpde_hip_base.so; else unset SRPDE_LIB; fi
-    timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/stepab_${T}_${v}_$rep.json 2> gpurun_out/stepab_${T}_${v}_$rep.err || { echo "bench $v failed"; tail gpurun_out/stepab_${T}_${v}_$rep.err; exit 1; }
+    timeout -k 10 200 python bench.py --no-cpu-baseline --no-live-traffic --steps 20 > gpurun_out/stepab_${T}_${v}_$rep.json 2> gpurun_out/stepab_${T}_${v}_$rep.err || { echo "bench $v failed"; tail gpurun_out/stepab_${T}_${v}_$rep.err; exit 1; }
     echo "$v $rep $(python -c "import json; d=json.load(open('gpurun_out/stepab_${T}_${v}_$rep.json')); print(d['ms_per_step'], d['value'])")"
   done
 done
