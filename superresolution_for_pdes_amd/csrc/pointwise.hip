@@ -347,32 +347,47 @@ __global__ __launch_bounds__(256) void upsample_fwd_px_kernel(const float* __res
 // (models.py:124-125: sa = sigmoid(conv1x1(g)) with g = up(d), models.py:89,92): the block's x
 // threads hold one output pixel's channels, so the 1x1 conv is a shuffle reduction over them and g
 // is not re-read for it.  c / 4 a power of two <= 64 (one pixel per half or whole wave).
+// UPX pixel groups per block (blockDim.y pixels each), every group's four source loads issued before
+// any interpolation: fewer, longer blocks with more loads in flight (the output write, 2/3 of the bytes,
+// set the pace; 205 k eight-pixel blocks for u2 spent their time in dispatch and load latency)
+constexpr int UPX = 4;
 __global__ __launch_bounds__(256) void upsample_gate_fwd_px_kernel(const float* __restrict__ x, int ldx,
                                                                    float* __restrict__ out, int ldo, unsigned npix,
                                                                    int H, int W, int Ho, int Wo,
                                                                    const float* __restrict__ wg,
                                                                    const float* __restrict__ bg,
                                                                    float* __restrict__ sa) {
-  const unsigned q = px_index();
-  const bool on = q < npix;
-  const unsigned qq = on ? q : 0;
-  const unsigned ox = qq % (unsigned)Wo, t = qq / (unsigned)Wo, oy = t % (unsigned)Ho, n = t / (unsigned)Ho;
   const int c = threadIdx.x * 4;
-  const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
-  const float* base = x + (size_t)n * H * W * ldx + c;
-  const float4 a = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i0) * ldx);
-  const float4 b = *reinterpret_cast<const float4*>(base + (size_t)(ly.i0 * W + lx.i1) * ldx);
-  const float4 d = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i0) * ldx);
-  const float4 f = *reinterpret_cast<const float4*>(base + (size_t)(ly.i1 * W + lx.i1) * ldx);
-  float4 o;
-#define UP(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
-  UP(x) UP(y) UP(z) UP(w)
-#undef UP
-  if (on) *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
   const float4 wv = *reinterpret_cast<const float4*>(wg + c);
-  float acc = o.x * wv.x + o.y * wv.y + o.z * wv.z + o.w * wv.w;
-  for (int off = 1; off < (int)blockDim.x; off <<= 1) acc += __shfl_xor(acc, off, 64);
-  if (on && threadIdx.x == 0) sa[q] = 1.f / (1.f + expf(-(acc + bg[0])));
+  const float bias = bg[0];
+  float4 a[UPX], b[UPX], d[UPX], f[UPX];
+  Lerp ly[UPX], lx[UPX];
+#pragma unroll
+  for (int u = 0; u < UPX; ++u) {
+    const unsigned q = (blockIdx.x * UPX + u) * blockDim.y + threadIdx.y;
+    const unsigned qq = q < npix ? q : 0;
+    const unsigned ox = qq % (unsigned)Wo, t = qq / (unsigned)Wo, oy = t % (unsigned)Ho, n = t / (unsigned)Ho;
+    ly[u] = lerp_index(oy, H, Ho);
+    lx[u] = lerp_index(ox, W, Wo);
+    const float* base = x + (size_t)n * H * W * ldx + c;
+    a[u] = *reinterpret_cast<const float4*>(base + (size_t)(ly[u].i0 * W + lx[u].i0) * ldx);
+    b[u] = *reinterpret_cast<const float4*>(base + (size_t)(ly[u].i0 * W + lx[u].i1) * ldx);
+    d[u] = *reinterpret_cast<const float4*>(base + (size_t)(ly[u].i1 * W + lx[u].i0) * ldx);
+    f[u] = *reinterpret_cast<const float4*>(base + (size_t)(ly[u].i1 * W + lx[u].i1) * ldx);
+  }
+#pragma unroll
+  for (int u = 0; u < UPX; ++u) {
+    const unsigned q = (blockIdx.x * UPX + u) * blockDim.y + threadIdx.y;
+    const bool on = q < npix;
+    float4 o;
+#define UP(X) o.X = ly[u].l0 * (lx[u].l0 * a[u].X + lx[u].l1 * b[u].X) + ly[u].l1 * (lx[u].l0 * d[u].X + lx[u].l1 * f[u].X);
+    UP(x) UP(y) UP(z) UP(w)
+#undef UP
+    if (on) *reinterpret_cast<float4*>(out + (size_t)q * ldo + c) = o;
+    float acc = o.x * wv.x + o.y * wv.y + o.z * wv.z + o.w * wv.w;
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    if (on && threadIdx.x == 0) sa[q] = 1.f / (1.f + expf(-(acc + bias)));
+  }
 }
 
 // gsa / gw (nullable): the attention gating gradient folded in, the upsampled tensor's gradient
@@ -1144,6 +1159,7 @@ int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ld
                   "srpde_upsample_bilinear_gate_fwd: bad args (c / 4 a power of two <= 64)");
   dim3 g, b;
   SRPDE_CHECK_ARG(px_geometry((long long)n * ho * wo, c, &g, &b), "srpde_upsample_bilinear_gate_fwd: bad geometry");
+  g.x = (g.x + UPX - 1) / UPX;
   hipLaunchKernelGGL(upsample_gate_fwd_px_kernel, g, b, 0, stream, x, ldx, out, ldo, (unsigned)(n * ho * wo), h, w,
                      ho, wo, wg, bg, sa);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_gate_fwd");
