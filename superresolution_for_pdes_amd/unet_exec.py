@@ -355,7 +355,6 @@ class WgradStream:
             WgradStream._streams[key] = side
         self.side = side
 
-
     def submit(self, fn, keep=()):
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
