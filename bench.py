@@ -401,7 +401,7 @@ def measure_traffic_live(layer):
     env = dict(os.environ, TMPDIR="/tmp")
     try:
         for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
-            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", c, "--kernel-trace", "--output-format", "csv",
+            cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", c, "--kernel-trace", "--output-format", "csv",
                    "-d", d, "-o", f"p{i}", "--", sys.executable, os.path.join(ROOT, "tools", "conv_bench.py"),
                    "--layers", layer, "--only", "fwd", "--iters", "3"]
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
