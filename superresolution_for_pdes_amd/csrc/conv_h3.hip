@@ -113,7 +113,8 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   constexpr int B_TAP = 2 * BP_BYTES;      // hi + lo planes of one tap
   constexpr int B_STAGE = TPS * B_TAP;
   constexpr int NS = (9 + TPS - 1) / TPS;  // stages per channel chunk
-  constexpr int AQ = (8 + NS - 2) / (NS - 1);   // halo-slice DMAs per wave in stages 0..NS-2 (8 per wave per chunk)
+  constexpr int AQ = (64 / NW + NS - 2) / (NS - 1);   // halo-slice DMAs per wave in stages 0..NS-2 (64 / NW per wave
+                                                      // and chunk: arows <= 512)
   constexpr int AD = BNB ? 2 : 1;               // DMAs per halo slice (BNB: the gradient and the BN input)
   static_assert(BM % SRB == 0 && WM % (BM / SRB) == 0, "statistics sub-blocks");
   static_assert(TPS >= 1 && TPS <= 3, "taps per stage");
