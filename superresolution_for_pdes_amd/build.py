@@ -29,6 +29,8 @@ ARCH = os.environ.get("SRPDE_ARCH", "gfx950")
 # DESIGN.md 7.4, tools/race_up.py); the host compile ignores the feature (one warning per file)
 NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"] + NO_PK
+# SRPDE_EXTRA_FLAGS: extra compile flags (e.g. -DBNAS_U=8) for an A/B variant built with SRPDE_BUILD_OUT
+FLAGS += os.environ.get("SRPDE_EXTRA_FLAGS", "").split()
 
 
 def sources():

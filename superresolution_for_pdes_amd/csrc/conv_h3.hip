@@ -178,7 +178,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
   // per tap: the LDS byte offset of this lane's A fragment (hi pieces; lo = XOR 64) of its 16x16x32
   // row (lane & 15 of each 16-row block, chunk lane >> 4) shifted by the tap; the zero row for taps
   // outside the image.  Computed once per tile.
-  const int lr = lane & 31, lh = lane >> 5;
+  const int lr = lane & 31;
   const int l16 = lane & 15, lq = lane >> 4;
   const int wmi = wave % WM, wni = wave / WM;
   const int wm0 = wmi * TM, wn0 = wni * TN;
