@@ -98,13 +98,13 @@ class FusedAdamW(torch.optim.Optimizer):
     def clip_grad_norm_(self, max_norm, grad_scale=1.0):
         """clip_grad_norm_(all params, max_norm) on device.  Like torch's, the NEXT step()
         uses the clipped gradients (the coefficient is applied inside the fused update
-        instead of rewriting the gradients).  Returns the total-norm tensor (device)."""
+        instead of rewriting the gradients).  Returns the total-norm tensor (device), a fresh one per call
+        as torch's is (a caller keeping a step's norm must not see the next step's)."""
         grads = [p.grad for g in self.param_groups for p in g["params"]]
         flat = _flat_span(sorted(grads, key=lambda t: t.data_ptr())) if all(g is not None for g in grads) else None
         if flat is None:
             flat = torch.cat([g.reshape(-1) for g in grads if g is not None])
-        if self._coef is None or self._coef.device != flat.device:
-            self._coef = torch.empty(2, dtype=torch.float32, device=flat.device)
+        self._coef = torch.empty(2, dtype=torch.float32, device=flat.device)   # caching allocator: no launch
         H.clip_coef(flat, grad_scale, float(max_norm) if max_norm is not None else -1.0, self._coef)
         self._pending = True
         self.last_total_norm = self._coef[1]

