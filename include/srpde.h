@@ -32,6 +32,16 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
+/* ABI version: bumped whenever an exported signature or a documented buffer layout changes.
+ * A binding built against this header checks srpde_version() == SRPDE_ABI_VERSION at load time
+ *  and refuses a mismatched library instead of misreading arguments.
+ *   1  round 1-2 layout
+ *   4  round 3 changes (srpde_conv_fwd_h3: in_scale ... ep_amax before the workspace; the
+ *      srpde_prepare_weights_h3 descriptor row grew to 10 columns; srpde_conv_wgrad_h3p reads dy
+ *      planes with a row stride of cout rounded up to 32) and round 4's additions
+ *      (srpde_conv_h4_set, srpde_poisson_debug_abort) */
+#define SRPDE_ABI_VERSION 4
+
 const char* srpde_last_error(void);
 int srpde_version(void);
 
@@ -75,6 +85,12 @@ int srpde_conv_h3_stats_rows(void);
  * kernel.  Both compute the same outputs, statistics and stored splits bit for bit (outside a
  * K-split tail).  Returns the previous value.  Tuning and tests. */
 int srpde_conv_h3r_set(int on);
+/* Kernel choice of srpde_conv_fwd_h3 / srpde_conv_fwd_h3_presplit for 128-column output tiles
+ * (cout % 128 == 0) at W = 10 (dilation 1 or 2) and W = 20 (dilation 1): 1 = the h4 kernel
+ * (conv_h4.hip: one-tap weight ring, fragments read a tap ahead; default, SRPDE_H4=0 turns it
+ * off), 0 = the h3 8-wave kernel.  Bit-identical outputs, statistics and stored splits.  Returns
+ * the previous value.  Tuning and tests. */
+int srpde_conv_h4_set(int on);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]
@@ -353,7 +369,13 @@ size_t srpde_poisson_workspace_size(int B, int n);
  * points below and polls convergence every 128 iterations, synchronising `stream`. */
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* Problems per cooperative grid-CG launch at this n; 0 when one problem does not fit the
+ * co-resident grid or n > 2048 (the stencil's neighbour rows must lie in the adjacent block). */
 int srpde_poisson_coop_problems(int n);
+/* Test hook: 1 = every following cooperative grid-CG launch starts aborted (iters_out = -1 for its
+ * problems, u undefined), 0 = normal.  Returns the previous setting.  Exercises callers' handling of
+ * a stuck grid barrier (poisson.solve_batched raises). */
+int srpde_poisson_debug_abort(int on);
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream);
 int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,

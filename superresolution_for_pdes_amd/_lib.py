@@ -69,7 +69,13 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `python -m superresolution_for_pdes_amd.build` "
                 "(the HIP path has no CPU fallback)")
-        _lib = ctypes.CDLL(LIB_PATH)
+        cd = ctypes.CDLL(LIB_PATH)
+        want = int(re.search(r"#define SRPDE_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+        have = cd.srpde_version()
+        if have != want:   # a library built against another header would misread arguments
+            raise RuntimeError(f"{LIB_PATH}: ABI version {have}, include/srpde.h declares {want}: rebuild it "
+                               "(python -m superresolution_for_pdes_amd.build --force)")
+        _lib = cd
         _protos = parse_header()
         for name, (res, args) in _protos.items():
             fn = getattr(_lib, name)

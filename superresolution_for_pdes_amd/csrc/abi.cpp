@@ -21,6 +21,6 @@ extern "C" {
 
 const char* srpde_last_error(void) { return srpde::g_err; }
 
-int srpde_version(void) { return 1; }
+int srpde_version(void) { return SRPDE_ABI_VERSION; }
 
 }  // extern "C"

@@ -1021,7 +1021,7 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   if (v2_ok(p)) {
     switch (fwd_config(cout)) {
       case 0: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream, workspace, ws_bytes);

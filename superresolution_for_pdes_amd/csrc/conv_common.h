@@ -6,6 +6,14 @@
 #include <cstdlib>
 #include "common.h"
 
+// Timing-only diagnostics of the h3 kernels (phase ablation): a compile-time bit set,
+// 0 in the product build -- an A/B library is built with SRPDE_EXTRA_FLAGS=-DSRPDE_CONV_DBG=<bits>
+// (results wrong when non-zero).  1 = no DMA in the loop, 2 = no stage barrier, 4 = no per-chunk
+// convert, 16 = no epilogue, 32 = no prologue halo DMA, 64 = no prologue convert, 128 = no MFMAs.
+#ifndef SRPDE_CONV_DBG
+#define SRPDE_CONV_DBG 0
+#endif
+
 namespace srpde {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -22,7 +30,6 @@ struct ConvParams {
   // tail split (v2 only): the last `ntail` tiles are computed as `tsplit` K-pieces each,
   // written raw to `part`, and finished (sum, bias, store, BN partials) by conv_tail_fixup
   int ntail, tsplit;
-  int dbg;              // diagnostics (SRPDE_CONV_DBG): 1 = x6 kernel skips the per-stage DMA
   float* part;
   // optional fused BatchNorm-backward reduction (h3 dgrad): the output is the gradient of a
   // BN + ReLU output a = relu(gamma * (bn_y - mean) * invstd + beta); per (SRB-row block, channel)
@@ -631,7 +638,7 @@ int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, in
 // ---------------- host: K-split of the last, under-filled round of tiles ----------------
 // tail split plan shared by the LDS-DMA forward kernels (see launch_fwd_v2)
 static void plan_tail(ConvParams& p, int T, int slots, int BM, int BN, void* ws, size_t ws_bytes) {
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   const int nall = p.K / BK2;
   const int rem = T % slots;
   if (T >= slots && rem > 0 && 2 * rem <= slots && ws != nullptr) {

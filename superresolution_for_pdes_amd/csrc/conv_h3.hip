@@ -29,76 +29,9 @@
 #include <atomic>
 
 #include "conv_common.h"
+#include "conv_h3.h"
 
 namespace srpde {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-
-
-__device__ __forceinline__ void split2h(const float4 a, const float4 b, float s, half8& hi, half8& lo) {
-  const float v[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const _Float16 h = (_Float16)v[k];
-    hi[k] = h;
-    lo[k] = (_Float16)(v[k] - (float)h);
-  }
-}
-
-// 32-half (64-B) weight rows: 16-B chunk c of row r sits in slot c ^ g((r >> 2) & 3), g = (0, 2, 3, 1):
-// conflict-free for the 16x16x32 B-fragment reads (lane: row (lane & 15), chunk lane >> 4) of every
-// ds_read_b128 lane group (MI355X_MICROARCH.md, LDS table)
-__device__ __forceinline__ int swzh(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// The main loops run v_mfma_f32_16x16x32_f16 (one 32-channel chunk of a tap per instruction): at
-// equal cycles per FLOP the 16x16 shape holds a higher clock under load on random data than
-// 32x32x16 (tools/mfma_peak.hip: 2058 vs 1791-1861 TF dense, profiles/r03_mfma_shapes.txt).  The
-// epilogue (x6_finish) keeps the 32x32x16 accumulator layout; a 32x32 block is four 16x16 blocks
-// (a, b) (rows 16a.., cols 16b..), regrouped in registers by two lane swaps per dword:
-// X = (a, 0), Y = (a, 1) at one element q -> permlane16_swap -> permlane32_swap gives the 32x32
-// elements 4 (2a) + q and 4 (2a + 1) + q.
-template <int TI, int TJ>
-__device__ __forceinline__ void acc16_to_32(const floatx4 (&a16)[2 * TI][2 * TJ], floatx16 (&a32)[TI][TJ]) {
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const auto r1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a16[2 * i + a][2 * j][q]),
-                                                           __float_as_uint(a16[2 * i + a][2 * j + 1][q]), false, false);
-          const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
-          a32[i][j][8 * a + q] = __uint_as_float(r2[0]);
-          a32[i][j][8 * a + 4 + q] = __uint_as_float(r2[1]);
-        }
-}
-
-struct H3Args {
-  const _Float16* wsp;     // [2][Cout][K] hi / lo planes
-  const int* wexp;         // [Cout] weight scale exponents
-  const unsigned* amax0;   // max|x0| (float bits), or null
-  const unsigned* amax1;   // max|x1|, or null
-  int halo;                // (W + 1) * dil
-  int arows;               // BM + 2 * halo, rounded up to 8 (<= 512: at most 8 slices per wave)
-  int relax;               // 1: a stage waits only for its weight DMA (halo slices land later)
-  _Float16* xsplit;        // optional [2][P][Cin] hi / lo planes of the (scaled) input, written
-                           // as a by-product of the split for the weight-gradient kernel
-  const float* in_scale;   // optional per-channel affine + ReLU applied to x0 in the split
-  const float* in_shift;   // (the producing BatchNorm, fused; c1 == 0)
-  int wide;                // 1: the epilogue stores 16-B rows through LDS (ldy % 4 == 0, y 16-B aligned)
-  // BNB kernels (dgrad with the BatchNorm(+ReLU) backward apply fused into the operand transform):
-  // x0 is the gradient da of the BN + ReLU output; the operand is
-  //   dy = gamma*invstd * (dz - m1 - xhat*m2),  xhat = (y - mean)*invstd,  dz = da * [xhat*gamma + beta > 0]
-  // (m1 = m2 = 0 in eval mode), computed per halo element from a second fp32 halo tile of y
-  const float* bnb_y; int bnb_ldy;
-  const float* bnb_mean; const float* bnb_invstd; const float* bnb_gamma; const float* bnb_beta;
-  const float* bnb_m1; const float* bnb_m2;
-  int bnb_relu;
-};
 
 // TWO_LEVEL: one partial MFMA chain per channel chunk folded into the accumulator (needs twice
 // the accumulator registers); otherwise one fp32 MFMA chain over all of K, as a CPU GEMM sums.
@@ -350,12 +283,12 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
       for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
 
   // prologue: whole halo tile of the first chunk + first weight stage
-  if (!(p.dbg & 32))   // diagnostics: 32 = no prologue halo DMA, 64 = no prologue convert
+  if (!(SRPDE_CONV_DBG & 32))   // diagnostics: 32 = no prologue halo DMA, 64 = no prologue convert
     for (int q = wave; q < na; q += NW) issue_a(c_beg, q);
   issue_b(c_beg, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (!PRE && !(p.dbg & 64)) convert(c_beg);
+  if (!PRE && !(SRPDE_CONV_DBG & 64)) convert(c_beg);
   __syncthreads();
 
   int sidx = 0;      // stage counter (B buffer parity)
@@ -425,7 +358,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     // prefetch: the next weight stage, then AQ slices of the next chunk's halo tile (F is free:
     // the current chunk was converted to S before its first stage)
     const bool more = ch + 1 < c_end;
-    const bool dma = !(p.dbg & 1);   // diagnostics (SRPDE_CONV_DBG, results wrong): 1 = no DMA in the loop
+    const bool dma = !(SRPDE_CONV_DBG & 1);   // diagnostics (SRPDE_CONV_DBG, results wrong): 1 = no DMA in the loop
     // waves 4..7 issue the stage's LDS-DMA pieces between its two taps, waves 0..3 before them: the two
     // waves of a SIMD issue out of phase, each under the other's MFMAs (fwd -1.7 %, dgrad -0.6 % on the
     // deep layers, tools/gpu/dma_ab.sh)
@@ -444,7 +377,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     if (!late_b) dma_b();
     if (!late_a) dma_a();
     const char* b = bbuf0 + (sidx & 1) * B_STAGE;
-    if (!(p.dbg & 128)) {   // diagnostics: 128 = no MFMA work
+    if (!(SRPDE_CONV_DBG & 128)) {   // diagnostics: 128 = no MFMA work
       tap_body(b, std::integral_constant<int, ST * TPS>{});
       if (late_b) dma_b();
       if (late_a) dma_a();
@@ -461,7 +394,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ * AD) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!(p.dbg & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
+    if (!(SRPDE_CONV_DBG & 2)) __syncthreads();   // diagnostics: 2 = no stage barrier
   };
   for (int ch = c_beg; ch < c_end; ++ch) {
     if constexpr (PRE) acur = (ch & 1) * abuf;
@@ -481,7 +414,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
 #pragma unroll
         for (int j = 0; j < TJ16; ++j) acc[i][j] += part[i][j];
     }
-    if (!PRE && ch + 1 < c_end && !(p.dbg & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
+    if (!PRE && ch + 1 < c_end && !(SRPDE_CONV_DBG & 4)) {   // the next chunk's halo tile has landed in F (vmcnt(0) + barrier)
       convert(ch + 1);                      // (diagnostics: 4 = no per-chunk convert)
       __syncthreads();
     }
@@ -510,7 +443,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
     }
     if (col >= p.Cout) colscale[j] = 0.f;
   }
-  if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+  if (SRPDE_CONV_DBG & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -802,7 +735,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
       issue_b(c < c_end ? c : -1, TGT % NS, cur == 0 ? NB - 1 : cur - 1);
     }
     const char* b = bbuf0 + cur * B_STAGE;
-    if (!(p.dbg & 128)) {   // diagnostics (SRPDE_CONV_DBG, results wrong): 128 = no MFMA work
+    if (!(SRPDE_CONV_DBG & 128)) {   // diagnostics (SRPDE_CONV_DBG, results wrong): 128 = no MFMA work
       tap_body(b, std::integral_constant<int, ST * TPS>{});
       if constexpr (TPS > 1 && ST * TPS + 1 < 9) tap_body(b + B_TAP, std::integral_constant<int, ST * TPS + 1>{});
       if constexpr (TPS > 2 && ST * TPS + 2 < 9) tap_body(b + 2 * B_TAP, std::integral_constant<int, ST * TPS + 2>{});
@@ -840,7 +773,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     if constexpr (NS > 7) stage(ch, std::integral_constant<int, 7>{});
     if constexpr (NS > 8) stage(ch, std::integral_constant<int, 8>{});
     if (ch + 1 < c_end) {   // every wave is past the chunk's last stage barrier: S is free
-      if (!(p.dbg & 4)) convert(ch + 1);   // diagnostics: 4 = no per-chunk split
+      if (!(SRPDE_CONV_DBG & 4)) convert(ch + 1);   // diagnostics: 4 = no per-chunk split
       __syncthreads();
     }
   }
@@ -864,7 +797,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     }
     if (col >= p.Cout) colscale[j] = 0.f;
   }
-  if (p.dbg & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+  if (SRPDE_CONV_DBG & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -1732,23 +1665,6 @@ constexpr int H3_SRB = 128;
 
 static int h3_arows(int w, int dil, int bm = H3_BM) { return (bm + 2 * (w + 1) * dil + 7) / 8 * 8; }
 
-// the K-split tail's fixup: one block per statistics sub-block of each tail tile (twice the blocks of a
-// whole-tile fixup for the same work: the tail has few tiles; 32.15 -> 32.12 ms per step) unless the
-// per-tile max|out| slot is wanted
-template <int BM, int BN, int SRB>
-static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
-  if constexpr (BM > SRB) {
-    if (p.out_max == nullptr) {
-      hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB, SRB>), dim3(p.ntail, BM / SRB), dim3(1024), 0, st, p);
-      SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
-      return 0;
-    }
-  }
-  hipLaunchKernelGGL((conv_tail_fixup_kernel<BM, BN, SRB>), dim3(p.ntail), dim3(1024), 0, st, p);
-  SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(tail fixup)");
-  return 0;
-}
-
 static size_t h3_lds(int bn, int arows, int tps = 1, bool bnb = false, bool pre = false) {
   if (pre) return (size_t)2 * (arows + 1) * 128 + (size_t)2 * tps * 2 * bn * 64 + 1024;
   return (size_t)arows * ((bnb ? 2 : 1) * ROW2 + 128) + (size_t)2 * tps * 2 * bn * 64 + 128 + 1024;
@@ -1776,8 +1692,6 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   // resident workgroups: by waves (8 per CU) and by LDS
   const int slots = cus * std::max(1, std::min(8 / (WM * WN), (int)((160 * 1024) / lds)));
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
-  static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
-  p.dbg = dbg;   // diagnostics only (timing experiments; results wrong when non-zero)
   const int nch = p.Cin / BK2;
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
@@ -1808,6 +1722,18 @@ static bool h3r_on() {
   }
   return v != 0;
 }
+static std::atomic<int> g_h4{-1};
+bool h4_on() {
+  int v = g_h4.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("SRPDE_H4");   // A/B switch between two bit-identical kernels: 0 = the h3 8-wave kernel
+    v = (!e || atoi(e) != 0) ? 1 : 0;
+    int expect = -1;
+    g_h4.compare_exchange_strong(expect, v);
+    v = g_h4.load(std::memory_order_relaxed);
+  }
+  return v != 0;
+}
 // the h3r kernel takes this shape: an output tile of <= 64 channels, a halo tile that fits the
 // registers, and two workgroups' LDS per CU
 static bool h3r_fits(int bn, int arows) {
@@ -1828,8 +1754,6 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
     return std::max(1, cus) * 2;   // resident workgroups: two per CU
   }();
   plan_tail(p, T, slots, BM, BN, ws, ws_bytes);
-  static const int dbg = [] { const char* e = getenv("SRPDE_CONV_DBG"); return e ? atoi(e) : 0; }();
-  p.dbg = dbg;   // diagnostics only (timing experiments; results wrong when non-zero)
   const int nch = p.Cin / BK2;
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
@@ -1954,7 +1878,8 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   p.ldx1 = c0 + c1;
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
-  SRPDE_CHECK_ARG(2LL * p.P * std::max(cout, p.Cin) * 2 < (1LL << 31), "srpde_conv_wgrad_h3p: tensor too large");
+  // the dy planes' row stride is cout rounded up to 32 (p.lddy): the bound is on that width
+  SRPDE_CHECK_ARG(2LL * p.P * std::max(p.lddy, p.Cin) * 2 < (1LL << 31), "srpde_conv_wgrad_h3p: tensor too large");
   h3p_split(p.P, cout, p.K, &p.chunk, &p.splits);
   const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
   if (ws_bytes < need) {
@@ -1983,6 +1908,12 @@ using namespace srpde;
 extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
+
+int srpde_conv_h4_set(int on) {
+  const int prev = h4_on() ? 1 : 0;
+  g_h4.store(on ? 1 : 0);
+  return prev;
+}
 
 int srpde_conv_h3r_set(int on) {
   const int prev = h3r_on() ? 1 : 0;
@@ -2050,7 +1981,7 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   const long long maxld = std::max(ldx0, c1 ? ldx1 : 0);
   SRPDE_CHECK_ARG((long long)p.P * maxld * 4 < (1LL << 31) && 2LL * cout * p.K * 2 < (1LL << 31),
                   "srpde_conv_fwd_h3: tensor too large");
@@ -2085,6 +2016,7 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);
   }
+  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_)                                                                        \
   (tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
@@ -2119,7 +2051,7 @@ int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, 
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c; p.K = ksize * ksize * c;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   SRPDE_CHECK_ARG((long long)p.P * c * 4 < (1LL << 31) && 2LL * cout * p.K * 2 < (1LL << 31),
                   "srpde_conv_fwd_h3_presplit: tensor too large");
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
@@ -2143,6 +2075,7 @@ int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, 
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
   }
+  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, true, stream, workspace, ws_bytes);
   const int bn = h3_bn(h3_cfg(cout));
   SRPDE_CHECK_ARG(h3_lds(bn, a.arows, 1, false, true) <= 160 * 1024, "srpde_conv_fwd_h3_presplit: LDS (w=%d dil=%d)", w,
                   dil);
@@ -2185,7 +2118,7 @@ int srpde_conv_dgrad_h3_bnb(const float* da, int ldda, const unsigned* dy_amax, 
   p.stats = nullptr;
   p.N = n; p.H = h; p.W = w; p.Cout = cin_dx; p.ksize = 3; p.dil = dil; p.sign = -1; p.accumulate = 0;
   p.P = n * h * w; p.Cin = cout_dy; p.K = 9 * p.Cin;
-  p.ntail = 0; p.tsplit = 1; p.part = nullptr; p.dbg = 0;
+  p.ntail = 0; p.tsplit = 1; p.part = nullptr;
   SRPDE_CHECK_ARG((long long)p.P * std::max(ldda, bn_ldy_in) * 4 < (1LL << 31) && 2LL * cin_dx * p.K * 2 < (1LL << 31),
                   "srpde_conv_dgrad_h3_bnb: tensor too large");
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && bn_ldy % 4 == 0 &&

@@ -16,6 +16,7 @@
 //               block re-reduces the previous launch's partials in the same order, so all
 //               blocks agree on alpha/beta without a grid barrier or host round trip.
 //               A sticky per-problem `done` flag makes extra launches no-ops.
+#include <atomic>
 #include "common.h"
 
 #include <vector>
@@ -354,7 +355,15 @@ __device__ __forceinline__ void write_part_ag(double v, double* sh, double* dst)
   }
 }
 
-// epoch `epoch` (1, 2, ...) of the grid barrier; false on abort (a wait past ~1 s)
+// epoch `epoch` (1, 2, ...) of the grid barrier; false on abort (a wait past ~1 s, or the abort word
+// set before the launch by srpde_poisson_debug_abort).
+// Memory-model assumption: the barrier pairs `s_waitcnt vmcnt(0)` after each thread's
+// sc1 (L2-bypassing, agent-scope relaxed) stores with sc1 loads after the barrier, instead of an
+// agent-scope release / acquire.  That is correct on gfx950 because every byte handed between blocks
+// is written and read ONLY through those agent-scope atomics (st_ag / ld_ag), which are served by the
+// coherent memory side and never by a CU's L1 or an XCD's L2 (MI355X_MICROARCH.md, "Valid forms":
+// sc1 stores drained by vmcnt + sc1 loads behind a counter poll); it is not a guarantee of the HIP
+// memory model, and a port to another target must restore the release / acquire fences.
 __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long epoch, int* sflag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores have landed
   __syncthreads();
@@ -367,8 +376,9 @@ __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long 
     const unsigned long long target = epoch * (unsigned long long)g.ngrp;
     int ab = 0;
     for (unsigned spins = 0;; ++spins) {
-      if (__hip_atomic_load(g.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      // the abort word first: once any block has given up, nobody passes another barrier
       if (__hip_atomic_load(g.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ab = 1; break; }
+      if (__hip_atomic_load(g.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
       if (spins > (1u << 24)) {
         __hip_atomic_store(g.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab = 1;
@@ -646,11 +656,17 @@ static int coop_capacity() {
   return cap;
 }
 
-// Problems per cooperative launch at this n (0: one problem does not fit the co-resident grid)
+// Problems per cooperative launch at this n (0: one problem does not fit the co-resident grid, or
+// n > GCG_PTS: the kernel's stencil takes the neighbours at i -+ n from the adjacent block only)
 int srpde_poisson_coop_problems(int n) {
+  if (n > GCG_PTS) return 0;
   const long long nb = ceil_div((long long)n * n, GCG_PTS);
   return nb <= coop_capacity() ? (int)(coop_capacity() / nb) : 0;
 }
+
+// test hook: every cooperative grid-CG launch starts with its abort word set (iters = -1 for every
+// problem of the launch, u undefined), so a caller's abort handling can be exercised
+static std::atomic<int> g_debug_abort{0};
 
 // the whole grid CG of problems [b0, b0 + cnt) in one cooperative launch (workspace carved for B)
 static int coop_solve(const double* f, const double* theta, double* u, int* iters, int b0, int cnt, int B, int n,
@@ -665,6 +681,8 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   g.bar = coop_ctl(ws, B, n);
   g.ctl = reinterpret_cast<unsigned*>(g.bar + 1 + g.ngrp);
   hipError_t e = hipMemsetAsync(g.bar, 0, (g.ngrp + 2) * sizeof(unsigned long long), stream);
+  if (e == hipSuccess && g_debug_abort.load(std::memory_order_relaxed))
+    e = hipMemsetAsync(g.ctl + 1, 0x01, 1, stream);
   if (e != hipSuccess) { set_error("srpde_poisson_cg_batched: memset: %s", hipGetErrorString(e)); return (int)e; }
   const double* fb = f + b0 * N2;
   const double* tb = theta + b0 * N2;
@@ -679,6 +697,8 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   }
   return 0;
 }
+
+int srpde_poisson_debug_abort(int on) { return g_debug_abort.exchange(on ? 1 : 0); }
 
 // One entry for any n (SURVEY 8(b)'s srpde_poisson_cg_batched), stream-ordered: n <= 128 is one
 // launch of the LDS-resident CG; n > 128 runs the grid CG as cooperative launches (one per group of

@@ -112,6 +112,12 @@ def set_h3r(on: bool) -> bool:
     return bool(query("srpde_conv_h3r_set", int(bool(on))))
 
 
+def set_h4(on: bool) -> bool:
+    """Kernel choice for 128-column h3 tiles at W = 10 / 20: the h4 kernel (conv_h4.hip) or the h3
+    8-wave one (bit-identical).  Returns the previous choice."""
+    return bool(query("srpde_conv_h4_set", int(bool(on))))
+
+
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
     return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, ksize))
 

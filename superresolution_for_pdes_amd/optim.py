@@ -121,6 +121,11 @@ class FusedAdamW(torch.optim.Optimizer):
             self.clip_grad_norm_(mgn, grad_scale)
         coef = self._coef if getattr(self, "_pending", False) else None
         self._pending = False
+        if coef is not None and coef.is_cuda:
+            # the next clip_grad_norm_ replaces (frees) this buffer: if this step runs on another
+            # stream than the one that allocated it, the caching allocator must not hand its memory
+            # out again before this stream's update kernel has read it
+            coef.record_stream(torch.cuda.current_stream(coef.device))
         _STEPS[0] += 1
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]

@@ -37,9 +37,19 @@ def forcing_batched(k12, n: int, device="cuda"):
     return out
 
 
+class GridBarrierAbort(RuntimeError):
+    """A cooperative grid-CG launch gave up at a grid barrier (iters = -1): its u is not a solution."""
+
+
 def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, device="cuda",
-                  return_iters: bool = False):
-    """u[B, n, n] (float64, on device) with theta*Lap(u) = f per problem."""
+                  return_iters: bool = False, check: bool = True):
+    """u[B, n, n] (float64, on device) with theta*Lap(u) = f per problem.
+
+    For n above the LDS solver's limit the solve runs as cooperative launches whose grid barriers
+    abort after ~1 s of waiting (srpde_poisson_cg_batched marks those problems iters = -1 and
+    leaves u unconverged).  ``check`` (default) reads the iteration counts back -- one host sync,
+    only on that path, not under stream capture -- and raises GridBarrierAbort instead of returning
+    such a u (every data-generation caller otherwise consumed it silently)."""
     f = _dev_f64(f, device)
     theta = _dev_f64(theta, device)
     if f.dim() == 2:
@@ -59,6 +69,11 @@ def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, devic
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
     call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),
          iters.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
+    if check and n > int(query("srpde_poisson_lds_max_n")) and not torch.cuda.is_current_stream_capturing():
+        bad = int((iters < 0).sum())
+        if bad:
+            raise GridBarrierAbort(f"srpde_poisson_cg_batched: {bad} of {B} problems (n={n}) aborted at a grid "
+                                   "barrier; their u is not a solution")
     return (u, iters) if return_iters else u
 
 

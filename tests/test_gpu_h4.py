@@ -1,0 +1,105 @@
+"""The h4 convolution kernel (conv_h4.hip) against the h3 8-wave kernel it replaces for 128-column
+tiles at W = 10 (dilation 1 and 2) and W = 20: same fragments, products, accumulation order and
+epilogue, so every output must be EQUAL bit for bit -- forward (bias, BN statistics, stored input
+split, fused input BN + ReLU, virtual concat, the K-split tail), the eval-mode epilogue (BN + ReLU,
+max|y| word), the dgrad from an fp32 dy (stored dy split, fused BN-backward partials, per-tile
+max|dx|) and the dgrad from a pre-split dy.  The layer shapes are the U-Net's
+(src/models.py:16-19, 43-49: enc2 / dec2 at 20x20, enc3 / bridge / dec3 at 10x10)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,hw,dil", [
+    (9, 128, 0, 128, 20, 1),      # enc2.conv2 / dec2.conv2 (fused input BN + ReLU)
+    (7, 256, 128, 128, 20, 1),    # dec2.conv1 (virtual concat)
+    (21, 128, 0, 256, 10, 1),     # enc3.conv1
+    (13, 512, 256, 256, 10, 1),   # dec3.conv1 (virtual concat)
+    (11, 256, 0, 512, 10, 2),     # bridge.0
+    (170, 512, 0, 512, 10, 2),    # bridge.3 with a K-split tail (268 tiles on 256 CUs)
+    (2, 64, 64, 128, 20, 1),      # a partial last row tile, two 32-channel chunks per input
+])
+def test_conv_h4_equals_h3(n, c0, c1, cout, hw, dil):
+    from superresolution_for_pdes_amd import hipops as H
+    if H.conv_math() != "h3":
+        pytest.skip("h3 kernels off")
+    cin = c0 + c1
+    g = torch.Generator(device=DEV).manual_seed(7)
+    P = n * hw * hw
+    x = torch.randn(P, cin, device=DEV, generator=g)
+    x0, x1 = (x[:, :c0], x[:, c0:]) if c1 else (x, None)
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, wd = H.pack_conv_weights(w, cin, True, True)
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    by = torch.randn(P, cin, device=DEV, generator=g)
+    bmean, binv = torch.randn(cin, device=DEV, generator=g) * 0.1, torch.rand(cin, device=DEV, generator=g) + 0.5
+    bga, bbe = torch.randn(cin, device=DEV, generator=g), torch.randn(cin, device=DEV, generator=g) * 0.1
+    emean, einv = torch.randn(cout, device=DEV, generator=g) * 0.1, torch.rand(cout, device=DEV, generator=g) + 0.5
+    ega, ebe = torch.randn(cout, device=DEV, generator=g), torch.randn(cout, device=DEV, generator=g) * 0.1
+    for t in (x0, x1, dy):
+        if t is not None:
+            t._srpde_amax = H.amax_of(t)
+    aff = None
+    if c1 == 0:
+        aff = (torch.rand(c0, device=DEV, generator=g) + 0.5, torch.randn(c0, device=DEV, generator=g) * 0.2)
+    outs = []
+    prev = H.set_h4(True)
+    try:
+        for on in (False, True):
+            H.set_h4(on)
+            y = torch.empty(P, cout, device=DEV)
+            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, dil)
+            xp = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp, in_affine=aff)
+            ye = torch.empty(P, cout, device=DEV)
+            eam = torch.zeros(1, dtype=torch.int32, device=DEV)
+            H.conv_fwd(x0, x1, wf, b, ye, n, hw, hw, cout, 3, dil, 1, False, None, ep_bn=(emean, einv, ega, ebe, eam))
+            dx = torch.empty(P, cin, device=DEV)
+            dyp = H.split_planes_buffer(P, cout, DEV)
+            part = H.bn_bwd_partials(n, hw, hw, cin, DEV)
+            dmax = H.out_max_slots(n, hw, hw, cout, cin, dil, DEV)
+            H.conv_fwd(dy, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp,
+                       bn_bwd=(by, bmean, binv, bga, bbe, part), out_max=dmax)
+            dx2 = torch.empty(P, cin, device=DEV)
+            part2 = H.bn_bwd_partials(n, hw, hw, cin, DEV)
+            dmax2 = H.out_max_slots(n, hw, hw, cout, cin, dil, DEV)
+            H.conv_fwd_presplit(dyp, wd, None, dx2, n, hw, hw, cin, 3, dil, -1, False, None,
+                                bn_bwd=(by, bmean, binv, bga, bbe, part2), out_max=dmax2)
+            torch.cuda.synchronize()
+            outs.append((y, stats, xp, ye, eam, dx, dyp, part, dmax, dx2, part2, dmax2))
+    finally:
+        H.set_h4(prev)
+    names = ("y", "stats", "xsplit", "y_eval", "amax_eval", "dx", "dysplit", "bn_part", "dx_max", "dx_presplit",
+             "bn_part_presplit", "dx_max_presplit")
+    for name, a, b_ in zip(names, *outs):
+        assert torch.equal(a, b_), name
+    # the pre-split dgrad reads the same pieces the fp32 one split: equal outputs as well
+    assert torch.equal(outs[1][5], outs[1][9])
+
+
+def test_conv_h4_accumulate_and_strided_output():
+    """accumulate=1 into a channel slice of a wider output (the dgrad into a virtual-concat input)."""
+    from superresolution_for_pdes_amd import hipops as H
+    n, cin, cout, hw = 6, 256, 128, 10
+    g = torch.Generator(device=DEV).manual_seed(3)
+    P = n * hw * hw
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    _, wd = H.pack_conv_weights(w, cin, True, True)
+    dy._srpde_amax = H.amax_of(dy)
+    base = torch.randn(P, cin + 128, device=DEV, generator=g)
+    outs = []
+    prev = H.set_h4(True)
+    try:
+        for on in (False, True):
+            H.set_h4(on)
+            big = base.clone()
+            H.conv_fwd(dy, None, wd, None, big[:, 64:64 + cin], n, hw, hw, cin, 3, 1, -1, True)
+            torch.cuda.synchronize()
+            outs.append(big)
+    finally:
+        H.set_h4(prev)
+    assert torch.equal(outs[0], outs[1])
