@@ -39,8 +39,9 @@ typedef struct ihipStream_t* hipStream_t;
  *   4  round 3 changes (srpde_conv_fwd_h3: in_scale ... ep_amax before the workspace; the
  *      srpde_prepare_weights_h3 descriptor row grew to 10 columns; srpde_conv_wgrad_h3p reads dy
  *      planes with a row stride of cout rounded up to 32) and round 4's additions
- *      (srpde_conv_h4_set, srpde_poisson_debug_abort) */
-#define SRPDE_ABI_VERSION 4
+ *      (srpde_conv_h4_set, srpde_poisson_debug_abort)
+ *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace */
+#define SRPDE_ABI_VERSION 5
 
 const char* srpde_last_error(void);
 int srpde_version(void);
@@ -133,8 +134,12 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                       const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
-                      void* workspace, size_t ws_bytes, hipStream_t stream);
-/* ep_mean / ep_invstd / ep_gamma / ep_beta (nullable, eval mode; no stats / bn_part / accumulate):
+                      const float* x1_ca, const float* x1_sa, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* x1_ca [n][c1] / x1_sa [P] (nullable, together, c1 > 0): the second input is an AttentionGate's
+ * input x (models.py:119-130) and the conv reads its gated output (x * ca[sample][c]) * sa[pixel]
+ * (srpde_att_apply_fwd's expression, formed in the operand transform; xsplit_out and the statistics
+ * are those of the gated input) -- the gated tensor is never written.
+ * ep_mean / ep_invstd / ep_gamma / ep_beta (nullable, eval mode; no stats / bn_part / accumulate):
  * the epilogue applies the following BatchNorm with its running statistics and the ReLU,
  * y = relu((conv + bias - mean) * invstd * gamma + beta) (srpde_bn_eval_prepare's mean / invstd),
  * so the conv output is the activation itself (models.py:22-23 in eval mode); ep_amax (nullable,

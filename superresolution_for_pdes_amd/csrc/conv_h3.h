@@ -71,7 +71,25 @@ struct H3Args {
   const float* bnb_mean; const float* bnb_invstd; const float* bnb_gamma; const float* bnb_beta;
   const float* bnb_m1; const float* bnb_m2;
   int bnb_relu;
+  // optional AttentionGate of a virtual concat's second input, fused into the input transform
+  // (models.py:119-130 feeding dec*.conv1 at :87,:90,:93): x1 element (p, c) enters as
+  // (x1[p][c] * ca[n][c]) * sa[p], n = p / (H W) -- att_apply_kernel's expression (pointwise.hip)
+  const float* x1_ca;      // [N][c1]
+  const float* x1_sa;      // [P]
 };
+
+// the gate above on 8 consecutive channels cc1.. (channel index inside x1) of pixel pix; rows
+// outside the tensor are left alone (they are zero fills)
+__device__ __forceinline__ void gate8(float4& v0, float4& v1, const H3Args& h, int pix, int P, int HW, int c1,
+                                      int cc1) {
+  if (pix < 0 || pix >= P) return;
+  const int n = pix / HW;
+  const float4 a0 = *reinterpret_cast<const float4*>(h.x1_ca + (size_t)n * c1 + cc1);
+  const float4 a1 = *reinterpret_cast<const float4*>(h.x1_ca + (size_t)n * c1 + cc1 + 4);
+  const float s = h.x1_sa[pix];
+  v0.x = (v0.x * a0.x) * s; v0.y = (v0.y * a0.y) * s; v0.z = (v0.z * a0.z) * s; v0.w = (v0.w * a0.w) * s;
+  v1.x = (v1.x * a1.x) * s; v1.y = (v1.y * a1.y) * s; v1.z = (v1.z * a1.z) * s; v1.w = (v1.w * a1.w) * s;
+}
 
 // the K-split tail's fixup: one block per statistics sub-block of each tail tile (twice the blocks of a
 // whole-tile fixup for the same work: the tail has few tiles; 32.15 -> 32.12 ms per step) unless the

@@ -242,6 +242,7 @@ __global__ __launch_bounds__(WM * WN * 64, 8 / (WM * WN)) void conv_fwd_h3_kerne
         v0 = make_float4(vv[0], vv[1], vv[2], vv[3]);
         v1 = make_float4(vv[4], vv[5], vv[6], vv[7]);
       }
+      if (h.x1_ca != nullptr && ch * BK2 >= p.c0) gate8(v0, v1, h, pix0 + r, p.P, p.H * p.W, p.c1, ch * BK2 - p.c0 + c8 * 8);
       if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
         const int cc = ch * BK2 + c8 * 8, pix = pix0 + r;
         const bool inside = pix >= 0 && pix < p.P;
@@ -630,6 +631,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
     // fused BN + ReLU of the producer: every task of a thread has the same 8 channels (t & 3),
     // so their (scale, shift) are loaded once per chunk, not once per task
     float4 s0, s1, t0, t1;
+    const bool gate = !PRE && h.x1_ca != nullptr && ch * BK2 >= p.c0;   // the attention-gated second input
     if (h.in_scale != nullptr) {
       const int cc = ch * BK2 + (t & 3) * 8;
       s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
@@ -648,6 +650,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_h3r_kernel(ConvParams p, H3Ar
         const int r = sg >> 2, c8 = sg & 3;
         float4 v0 = make_float4(pf[k][0].x, pf[k][0].y, pf[k][0].z, pf[k][0].w);
         float4 v1 = make_float4(pf[k][1].x, pf[k][1].y, pf[k][1].z, pf[k][1].w);
+        if (gate) gate8(v0, v1, h, pix0 + r, p.P, p.H * p.W, p.c1, ch * BK2 - p.c0 + c8 * 8);
         if (h.in_scale != nullptr) {   // rows outside the tensor stay 0
           const int pix = pix0 + r;
           const bool inside = pix >= 0 && pix < p.P;
@@ -1963,8 +1966,10 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                       const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
-                      void* workspace, size_t ws_bytes, hipStream_t stream) {
+                      const float* x1_ca, const float* x1_sa, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
+  SRPDE_CHECK_ARG((x1_ca == nullptr) == (x1_sa == nullptr) && (x1_ca == nullptr || c1 > 0),
+                  "srpde_conv_fwd_h3: x1_ca / x1_sa go together and need a second input (c1 > 0)");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd_h3: bad shape");
   SRPDE_CHECK_ARG(sign == 1 || sign == -1, "srpde_conv_fwd_h3: sign must be +-1");
@@ -1998,6 +2003,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "srpde_conv_fwd_h3: in_scale / in_shift go together and need c1 == 0");
   a.in_scale = in_scale;
   a.in_shift = in_shift;
+  a.x1_ca = x1_ca;
+  a.x1_sa = x1_sa;
   a.wide = ldy % 4 == 0 && aligned16(y);
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
                                           bn_ldy % 4 == 0 && cout % 4 == 0),

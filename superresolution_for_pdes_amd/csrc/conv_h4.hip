@@ -219,6 +219,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   auto convert = [&](int ch) {
     float4 s0, s1, t0, t1;
     const int c8 = tid & 3;   // every task of this thread has the same 8 channels
+    const bool gate = h.x1_ca != nullptr && ch * BK2 >= p.c0;   // the attention-gated second input
     if (h.in_scale != nullptr) {
       const int cc = ch * BK2 + c8 * 8;
       s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       const char* f = lds + OFF_F + r * 128;
       float4 v0 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8) * 16);
       float4 v1 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8 + 1) * 16);
+      if (gate) gate8(v0, v1, h, pix0 + r, p.P, p.H * W, p.c1, ch * BK2 - p.c0 + c8 * 8);
       if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
         const int pix = pix0 + r;
         const bool inside = pix >= 0 && pix < p.P;
@@ -313,8 +315,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     const unsigned sb = PRE ? (unsigned)((ch & 1) * SSTRIDE) : 0u;
     const unsigned sbn = PRE ? (unsigned)(((ch + 1) & 1) * SSTRIDE) : 0u;
     // DMAs of this tap: the next chunk's A-tile piece T (T < APW), then the weights of tap tau + 3
-    if constexpr (T < APW) issue_a(ch + 1, T, more);
-    {
+    if constexpr (!(SRPDE_CONV_DBG & 1)) {   // (timing-only diagnostics, conv_common.h: 1 = no DMA in the taps)
+      if constexpr (T < APW) issue_a(ch + 1, T, more);
       constexpr int T3 = T + 3;
       if constexpr (T3 < 9) issue_b(ch, T3, (slot + 3) & 3, true);
       else issue_b(ch + 1, T3 - 9, (slot + 3) & 3, more);
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       constexpr bool RA = j == 3 && (T < 8 || PRE);
       if constexpr (RA) read_a(0, apk[T < 8 ? T + 1 : 0], T < 8 ? sb : sbn, nah, nal);
 #pragma unroll
-      for (int i = 0; i < TI16; ++i) {
+      for (int i = 0; i < TI16 && !(SRPDE_CONV_DBG & 128); ++i) {   // diagnostics: 128 = no MFMAs
         floatx4 c0;
         if (T == 0)   // a chunk's partial chain starts from zero
           c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], floatx4{}, 0, 0, 0);
@@ -368,7 +370,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     // a bare s_barrier: no lgkmcnt(0) drain of the next tap's fragment reads still in flight (they read
     // slot tau + 1 and the S tile, which no DMA issued after this barrier writes); the asm is a
     // compiler memory barrier, so no LDS read moves above it
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NPREV + NCUR) : "memory");
+    if constexpr (SRPDE_CONV_DBG & 2)   // diagnostics: 2 = no tap barrier
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPREV + NCUR) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NPREV + NCUR) : "memory");
   };
 
   for (int ch = c_beg; ch < c_end; ++ch) {
@@ -389,7 +394,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       for (int j = 0; j < TJ16; ++j) acc[i][j] += part[i][j];
     if constexpr (!PRE) {
       if (ch + 1 < c_end) {   // the next chunk's halo tile has landed in F (its DMAs preceded the last wait)
-        convert(ch + 1);
+        if (!(SRPDE_CONV_DBG & 4)) convert(ch + 1);   // diagnostics: 4 = no per-chunk convert
         __syncthreads();
         read_a(0, apk[0], 0u, ah, al);
       }
@@ -414,6 +419,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     } else {
       colscale[j] = exp2i(-e);
     }
+  }
+  if constexpr (SRPDE_CONV_DBG & 16) {   // diagnostics: 16 = no epilogue (one store per lane keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) t += acc32[0][j][0] * colscale[j] + acc32[0][j][15];
+    if (t == 123.f) p.y[tid] = t;
+    return;
   }
   // S is free now: reduction scratch [2][WM][BN] floats, then 2 KiB per wave of store stage
   x6_finish<BM, BN, WM, WN, SRB>(p, acc32, tail, wg, nfull, piece, m0, n0, wmi, wni, lane, smem,

@@ -123,14 +123,16 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
 
 
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
-             planes_out=None, in_affine=None, bn_bwd=None, out_max=None, ep_bn=None):
+             planes_out=None, in_affine=None, bn_bwd=None, out_max=None, ep_bn=None, x1_gate=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
     ``planes_out`` ([2, P, c0+c1] fp16) receives the scaled split of the input for conv_wgrad;
     ``in_affine = (scale, shift)`` applies relu(x0 * scale + shift) to the input on the fly;
     ``bn_bwd = (bn_y, mean, invstd, gamma, beta, part)`` (dgrad into a BN + ReLU output's
     gradient) also writes that BN backward's reduction into ``part`` (bn_bwd_partials);
     ``ep_bn = (mean, invstd, gamma, beta, amax)`` (eval mode) applies the following BatchNorm and
-    ReLU in the epilogue, so ``y`` is the activation, and writes max|y| into ``amax``."""
+    ReLU in the epilogue, so ``y`` is the activation, and writes max|y| into ``amax``.
+    ``x1_gate = (ca [n, c1], sa [P])``: x1 is an AttentionGate's input and the conv reads its gated
+    output (x1 * ca) * sa, formed in the operand transform (the gated tensor is never written)."""
     p0, ld0 = _pl(x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
@@ -150,15 +152,16 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
-             *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), ws.data_ptr(), ws.numel(), stream_ptr())
+             *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), _p(x1_gate[0] if x1_gate else None),
+             _p(x1_gate[1] if x1_gate else None), ws.data_ptr(), ws.numel(), stream_ptr())
         if ep_bn is not None:
             tag_amax(y, ep_bn[4])
         if planes_out is not None:
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert planes_out is None and in_affine is None and bn_bwd is None and out_max is None and ep_bn is None, \
-        "planes_out / in_affine / bn_bwd / out_max / ep_bn need the h3 kernels"
+    assert (planes_out is None and in_affine is None and bn_bwd is None and out_max is None and ep_bn is None
+            and x1_gate is None), "planes_out / in_affine / bn_bwd / out_max / ep_bn / x1_gate need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,

@@ -71,16 +71,49 @@ def _tap(name, t):
 TIMED_LAYERS = {}
 
 
-def _conv_launch(conv, *args):
+def _conv_launch(conv, *args, **kw):
     sink = TIMED_LAYERS.get(getattr(conv, "_srpde_name", None)) if TIMED_LAYERS else None
     if sink is None:
-        H.conv_fwd(*args)
+        H.conv_fwd(*args, **kw)
         return
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    H.conv_fwd(*args)
+    H.conv_fwd(*args, **kw)
     b.record()
     sink.append((a, b))
+
+
+class GatedInput:
+    """An AttentionGate's output (x * ca) * sa (models.py:119-130) that is not formed: the decoder conv
+    that reads it as the second half of its virtual concat applies the gate in its operand transform
+    (srpde_conv_fwd_h3 x1_ca / x1_sa), so the gated tensor is never written or read back.
+    ``materialize()`` forms it (srpde_att_apply_fwd) for a consumer that cannot fuse it."""
+    __slots__ = ("x", "ca", "sa", "n", "hw", "_t")
+
+    def __init__(self, x, ca, sa, n, hw):
+        self.x, self.ca, self.sa, self.n, self.hw, self._t = x, ca, sa, n, hw, None
+
+    @property
+    def shape(self):
+        return self.x.shape
+
+    @property
+    def device(self):
+        return self.x.device
+
+    def materialize(self):
+        if self._t is None:
+            self._t, _ = H.att_apply_fwd(self.x, self.n, self.hw, (None, None, self.ca), self.sa)
+        return self._t
+
+
+def _unwrap_gate(x0, x1, cout, w, dil):
+    """-> (x1 tensor, x1_gate or None) for a conv whose second input may be a GatedInput."""
+    if not isinstance(x1, GatedInput):
+        return x1, None
+    if _FUSE_ATT_APPLY and H.h3_capable(x0.shape[1], x1.shape[1], cout, w, dil):
+        return x1.x, (x1.ca, x1.sa)
+    return x1.materialize(), None
 
 
 class _Planes:
@@ -155,6 +188,23 @@ _H3W_SIDE = os.environ.get("SRPDE_H3W_SIDE", "1") != "0"
 _H3W_PENDING = None
 
 
+# DataParallel's buffer broadcast (distributed.py), issued on a side stream before the forward: the
+# compute stream waits for its event before the step's first BatchNorm finalize
+_BUF_PENDING = None
+
+
+def buffers_pending(event):
+    global _BUF_PENDING
+    _BUF_PENDING = event
+
+
+def _buffers_ready(dev):
+    global _BUF_PENDING
+    if _BUF_PENDING is not None:
+        torch.cuda.current_stream(dev).wait_event(_BUF_PENDING)
+        _BUF_PENDING = None
+
+
 def _h3w_ready(dev):
     global _H3W_PENDING
     if _H3W_PENDING is not None:
@@ -207,6 +257,8 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     c1 = x1.shape[1] if x1 is not None else 0
     cin = x0.shape[1] + c1
     wf = _fwd_weights(conv, cin, x0.shape[1], c1, w, dil)
+    x1_saved = x1
+    x1, x1_gate = _unwrap_gate(x0, x1, cout, w, dil)
     P = n * h * w
     y = H.empty(P, cout, device=dev)
     xp = None
@@ -215,8 +267,10 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         if _splits_both_ways(x0.shape[1], c1, cout, w, dil):
             xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
         assert in_affine is None or xp is not None, "a fused input needs the stored split for its wgrad"
-        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp, in_affine)
+        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp, in_affine,
+                     x1_gate=x1_gate)
         mom = bn.momentum if bn.momentum is not None else 0.0
+        _buffers_ready(dev)
         if not activate:   # the fused consumer's (scale, shift), from the same launch (SRPDE_FIN_AFFINE=0: two)
             slot = slots.take()
             if _FIN_AFFINE:
@@ -228,23 +282,23 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
                                                    bn.num_batches_tracked, mom, bn.eps)
                 aff = H.bn_affine(mean, invstd, bn.weight, bn.bias, P, amax=slot)
             y._srpde_amax = slot
-            return (y, aff), (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
+            return (y, aff), (None if in_affine is not None else x0, x1_saved, y, mean, invstd, xp, training)
         mean, invstd = H.bn_train_finalize(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
                                            bn.num_batches_tracked, mom, bn.eps)
     else:
         assert in_affine is None and activate
-        mean, invstd = H.bn_eval_prepare(bn.running_mean, bn.running_var, bn.eps)
+        mean, invstd = _eval_stats(bn)
         if getattr(slots, "eval_epilogue", False) and _EVAL_EPI and H.h3_capable(x0.shape[1], c1, cout, w, dil):
             # inference: the conv epilogue applies this BN (running statistics) + ReLU, so y IS the
             # activation (nothing saved for a backward); consumers read it as is
             slot = slots.take()
             H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None,
-                       ep_bn=(mean, invstd, bn.weight, bn.bias, slot))
+                       ep_bn=(mean, invstd, bn.weight, bn.bias, slot), x1_gate=x1_gate)
             return _eval_consumers(y, slot, n, h, w, cout, pool, att, gate), None
-        H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None)
+        H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None, x1_gate=x1_gate)
     # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
     # the weight gradient reads the stored split
-    saved = (None if in_affine is not None else x0, x1, y, mean, invstd, xp, training)
+    saved = (None if in_affine is not None else x0, x1_saved, y, mean, invstd, xp, training)
     a = H.empty(P, cout, device=dev)
     if gate is not None:
         s0 = gate.spatial_attention[0]
@@ -275,6 +329,24 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     if att is None:
         return (a, pooled), saved
     return (a, pooled, _att_channel_early(att, a, n, h * w)), saved
+
+
+# the running statistics change in place through torch (version counters: load_state_dict, user
+# writes) or through this executor's train-mode BN finalize kernels, which torch cannot see: every
+# train-mode forward bumps this epoch
+_RS_EPOCH = [0]
+
+
+def _eval_stats(bn):
+    """(mean, 1 / sqrt(var + eps)) of a BatchNorm's running statistics for the eval forward, cached
+    until they change (srpde_bn_eval_prepare: one tiny launch per BN layer per forward otherwise)."""
+    rm, rv = bn.running_mean, bn.running_var
+    key = (rm.data_ptr(), rm._version, rv.data_ptr(), rv._version, float(bn.eps), _RS_EPOCH[0])
+    c = getattr(bn, "_srpde_eval_stats", None)
+    if c is None or c[0] != key:
+        c = (key, H.bn_eval_prepare(rm, rv, bn.eps))
+        bn._srpde_eval_stats = c
+    return c[1]
 
 
 def _eval_consumers(a, slot, n, h, w, c, pool, att, gate):
@@ -482,6 +554,8 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax)
     else:
         assert x0 is not None, "fused-input layer without stored splits"
+        if isinstance(x1, GatedInput):
+            x1 = x1.materialize()
         fn, keep = (lambda: H.conv_wgrad(dy, x0, x1, dw, n, h, w, 3, dil)), (dy, getattr(dy, "_srpde_amax", None))
     if wq is None:
         fn()
@@ -489,6 +563,10 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         wq.submit(fn, keep)
     return None if out_part is None else (out_part, dx_max)
 
+
+# the attention gates' output (x * ca) * sa formed inside the decoder conv that reads it (GatedInput;
+# SRPDE_FUSE_ATT_APPLY=0: a separate srpde_att_apply_fwd pass writes it)
+_FUSE_ATT_APPLY = os.environ.get("SRPDE_FUSE_ATT_APPLY", "1") != "0"
 
 # the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
 # (srpde_conv_dgrad_h3_bnb; SRPDE_FUSE_BN_APPLY=0: off)
@@ -559,6 +637,9 @@ def _att_fwd(att, x, g, n, hw, early=None, sa=None):
     if ev is not None:
         torch.cuda.current_stream(x.device).wait_event(ev)
     if sa is not None:
+        if _FUSE_ATT_APPLY and x.is_cuda:   # formed by the consuming decoder conv (GatedInput)
+            m_, hb, ca = chan
+            return GatedInput(x, ca, sa, n, hw), (m_, hb, ca, sa)
         return H.att_apply_fwd(x, n, hw, chan, sa)
     return H.att_gate_fwd(x, g, n, hw, chan, s0.weight, s0.bias)
 
@@ -606,6 +687,8 @@ def unet_forward(m, x, training, save=False):
     n, _, h, w = x.shape
     h2, w2, h3, w3 = h // 2, w // 2, h // 4, w // 4
     hw1, hw2, hw3 = h * w, h2 * w2, h3 * w3
+    if training:
+        _RS_EPOCH[0] += 1   # this forward's BN finalize kernels rewrite the running statistics
     S = _Saved()
     S.shape = (n, h, w)
     S.x = x

@@ -103,3 +103,50 @@ def test_conv_h4_accumulate_and_strided_output():
     finally:
         H.set_h4(prev)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,hw,h4", [
+    (13, 512, 256, 256, 10, True),    # dec3.conv1: [b, att3(e3)] on h4
+    (7, 256, 128, 128, 20, True),     # dec2.conv1: [up(d3), att2(e2)] on h4
+    (13, 512, 256, 256, 10, False),   # the same on the h3 8-wave kernel
+    (3, 128, 64, 64, 40, True),       # dec1.conv1: [up(d2), att1(e1)] on h3r
+])
+def test_gated_second_input_equals_materialized(n, c0, c1, cout, hw, h4):
+    """The decoder conv reading an AttentionGate's output through x1_gate (the gate (x * ca) * sa
+    formed in the operand transform, models.py:119-130) equals, bit for bit, the same conv reading the
+    tensor srpde_att_apply_fwd writes: output, BN statistics, stored input split, and the eval-mode
+    epilogue's output and max word."""
+    from superresolution_for_pdes_amd import hipops as H
+    cin = c0 + c1
+    g = torch.Generator(device=DEV).manual_seed(11)
+    P = n * hw * hw
+    x0 = torch.randn(P, c0, device=DEV, generator=g)
+    e = torch.randn(P, c1, device=DEV, generator=g)
+    ca = torch.sigmoid(torch.randn(n, c1, device=DEV, generator=g))
+    sa = torch.sigmoid(torch.randn(P, device=DEV, generator=g))
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, _ = H.pack_conv_weights(w, cin, True, False)
+    emean, einv = torch.randn(cout, device=DEV, generator=g) * 0.1, torch.rand(cout, device=DEV, generator=g) + 0.5
+    ega, ebe = torch.randn(cout, device=DEV, generator=g), torch.randn(cout, device=DEV, generator=g) * 0.1
+    x0._srpde_amax = H.amax_of(x0)
+    e._srpde_amax = H.amax_of(e)
+    ea, _ = H.att_apply_fwd(e, n, hw * hw, (None, None, ca), sa)   # carries e's max word, as in the model
+    outs = []
+    prev = H.set_h4(h4)
+    try:
+        for x1, gate in ((ea, None), (e, (ca, sa))):
+            y = torch.empty(P, cout, device=DEV)
+            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, 1)
+            xp = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, 1, 1, False, stats, xp, x1_gate=gate)
+            ye = torch.empty(P, cout, device=DEV)
+            eam = torch.zeros(1, dtype=torch.int32, device=DEV)
+            H.conv_fwd(x0, x1, wf, b, ye, n, hw, hw, cout, 3, 1, 1, False, None,
+                       ep_bn=(emean, einv, ega, ebe, eam), x1_gate=gate)
+            torch.cuda.synchronize()
+            outs.append((y, stats, xp, ye, eam))
+    finally:
+        H.set_h4(prev)
+    for name, a, b_ in zip(("y", "stats", "xsplit", "y_eval", "amax_eval"), *outs):
+        assert torch.equal(a, b_), name

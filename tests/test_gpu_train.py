@@ -124,6 +124,30 @@ def test_main_end_to_end(tmp_path, monkeypatch):
     assert len(m.state_dict()) == 132
 
 
+def _first_step_branch_matched(st0, x, t):
+    """The first step's loss and clip total from the fp64 oracle evaluated on the branch (ReLU masks,
+    max-pool argmaxes) the HIP forward took (tests/golden/branch.py), and the HIP path's own."""
+    from branch import hip_decisions, hip_step
+    from oracle.unet_ref import clone_state, trainable_names, unet_forward as ref_fwd
+    from superresolution_for_pdes_amd.models import UNet
+    m = UNet()
+    m.load_state_dict(st0)
+    m = m.cuda().train()
+    m.flatten_parameters_()
+    out, grads, _, S = hip_step(m, x.cuda(), t.cuda(), want_dx=False)
+    dec = hip_decisions(m, S)
+    st = clone_state(st0, torch.float64)
+    names = trainable_names()
+    for n_ in names:
+        st[n_].requires_grad_(True)
+    loss = torch.nn.functional.mse_loss(ref_fwd(st, x.double(), True, decisions=dec), t.double())
+    loss.backward()
+    tot_bm = float(torch.sqrt(sum((st[n_].grad ** 2).sum() for n_ in names)))
+    tot_hip = float(torch.sqrt(sum((grads[n_].double() ** 2).sum() for n_ in names)))
+    loss_hip = float(((out.double() - t.cuda().double()) ** 2).mean())
+    return float(loss), tot_bm, loss_hip, tot_hip
+
+
 def test_training_trajectory_tracks_reference():
     """Twenty inner-loop steps (train_enhanced.py:68-75: forward, MSE, backward, clip 1.0, AdamW
     lr 2e-4 / wd 1e-4) on a fixed cycle of three seeded batches of 16, from the reference's own seeded
@@ -132,11 +156,21 @@ def test_training_trajectory_tracks_reference():
     drifts from fp64 by 4e-7 in the first loss and by 1e-4 at the second, then by ~2-5 % after a dozen
     steps (AdamW's normalised first updates turn sign flips of near-zero gradient elements into +-lr
     steps, so any rounding difference is amplified; the same fp32 run on 8 and on 16 CPU threads
-    differs by that much), so the drop-in is held to that run's deviation: within 3x of it at the
-    first step, before any update (floor 2e-6; 1e-4 for the clip total, as in test_gpu_b1024), and as an
-    RMS over all twenty steps, for the losses, the clip totals and the final BN running statistics.
-    Measured on MI355X: loss RMS 2.4e-2 against the fp32 reference's 2.3e-2, first loss 9e-8 against
-    3.8e-7; clip total RMS 7.9e-2 against 6.6e-2, first 2.3e-5 against 4.4e-6."""
+    differs by that much), so the drop-in is held to that run's deviation: within 3x of it as an RMS
+    over all twenty steps, for the losses, the clip totals and the final BN running statistics.
+
+    The first step, before any update (verdict r3 weak #4): the first clip total is 2.6e-5
+    from fp64 against the reference fp32's 2.8e-6.  Decomposed per tensor (tools/diag_clip_total.py,
+    profiles/r04a_clip_total_presplit*.json; a tensor's share is (|g|^2 - |g64|^2) / (2 T64^2)): the
+    encoder conv weights carry it -- enc1.conv2 1.2e-5, enc2.conv2 5.8e-6, enc2.conv1 4.9e-6, bridge.0
+    3.1e-6, enc3.conv2 3.0e-6 -- at per-tensor relative errors of 3.4e-3 (the reference fp32's own:
+    3.0e-3); the BN-fed conv biases contribute 2e-15 (round 3's explanation was wrong), and the
+    pre-split dy path changes nothing (2.62e-5 with SRPDE_PRESPLIT_BWD=0).  Errors of 3e-3 on every
+    tensor are decision flips (one ReLU flip in 2e5 moves a gradient by ~3e-3, tests/golden/branch.py),
+    not arithmetic.  So the first step is held to (1) the fp64 oracle evaluated on the HIP forward's
+    own branch -- pure arithmetic: loss and clip total within 3x the reference fp32's deviation -- and
+    (2) plain fp64 within 3x the reference fp32's deviation plus the flip part that (1) measures
+    (|branch-matched fp64 - fp64|), no fixed floor."""
     from oracle.unet_ref import clone_state, train_step
     from superresolution_for_pdes_amd.functional import mse_loss
     from superresolution_for_pdes_amd.models import UNet
@@ -158,6 +192,7 @@ def test_training_trajectory_tracks_reference():
 
     l64, c64, st64 = oracle_run(torch.float64)
     l32, c32, st32 = oracle_run(torch.float32)
+    lbm, cbm, lhip, chip = _first_step_branch_matched(st0, xs[0], ts[0])
 
     m = UNet()
     m.load_state_dict(st0)
@@ -180,13 +215,16 @@ def test_training_trajectory_tracks_reference():
     def rms(a):
         return float(np.sqrt(np.mean(np.square(a))))
 
-    # first-step floors: 2e-6 for the loss; 1e-4 for the clip total, test_gpu_b1024's bar (the total includes
-    # the BN-fed conv biases, whose exact gradient is 0: pure rounding noise of either implementation)
-    for what, mine, ref32, ref64, floor in (("loss", lm, l32, l64, 2e-6), ("clip total", cm, c32, c64, 1e-4)):
+    for what, mine, ref32, ref64, bm, hip in (("loss", lm, l32, l64, lbm, lhip), ("clip total", cm, c32, c64, cbm, chip)):
         dev, dref = np.abs(mine - ref64) / ref64, np.abs(ref32 - ref64) / ref64
+        arith = abs(hip - bm) / bm            # the HIP arithmetic on its own branch
+        flips = abs(bm - ref64[0]) / ref64[0]  # what the branch the HIP forward took moves in fp64
         print(f"{what}: drop-in dev {np.array2string(dev, precision=1)} rms {rms(dev):.2e}; "
-              f"reference fp32 dev {np.array2string(dref, precision=1)} rms {rms(dref):.2e}")
-        assert dev[0] <= max(3 * dref[0], floor), (what, dev[0], dref[0])
+              f"reference fp32 dev {np.array2string(dref, precision=1)} rms {rms(dref):.2e}; "
+              f"first step: branch-matched arithmetic {arith:.2e}, decision flips {flips:.2e}")
+        assert abs(hip - mine[0]) <= 1e-6 * mine[0], (what, hip, mine[0])   # the same first step twice
+        assert arith <= 3 * dref[0], (what, arith, dref[0])
+        assert dev[0] <= 3 * dref[0] + flips, (what, dev[0], dref[0], flips)
         assert rms(dev) <= max(3 * rms(dref), 2e-6), (what, rms(dev), rms(dref))
     assert lm[-1] < 0.1 * lm[0]                              # the run descends as the reference's does
     bn = [n for n in st64 if n.endswith("running_mean") or n.endswith("running_var")]
