@@ -40,8 +40,9 @@ typedef struct ihipStream_t* hipStream_t;
  *      srpde_prepare_weights_h3 descriptor row grew to 10 columns; srpde_conv_wgrad_h3p reads dy
  *      planes with a row stride of cout rounded up to 32) and round 4's additions
  *      (srpde_conv_h4_set, srpde_poisson_debug_abort)
- *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace */
-#define SRPDE_ABI_VERSION 5
+ *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace
+ *   6  srpde_conv_fwd: ep_mean, ep_invstd, ep_gamma, ep_beta, ep_amax before the workspace */
+#define SRPDE_ABI_VERSION 6
 
 const char* srpde_last_error(void);
 int srpde_version(void);
@@ -57,8 +58,11 @@ int srpde_pack_conv_weights(const float* w, float* wfwd, float* wdgrad, int cout
                             int ksize, hipStream_t stream);
 int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1, const float* wpack,
                    const float* bias, float* y, int ldy, int n, int h, int w, int cout, int ksize, int dil,
-                   int sign, int accumulate, float* stats, void* workspace, size_t ws_bytes,
-                   hipStream_t stream);
+                   int sign, int accumulate, float* stats, const float* ep_mean, const float* ep_invstd,
+                   const float* ep_gamma, const float* ep_beta, unsigned* ep_amax, void* workspace,
+                   size_t ws_bytes, hipStream_t stream);
+/* ep_* (nullable, eval mode, layers with cin % 32 != 0 -- enc1.conv1): the epilogue applies the
+ * following BatchNorm (running statistics) + ReLU, as srpde_conv_fwd_h3's ep_* below. */
 /* optional scratch for splitting the last, partially filled round of tiles over K (pass
  * NULL to disable); srpde_conv_fwd_workspace_size() bytes always suffice */
 size_t srpde_conv_fwd_workspace_size(int cout);

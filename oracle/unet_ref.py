@@ -133,15 +133,19 @@ def conv_block(st, name, x, training, decisions=None):
     return x
 
 
-def attention_gate(st, name, x, gating, decisions=None):
-    """AttentionGate.forward, models.py:119-130."""
+def attention_gate(st, name, x, gating, decisions=None, tap=None):
+    """AttentionGate.forward, models.py:119-130.  ``tap``: receives the spatial pre-activation
+    (``<name>.sa_pre``), whose gradient summed over the pixels is the spatial bias gradient."""
     m = x.mean(dim=(2, 3), keepdim=True)                                  # AdaptiveAvgPool2d(1)
     h = _relu(_conv_apply(st, f"{name}.channel_attention.1", m), decisions, f"{name}.channel_attention.2")
     ca = torch.sigmoid(_conv_apply(st, f"{name}.channel_attention.3", h))
     x = x * ca
     if gating.shape[-2:] != x.shape[-2:]:                                  # models.py:125-126
         gating = F.interpolate(gating, size=x.shape[-2:], mode="bilinear", align_corners=True)
-    sa = torch.sigmoid(_conv_apply(st, f"{name}.spatial_attention.0", gating))
+    pre = _conv_apply(st, f"{name}.spatial_attention.0", gating)
+    if tap is not None:
+        tap(f"{name}.sa_pre", pre)
+    sa = torch.sigmoid(pre)
     return x * sa
 
 
@@ -176,11 +180,11 @@ def unet_forward(st, x, training: bool, taps=None, decisions=None):
     e3 = tap("e3", conv_block(st, "enc3", _maxpool(e2, D, "pool2"), training, D))
     b = tap("b1", _relu(_bn_apply(st, "bridge.1", _conv_apply(st, "bridge.0", e3, 2, 2), training), D, "bridge.1"))
     b = tap("b", _relu(_bn_apply(st, "bridge.4", _conv_apply(st, "bridge.3", b, 2, 2), training), D, "bridge.4"))
-    e3a = tap("e3a", attention_gate(st, "att3", e3, b, D))
+    e3a = tap("e3a", attention_gate(st, "att3", e3, b, D, tap))
     d3 = tap("d3", conv_block(st, "dec3", torch.cat([b, e3a], 1), training, D))
-    e2a = tap("e2a", attention_gate(st, "att2", e2, tap("u3g", up2(d3)), D))
+    e2a = tap("e2a", attention_gate(st, "att2", e2, tap("u3g", up2(d3)), D, tap))
     d2 = tap("d2", conv_block(st, "dec2", torch.cat([tap("u3c", up2(d3)), e2a], 1), training, D))
-    e1a = tap("e1a", attention_gate(st, "att1", e1, tap("u2g", up2(d2)), D))
+    e1a = tap("e1a", attention_gate(st, "att1", e1, tap("u2g", up2(d2)), D, tap))
     d1 = tap("d1", conv_block(st, "dec1", torch.cat([tap("u2c", up2(d2)), e1a], 1), training, D))
     y = tap("o1", _relu(_bn_apply(st, "out_bn1", _conv_apply(st, "out_conv1", d1, 1), training), D, "out_bn1"))
     y = tap("o2", _relu(_bn_apply(st, "out_bn2", _conv_apply(st, "out_conv2", y, 1), training), D, "out_bn2"))

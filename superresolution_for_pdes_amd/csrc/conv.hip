@@ -150,81 +150,12 @@ __global__ __launch_bounds__(256) void conv_igemm_fwd_kernel(ConvParams p) {
     __syncthreads();
   }
 
-  // ---------------- epilogue: bias, store, BN partial statistics -----------------
-  float bcol[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn0 + j * 32 + lr;
-    bcol[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = n0 + wn0 + j * 32 + lr;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float v = acc[i][j][r] + bcol[j];
-        acc[i][j][r] = v;
-        if (row < p.P && col < p.Cout) {
-          float* dst = p.y + (size_t)row * p.ldy + col;
-          *dst = p.accumulate ? *dst + v : v;
-        }
-      }
-    }
-  if (p.stats == nullptr) return;
-
-  float* red = smem;  // [WM][BN] -- the K loop ended with a barrier, LDS is free
-  const int cnt = min(BM, p.P - m0);
-  float mean[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        s += (row < p.P) ? acc[i][j][r] : 0.f;
-      }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) s += red[w * BN + wn0 + j * 32 + lr];
-    mean[j] = s / (float)cnt;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float d = acc[i][j][r] - mean[j];
-        s += (row < p.P) ? d * d : 0.f;
-      }
-    s += __shfl_xor(s, 32, 64);
-    if (lh == 0) red[wmi * BN + wn0 + j * 32 + lr] = s;
-  }
-  __syncthreads();
-  if (wmi == 0 && lh == 0) {
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int cl = wn0 + j * 32 + lr, col = n0 + cl;
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + cl];
-      if (col < p.Cout) p.stats[(size_t)mt * p.Cout + col] = make_float2(mean[j], s);
-    }
-  }
+  // ---------------- epilogue: bias, (eval) BN + ReLU, store, BN partial statistics -------------
+  // the shared h3 epilogue (conv_common.h): 16-B row stores through LDS (the K loop ended with a
+  // barrier, LDS is free), per-SRB-row statistics, the eval-mode BN + ReLU and max word (ep_*)
+  x6_finish<BM, BN, WM, WN, BM>(p, acc, false, wg, nbm * nbn, 0, m0, n0, wmi, wni, lane, smem,
+                                (p.ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(p.y) & 15) == 0)
+                                    ? smem + 2 * WM * TI * BN : nullptr);
 }
 
 // ---------------------- forward v2: LDS-DMA staged, BK = 32 ----------------------
@@ -1003,7 +934,8 @@ size_t srpde_conv_fwd_workspace_size(int cout) {
 int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, int ldx1,
                    const float* wpack, const float* bias, float* y, int ldy,
                    int n, int h, int w, int cout, int ksize, int dil, int sign, int accumulate,
-                   float* stats, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                   float* stats, const float* ep_mean, const float* ep_invstd, const float* ep_gamma,
+                   const float* ep_beta, unsigned* ep_amax, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wpack && y, "srpde_conv_fwd: null pointer");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0, "srpde_conv_fwd: bad shape");
   SRPDE_CHECK_ARG(ksize == 1 || ksize == 3, "srpde_conv_fwd: ksize must be 1 or 3");
@@ -1022,6 +954,12 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
   p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil; p.sign = sign; p.accumulate = accumulate;
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
   p.ntail = 0; p.tsplit = 1; p.part = nullptr;
+  SRPDE_CHECK_ARG(ep_mean == nullptr || (ep_invstd && ep_gamma && ep_beta && !accumulate && stats == nullptr &&
+                                         cout % 4 == 0 && !v2_ok(p)),
+                  "srpde_conv_fwd: the epilogue BN + ReLU needs mean/invstd/gamma/beta, no accumulate / stats, "
+                  "cout %% 4 == 0, and a layer the register-staged kernel takes (cin %% 32 != 0)");
+  p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
+  p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
   if (v2_ok(p)) {
     switch (fwd_config(cout)) {
       case 0: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream, workspace, ws_bytes);

@@ -362,18 +362,20 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
         al[i] = nal[i];
       }
     }
-    // tap tau + 1's weights (issued at tap tau - 2) must have landed before this barrier: the DMAs
-    // of this tap and of the previous one may still be in flight (exact counts: every wave issues
-    // NCUR DMAs per tap, zero fills included; the prologue before the first tap drained to 0)
-    constexpr int NPREV = 2 + ((T == 0 ? 8 : T - 1) < APW ? 1 : 0);
+    // after this barrier the next tap tau + 1 reads its own weights (issued at tap tau - 2) AND the first
+    // column blocks of tap tau + 2's (issued at tap tau - 1): only this tap's DMAs may still be in
+    // flight (exact counts: every wave issues NCUR DMAs per tap, zero fills included; the prologue
+    // before the first tap drained to 0).  Round 4 waited for tap tau - 2 only, so the bnext reads of
+    // the following tap could see a slot before its DMA landed: a run-to-run race that showed under
+    // load (tools/diag_race.py: dgrad outputs changed in the first column blocks of a tile).
     constexpr int NCUR = 2 + (T < APW ? 1 : 0);
     // a bare s_barrier: no lgkmcnt(0) drain of the next tap's fragment reads still in flight (they read
     // slot tau + 1 and the S tile, which no DMA issued after this barrier writes); the asm is a
     // compiler memory barrier, so no LDS read moves above it
     if constexpr (SRPDE_CONV_DBG & 2)   // diagnostics: 2 = no tap barrier
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPREV + NCUR) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCUR) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NPREV + NCUR) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NCUR) : "memory");
   };
 
   for (int ch = c_beg; ch < c_end; ++ch) {

@@ -160,12 +160,15 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
             planes_out._srpde_amax = a0 if a1 is None else (a0, a1)
             planes_out._srpde_c0 = x0.shape[1]
         return
-    assert (planes_out is None and in_affine is None and bn_bwd is None and out_max is None and ep_bn is None
-            and x1_gate is None), "planes_out / in_affine / bn_bwd / out_max / ep_bn / x1_gate need the h3 kernels"
+    assert (planes_out is None and in_affine is None and bn_bwd is None and out_max is None
+            and x1_gate is None), "planes_out / in_affine / bn_bwd / out_max / x1_gate need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
     call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
-         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), ws.data_ptr(), ws.numel(), stream_ptr())
+         n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), *_ep_args(ep_bn), ws.data_ptr(), ws.numel(),
+         stream_ptr())
+    if ep_bn is not None:
+        tag_amax(y, ep_bn[4])
 
 
 def conv_fwd_presplit(xp, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
@@ -669,9 +672,10 @@ def att_gate_fwd(x, g, n, hw, chan, wg, bg, out=None):
 
 
 def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg,
-            defer_params=False):
-    """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None) is the
-    gating gradient's per-pixel factor for upsample_bwd(gate=...); ``params`` (when
+            defer_params=False, want_dsa=False):
+    """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None, or
+    ``want_dsa``) is the gating gradient's per-pixel factor d loss / d(spatial pre-activation), for
+    upsample_bwd(gate=...); the spatial bias gradient is its sum; ``params`` (when
     ``defer_params``) is a callable that launches the parameter-gradient reductions on the
     current stream, to be queued after this call (reads ``ws``, ``g``, ``m``, ``hb``)."""
     m, hb, ca, sa = saved
@@ -694,7 +698,7 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
                  ws_bytes, stream_ptr())
         params.keep = (ws,)
     # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
-    dsa = ws[:4 * x.shape[0]].view(torch.float32) if dg is None else None
+    dsa = ws[:4 * x.shape[0]].view(torch.float32) if dg is None or want_dsa else None
     return dsa, params
 
 

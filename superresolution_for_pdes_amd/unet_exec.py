@@ -66,6 +66,14 @@ def _tap(name, t):
         DEBUG_TAPS[name] = t.detach().clone()
 
 
+def _tap_dgrad(conv, dyp, dx, dx_max, out_part):
+    if DEBUG_TAPS is not None:
+        name = getattr(conv, "_srpde_name", "?")
+        for k, t in (("dyp", dyp), ("dx", dx), ("dx_max", dx_max), ("bn_part", out_part)):
+            if t is not None:
+                _tap(f"{k}:{name}", t)
+
+
 # bench/profiling hook: {conv module name: list} -> (start, end) HIP events recorded on the
 # compute stream around that layer's forward conv launch
 TIMED_LAYERS = {}
@@ -295,6 +303,13 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
             H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None,
                        ep_bn=(mean, invstd, bn.weight, bn.bias, slot), x1_gate=x1_gate)
             return _eval_consumers(y, slot, n, h, w, cout, pool, att, gate), None
+        if (getattr(slots, "eval_epilogue", False) and _EVAL_EPI and _EVAL_EPI_F32 and x1 is None and x1_gate is None
+                and x0.shape[1] % 32):
+            # the same on the register-staged fp32 kernel (enc1.conv1: 3 -> 4 padded input channels)
+            slot = slots.take()
+            H.conv_fwd(x0, None, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None,
+                       ep_bn=(mean, invstd, bn.weight, bn.bias, slot))
+            return _eval_consumers(y, slot, n, h, w, cout, pool, att, gate), None
         H.conv_fwd(x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, None, x1_gate=x1_gate)
     # a fused input is not the layer's real input (that is relu(bn(x0))): keep no reference to it,
     # the weight gradient reads the stored split
@@ -343,6 +358,8 @@ def _eval_stats(bn):
     rm, rv = bn.running_mean, bn.running_var
     key = (rm.data_ptr(), rm._version, rv.data_ptr(), rv._version, float(bn.eps), _RS_EPOCH[0])
     c = getattr(bn, "_srpde_eval_stats", None)
+    if not _EVAL_STATS_CACHE:
+        return H.bn_eval_prepare(rm, rv, bn.eps)
     if c is None or c[0] != key:
         c = (key, H.bn_eval_prepare(rm, rv, bn.eps))
         bn._srpde_eval_stats = c
@@ -384,6 +401,10 @@ def _eval_consumers(a, slot, n, h, w, c, pool, att, gate):
 # inference (eval, nothing saved for a backward): BN + ReLU in the conv epilogue (SRPDE_EVAL_EPI=0: the
 # separate passes)
 _EVAL_EPI = os.environ.get("SRPDE_EVAL_EPI", "1") != "0"
+# ... also on the register-staged fp32 kernel of enc1.conv1 (SRPDE_EVAL_EPI_F32=0: its separate BN + ReLU pass)
+_EVAL_EPI_F32 = os.environ.get("SRPDE_EVAL_EPI_F32", "1") != "0"
+# the eval forward's per-layer BN (mean, invstd) cached across forwards (SRPDE_EVAL_STATS_CACHE=0: recomputed)
+_EVAL_STATS_CACHE = os.environ.get("SRPDE_EVAL_STATS_CACHE", "1") != "0"
 _FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
 _FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
 # the gates' spatial attention formed by the upsample that produces their gating input
@@ -497,6 +518,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
             dx_max = H.dx_max_slots(n, h, w, cin, y.device)
         H.conv_dgrad_bnb(da, y, mean, invstd, bn.weight, bn.bias, m1, m2, dyw, wd, dx, n, h, w, cout, cin, dil, dyp,
                          bn_bwd=bn_bwd, dx_max=dx_max)
+        _tap_dgrad(conv, dyp, dx, dx_max, out_part)
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
         if wq is None:
             fn()
@@ -523,6 +545,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
                 dx_max = H.out_max_slots(n, h, w, H.cpad32(cout), cin, dil, y.device)
         H.conv_fwd_presplit(dyp, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, bn_bwd=bn_bwd,
                             out_max=dx_max)
+        _tap_dgrad(conv, dyp, dx, dx_max, out_part)
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
         if wq is None:
             fn()
@@ -549,6 +572,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
                 dx_max = H.out_max_slots(n, h, w, cout, cin, dil, y.device)
         H.conv_fwd(dy, None, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, dyp, bn_bwd=bn_bwd,
                    out_max=dx_max)
+        _tap_dgrad(conv, dyp, dx, dx_max, out_part)
     dw = grads[conv.weight]
     if xp is not None and dyp is not None:
         fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax)
@@ -665,10 +689,12 @@ def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=No
     c1, c3, s0 = _att_params(att)
     dsa, params = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
                             grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
-                            grads[s0.bias], defer_params=wq is not None)
+                            grads[s0.bias], defer_params=wq is not None, want_dsa=DEBUG_TAPS is not None)
+    if DEBUG_TAPS is not None:
+        _tap("dsa_pre:" + getattr(att, "_srpde_name", "?"), dsa)
     if params is not None:
         wq.submit(params, params.keep)
-    return None if dsa is None else (dsa, s0.weight)
+    return None if dsa is None or dg is not None else (dsa, s0.weight)
 
 
 def check_input(x):

@@ -57,7 +57,7 @@ def test_host_queries_without_gpu(lib):
 
 def test_argument_errors_are_reported(lib):
     """Bad shapes fail with a negative code and a message, before any launch."""
-    rc = lib.lib().srpde_conv_fwd(0, 3, 3, 0, 0, 0, 0, 0, 0, 3, 1, 8, 8, 16, 3, 1, 1, 0, 0, 0, 0, 0)
+    rc = lib.lib().srpde_conv_fwd(0, 3, 3, 0, 0, 0, 0, 0, 0, 3, 1, 8, 8, 16, 3, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
     assert rc < 0
     assert "null" in lib.last_error()
     with pytest.raises(RuntimeError, match="srpde_bn_relu_fwd"):
