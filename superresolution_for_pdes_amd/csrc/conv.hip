@@ -158,6 +158,158 @@ __global__ __launch_bounds__(256) void conv_igemm_fwd_kernel(ConvParams p) {
                                     ? smem + 2 * WM * TI * BN : nullptr);
 }
 
+// ------------------ the 4-channel-input 3x3 forward (enc1.conv1, models.py:16) ------------------
+// The U-Net's first conv reads the 3-channel input (padded to 4, the zero 4th channel meeting zero
+// weights) and writes 64 channels: K = 9 taps x 4 channels is far too short for the K-chunked kernels
+// (conv_igemm_fwd_kernel: 278 us at B = 1024, ~1.5 TB/s), and the pass is bound by the 64-channel
+// write.  Here a wave owns 64 pixels x 64 output channels and keeps the whole 64 x 36 weight tile in
+// registers: per tap it loads one fp32 of its 16 pixels' 4 channels per lane straight into the MFMA
+// operand (16-B pixels, a 256-B contiguous wave load) and runs 16 v_mfma_f32_16x16x4_f32 (weights as
+// the A operand, so a lane's accumulator is 4 consecutive channels of one pixel: 16-B row stores).
+// Epilogue: bias, the eval-mode BN + ReLU and max word (ep_*), BN partial statistics per 256 rows
+// (a workgroup's 4 waves), the same (mean, M2) layout as the other forward kernels.
+typedef float c4x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256, 3) void conv_fwd_c4_kernel(ConvParams p) {
+  constexpr int NPB = 4, NCB = 4;                  // 16-pixel blocks per wave, 16-channel blocks per tile
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;       // B column (pixel) / K row (channel); D row group
+  const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64;
+  const int HW = p.H * p.W;
+  // the weight tile as A operands: W[n0 + 16 cb + l16][tap][lg]
+  float wa[9][NCB];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) wa[t][cb] = p.w[(size_t)(n0 + cb * 16 + l16) * 36 + t * 4 + lg];
+  int pn[NPB], py[NPB], px[NPB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+    const int m = m0 + wave * 64 + pb * 16 + l16;
+    if (m < p.P) {
+      const int nn = m / HW, rem = m - nn * HW;
+      pn[pb] = nn * HW; py[pb] = rem / p.W; px[pb] = rem - py[pb] * p.W;
+    } else {
+      pn[pb] = -1; py[pb] = 0; px[pb] = 0;
+    }
+  }
+  c4x4 acc[NPB][NCB];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[pb][cb] = c4x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int oy = (t / 3 - 1) * p.dil * p.sign, ox = (t % 3 - 1) * p.dil * p.sign;
+    float xb[NPB];
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      const int iy = py[pb] + oy, ix = px[pb] + ox;
+      xb[pb] = (pn[pb] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+                   ? p.x0[(size_t)(pn[pb] + iy * p.W + ix) * 4 + lg] : 0.f;
+    }
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        acc[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][cb], xb[pb], acc[pb][cb], 0, 0, 0);
+  }
+  // lane: pixel m0 + 64 wave + 16 pb + l16, channels n0 + 16 cb + 4 lg + 0..3
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int c = n0 + cb * 16 + lg * 4;
+    const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 mu, is, ga, be;
+    if (p.ep_mean) {
+      mu = *reinterpret_cast<const float4*>(p.ep_mean + c);
+      is = *reinterpret_cast<const float4*>(p.ep_invstd + c);
+      ga = *reinterpret_cast<const float4*>(p.ep_gamma + c);
+      be = *reinterpret_cast<const float4*>(p.ep_beta + c);
+    }
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb) {
+      c4x4& v = acc[pb][cb];
+      v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
+      if (p.ep_mean) {
+        v[0] = ep_bn_relu(v[0], mu.x, is.x, ga.x, be.x);
+        v[1] = ep_bn_relu(v[1], mu.y, is.y, ga.y, be.y);
+        v[2] = ep_bn_relu(v[2], mu.z, is.z, ga.z, be.z);
+        v[3] = ep_bn_relu(v[3], mu.w, is.w, ga.w, be.w);
+      }
+      if (pn[pb] >= 0)
+        *reinterpret_cast<float4*>(p.y + (size_t)(m0 + wave * 64 + pb * 16 + l16) * p.ldy + c) =
+            make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (p.ep_amax != nullptr) {
+    float mx = 0.f;
+#pragma unroll
+    for (int pb = 0; pb < NPB; ++pb)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        if (pn[pb] >= 0)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(acc[pb][cb][r]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) red[wave][0] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(p.ep_amax, __float_as_uint(fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]))));
+  }
+  if (p.stats == nullptr) return;
+  // statistics of the workgroup's 256 rows: per channel the mean, then M2 about it
+  const int cnt = min(256, p.P - m0);
+  float mean[NCB][4];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int pb = 0; pb < NPB; ++pb) {
+          const float v = acc[pb][cb][r];
+          if (pass == 0) {
+            s += pn[pb] >= 0 ? v : 0.f;
+          } else {
+            const float d = v - mean[cb][r];
+            s = pn[pb] >= 0 ? __builtin_fmaf(d, d, s) : s;
+          }
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+        if (l16 == 0) red[wave][cb * 16 + lg * 4 + r] = s;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cl = cb * 16 + lg * 4 + r;
+        const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+        if (pass == 0) mean[cb][r] = t / (float)cnt;
+        else if (wave == 0 && l16 == 0) p.stats[(size_t)blockIdx.x * p.Cout + n0 + cl] = make_float2(mean[cb][r], t);
+      }
+    __syncthreads();
+  }
+}
+
+static bool c4_ok(const ConvParams& p) {
+  // Cout % 128 != 0: the 256-row statistics blocks srpde_conv_stats_rows_per_block gives those widths
+  return p.ksize == 3 && p.c0 == 4 && p.c1 == 0 && p.ldx0 == 4 && p.Cout % 64 == 0 && p.Cout % 128 != 0 &&
+         p.ldy % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(p.y) & 15) == 0 && !p.accumulate;
+}
+
+static int launch_fwd_c4(const ConvParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(conv_fwd_c4_kernel, dim3(ceil_div(p.P, 256), p.Cout / 64), dim3(256), 0, st, p);
+  SRPDE_LAUNCH_CHECK("srpde_conv_fwd(c4)");
+  return 0;
+}
+
 // ---------------------- forward v2: LDS-DMA staged, BK = 32 ----------------------
 // For Cin % 32 == 0 (every layer but enc1.conv1 fwd and out_conv2 dgrad).  Operand tiles
 // go HBM/L2 -> LDS with buffer_load ... lds (no VGPR staging, no ds_write): each wave
@@ -960,6 +1112,7 @@ int srpde_conv_fwd(const float* x0, int c0, int ldx0, const float* x1, int c1, i
                   "cout %% 4 == 0, and a layer the register-staged kernel takes (cin %% 32 != 0)");
   p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
+  if (c4_ok(p)) return launch_fwd_c4(p, stream);
   if (v2_ok(p)) {
     switch (fwd_config(cout)) {
       case 0: return launch_fwd_v2<128, 128, 2, 2, 4>(p, stream, workspace, ws_bytes);

@@ -2019,11 +2019,11 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "bn_part, cout %% 4 == 0");
   p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
+  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);
   }
-  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
   const int tps = h3_tps(h3_bn(h3_cfg(cout)), a.arows);
 #define H3_LAUNCH(BN_)                                                                        \
   (tps == 2 ? launch_fwd_h3<256, BN_, 8, 1, H3_SRB, true, 2>(p, a, stream, workspace, ws_bytes) \
@@ -2078,11 +2078,11 @@ int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, 
   a.xsplit = nullptr;
   a.in_scale = nullptr; a.in_shift = nullptr;
   a.wide = ldy % 4 == 0 && aligned16(y);
+  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, true, stream, workspace, ws_bytes);
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
   }
-  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, true, stream, workspace, ws_bytes);
   const int bn = h3_bn(h3_cfg(cout));
   SRPDE_CHECK_ARG(h3_lds(bn, a.arows, 1, false, true) <= 160 * 1024, "srpde_conv_fwd_h3_presplit: LDS (w=%d dil=%d)", w,
                   dil);

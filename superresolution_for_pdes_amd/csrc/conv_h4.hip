@@ -1,6 +1,7 @@
-// "h4": the 256 x 128 implicit-GEMM 3x3 convolution (forward and dgrad) of conv_h3.hip
-// (conv_fwd_h3_kernel<256, 128, 8, 1, 128, true, 2>), rebuilt around its main loop so the MFMA
-// pipes stay fed.  Same arithmetic, fragments, product order, two-level accumulation and
+// "h4": the 256 x 128 (and 256 x 64) implicit-GEMM 3x3 convolution (forward and dgrad) of
+// conv_h3.hip (conv_fwd_h3_kernel<256, BN, 8, 1, 128, true, ...>), rebuilt around its main loop so
+// the MFMA pipes stay fed.  Instantiated for W = 10 (dilation 1, 2) and 20 with 128- or 64-column
+// tiles, and for W = 40 with 64-column tiles (the W = 40 layers took the 4-wave h3r kernel before).  Same arithmetic, fragments, product order, two-level accumulation and
 // epilogue as that kernel, so the outputs are bit-identical to it (tests/test_gpu_kernels.py
 // ::test_conv_h4_equals_h3); reference calls: nn.Conv2d at src/models.py:16,18,43,46 and their
 // autograd convolution_backward (input gradient).
@@ -49,9 +50,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int W, int DIL>
+template <int W, int DIL, int BN_>
 struct H4Geom {
-  static constexpr int BM = 256, BN = 128;
+  static constexpr int BM = 256, BN = BN_;
   static constexpr int HALO = (W + 1) * DIL;
   static constexpr int AROWS = BM + 2 * HALO;                // halo tile rows
   static constexpr int SR = 160;                             // S row bytes: hi 64 | lo 64 | 32 unused
@@ -64,6 +65,7 @@ struct H4Geom {
   static constexpr int NBR = 4;                              // weight ring slots, one tap each
   static constexpr int BP = BN * 64;                         // one fp16 plane of a tap's weight tile
   static constexpr int BSLOT = 2 * BP;
+  static constexpr int NBD = BN / 64;                        // weight DMAs (1 KiB) per wave and tap
   template <bool PRE> static constexpr int nsb() { return PRE ? 2 : 1; }
   template <bool PRE> static constexpr int off_f() { return nsb<PRE>() * SSTRIDE; }
   template <bool PRE> static constexpr int off_b() { return off_f<PRE>() + (PRE ? 0 : FROWS * 128); }
@@ -72,18 +74,21 @@ struct H4Geom {
   template <bool PRE> static constexpr int apw() { return PRE ? (NQ + 7) / 8 : (NA + 7) / 8; }
 };
 
-template <int W, int DIL, int SIGN, bool PRE>
+template <int W, int DIL, int BN, int SIGN, bool PRE>
 __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Args h) {
-  using G = H4Geom<W, DIL>;
-  constexpr int BM = G::BM, BN = G::BN, WM = 8, WN = 1, SRB = 128;
-  constexpr int TI = 1, TJ = 4, TI16 = 2, TJ16 = 8;
+  using G = H4Geom<W, DIL, BN>;
+  constexpr int BM = G::BM, WM = 8, WN = 1, SRB = 128;
+  constexpr int TI = 1, TJ = BN / 32, TI16 = 2, TJ16 = BN / 16, NBD = G::NBD;
+  static_assert(BN == 64 || BN == 128, "h4 column tiles");
   constexpr int SR = G::SR, AROWS = G::AROWS, SSTRIDE = G::SSTRIDE, ZREL = G::ZREL;
   constexpr int BP = G::BP, BSLOT = G::BSLOT;
   constexpr int OFF_F = G::template off_f<PRE>(), OFF_B = G::template off_b<PRE>();
   constexpr int OFF_SINK = G::template off_sink<PRE>();   // target of the zero-fill DMAs that keep vmcnt counts exact
   constexpr int APW = G::template apw<PRE>();   // A-tile DMAs per wave and chunk, one per tap 0 .. APW-1
   static_assert(G::template lds<PRE>() <= 160 * 1024, "LDS");
-  static_assert(APW <= 6, "A DMAs fit the taps before the chunk's last three");
+  // the next chunk's A pieces are issued at taps 0 .. APW-1 and must have landed (the tap-end wait
+  // leaves only that tap's DMAs in flight) before PRE's tap 8 reads them / before the convert after tap 8
+  static_assert(APW <= (PRE ? 7 : 8), "A DMAs land before the next chunk's tile is read");
   static_assert(SSTRIDE + 64 < 65536 && ZREL < 65536, "16-bit fragment offsets");
   static_assert(2 * WM * BN * 4 + WM * 2048 <= AROWS * SR, "epilogue scratch fits S");
 
@@ -152,13 +157,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   }
   // B fragment reads: row r = 16 j + l16 of the tap's tile, 16-B chunk lq at slot swzh(r, lq)
   const unsigned b_lane = (unsigned)(OFF_B + l16 * 64 + swzh(l16, lq) * 16);
-  // B DMA (wave w: row block w of both planes): per-tile byte offsets; the tap / chunk part is soffset
-  unsigned b_voff[2];
-  {
-    const int r = wave * 16 + (lane >> 2);
-    const int c = swzh(r, lane & 3);
+  // B DMA d of wave w: 16-row block rb of plane pl (BN = 128: row block w of both planes; BN = 64: plane
+  // w / 4, row block w % 4); per-tile byte offsets, the tap / chunk part is soffset
+  unsigned b_voff[NBD], b_lds[NBD];
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl) b_voff[pl] = (unsigned)((pl * plane + (size_t)(n0 + r) * p.K + c * 8) * 2);
+  for (int d = 0; d < NBD; ++d) {
+    const int pl = NBD == 2 ? d : wave >> 2, rb = NBD == 2 ? wave : wave & 3;
+    const int r = rb * 16 + (lane >> 2);
+    const int c = swzh(r, lane & 3);
+    b_voff[d] = (unsigned)((pl * plane + (size_t)(n0 + r) * p.K + c * 8) * 2);
+    b_lds[d] = (unsigned)(pl * BP + rb * 1024);
   }
 
   const int nch = p.Cin / BK2;
@@ -208,9 +216,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   auto issue_b = [&](int ch, int tap, int slot, bool real) {
     const unsigned soff = (unsigned)((tap * p.Cin + ch * BK2) * 2);
 #pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-      dma16s(rsw, real ? b_voff[pl] : OOB, real ? soff : 0u,
-             lds0 + (unsigned)(real ? OFF_B + slot * BSLOT + pl * BP + wave * 1024 : OFF_SINK));
+    for (int d = 0; d < NBD; ++d)
+      dma16s(rsw, real ? b_voff[d] : OOB, real ? soff : 0u,
+             lds0 + (unsigned)(real ? OFF_B + slot * BSLOT + b_lds[d] : OFF_SINK));
   };
 
   // F (chunk ch, landed) -> S: scale and split every halo element once per chunk; the N-tile-0
@@ -301,11 +309,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   }
 
   // column blocks a B fragment pair is read ahead of its MFMAs: two where the registers allow (PRE: 243
-  // VGPRs), one with the convert path's registers (two: 24 VGPRs of spill)
-  constexpr int BPF = PRE ? 2 : 1;
+  // VGPRs; BN = 64: half the accumulators), one with the convert path's registers at BN = 128 (two: 24
+  // VGPRs of spill)
+  constexpr int BPF = (PRE || BN == 64) ? 2 : 1;
   int slot0 = 0;   // ring slot of the chunk's tap 0 (taps of a tile use slots 0, 1, 2, 3, 0, ...)
   // one tap: MFMAs of column block j with the B fragments of block j + 2 (or of the next tap)
-  // in flight; the next tap's A fragments read at block 3 (within the chunk)
+  // in flight; the next tap's A fragments read at block TJ16 / 2 - 1 (within the chunk)
   auto tap = [&](int ch, auto tap_tag) {
     constexpr int T = decltype(tap_tag)::value;
     const int slot = (slot0 + T) & 3;
@@ -339,7 +348,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       }
       // the next tap's A fragments: within the chunk; PRE also across it (the next chunk's S buffer
       // has landed: its pieces were issued at taps < APW and waited for with tap 8's weights)
-      constexpr bool RA = j == 3 && (T < 8 || PRE);
+      constexpr bool RA = j == TJ16 / 2 - 1 && (T < 8 || PRE);
       if constexpr (RA) read_a(0, apk[T < 8 ? T + 1 : 0], T < 8 ? sb : sbn, nah, nal);
 #pragma unroll
       for (int i = 0; i < TI16 && !(SRPDE_CONV_DBG & 128); ++i) {   // diagnostics: 128 = no MFMAs
@@ -368,7 +377,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     // before the first tap drained to 0).  Round 4 waited for tap tau - 2 only, so the bnext reads of
     // the following tap could see a slot before its DMA landed: a run-to-run race that showed under
     // load (tools/diag_race.py: dgrad outputs changed in the first column blocks of a tile).
-    constexpr int NCUR = 2 + (T < APW ? 1 : 0);
+    constexpr int NCUR = NBD + (T < APW ? 1 : 0);
     // a bare s_barrier: no lgkmcnt(0) drain of the next tap's fragment reads still in flight (they read
     // slot tau + 1 and the S tile, which no DMA issued after this barrier writes); the asm is a
     // compiler memory barrier, so no LDS read moves above it
@@ -435,9 +444,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
 }
 
 // ---------------------------------- host side ---------------------------------------
-template <int W, int DIL, int SIGN, bool PRE>
+template <int W, int DIL, int BN_, int SIGN, bool PRE>
 static int launch_h4_cfg(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
-  using G = H4Geom<W, DIL>;
+  using G = H4Geom<W, DIL, BN_>;
   constexpr int BM = G::BM, BN = G::BN;
   const int T = ceil_div(p.P, BM) * (p.Cout / BN);
   static const int cus = [] {
@@ -451,30 +460,37 @@ static int launch_h4_cfg(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
-  hipLaunchKernelGGL((conv_fwd_h4_kernel<W, DIL, SIGN, PRE>), dim3(grid), dim3(512), G::template lds<PRE>(), st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h4_kernel<W, DIL, BN, SIGN, PRE>), dim3(grid), dim3(512), G::template lds<PRE>(), st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h4)");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, 128>(p, st);
   return 0;
 }
 
+// the column tile: 128 where the weight ring and two S buffers fit LDS (W <= 20), else 64
+static int h4_bn(int w, int cout) { return (cout % 128 == 0 && w <= 20) ? 128 : 64; }
+
 bool h4_supported(int w, int dil, int cout, bool bnb) {
-  if (bnb || cout % 128 != 0) return false;
-  return (w == 10 && (dil == 1 || dil == 2)) || (w == 20 && dil == 1);
+  if (bnb || cout % 64 != 0) return false;
+  return (w == 10 && (dil == 1 || dil == 2)) || (w == 20 && dil == 1) || (w == 40 && dil == 1);
 }
 
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes) {
-#define H4_CASE(W_, D_)                                                                              \
-  if (p.W == W_ && p.dil == D_) {                                                                     \
-    if (pre) return p.sign > 0 ? launch_h4_cfg<W_, D_, 1, true>(p, h, st, ws, ws_bytes)               \
-                               : launch_h4_cfg<W_, D_, -1, true>(p, h, st, ws, ws_bytes);             \
-    return p.sign > 0 ? launch_h4_cfg<W_, D_, 1, false>(p, h, st, ws, ws_bytes)                       \
-                      : launch_h4_cfg<W_, D_, -1, false>(p, h, st, ws, ws_bytes);                     \
+#define H4_CASE(W_, D_, BN_)                                                                          \
+  if (p.W == W_ && p.dil == D_ && h4_bn(W_, p.Cout) == BN_) {                                         \
+    if (pre) return p.sign > 0 ? launch_h4_cfg<W_, D_, BN_, 1, true>(p, h, st, ws, ws_bytes)          \
+                               : launch_h4_cfg<W_, D_, BN_, -1, true>(p, h, st, ws, ws_bytes);        \
+    return p.sign > 0 ? launch_h4_cfg<W_, D_, BN_, 1, false>(p, h, st, ws, ws_bytes)                  \
+                      : launch_h4_cfg<W_, D_, BN_, -1, false>(p, h, st, ws, ws_bytes);                \
   }
-  H4_CASE(10, 1)
-  H4_CASE(10, 2)
-  H4_CASE(20, 1)
+  H4_CASE(10, 1, 128)
+  H4_CASE(10, 2, 128)
+  H4_CASE(20, 1, 128)
+  H4_CASE(10, 1, 64)
+  H4_CASE(10, 2, 64)
+  H4_CASE(20, 1, 64)
+  H4_CASE(40, 1, 64)
 #undef H4_CASE
-  set_error("srpde_conv_fwd_h3(h4): no instantiation for W=%d dil=%d", p.W, p.dil);
+  set_error("srpde_conv_fwd_h3(h4): no instantiation for W=%d dil=%d cout=%d", p.W, p.dil, p.Cout);
   return kErrArg;
 }
 

@@ -1,10 +1,10 @@
-"""The h4 convolution kernel (conv_h4.hip) against the h3 8-wave kernel it replaces for 128-column
-tiles at W = 10 (dilation 1 and 2) and W = 20: same fragments, products, accumulation order and
+"""The h4 convolution kernel (conv_h4.hip) against the h3 kernels it replaces (the 8-wave kernel for
+W = 10 (dilation 1 and 2) and W = 20, the 4-wave h3r for the 64-column tiles at W = 40): same fragments, products, accumulation order and
 epilogue, so every output must be EQUAL bit for bit -- forward (bias, BN statistics, stored input
 split, fused input BN + ReLU, virtual concat, the K-split tail), the eval-mode epilogue (BN + ReLU,
 max|y| word), the dgrad from an fp32 dy (stored dy split, fused BN-backward partials, per-tile
 max|dx|) and the dgrad from a pre-split dy.  The layer shapes are the U-Net's
-(src/models.py:16-19, 43-49: enc2 / dec2 at 20x20, enc3 / bridge / dec3 at 10x10)."""
+(src/models.py:16-19, 43-49: enc1 / dec1 at 40x40, enc2 / dec2 at 20x20, enc3 / bridge / dec3 at 10x10)."""
 import pytest
 import torch
 
@@ -20,6 +20,12 @@ DEV = "cuda"
     (11, 256, 0, 512, 10, 2),     # bridge.0
     (170, 512, 0, 512, 10, 2),    # bridge.3 with a K-split tail (268 tiles on 256 CUs)
     (2, 64, 64, 128, 20, 1),      # a partial last row tile, two 32-channel chunks per input
+    # 64-column tiles (h3: the 4-wave h3r kernel at W = 40, the 8-wave kernel below)
+    (5, 64, 0, 64, 40, 1),        # enc1.conv2 / dec1.conv2 (fused input BN + ReLU; dgrad 64 columns)
+    (3, 128, 64, 64, 40, 1),      # dec1.conv1 (virtual concat; dgrad 192 columns = 3 tiles)
+    (44, 64, 0, 64, 40, 1),       # W = 40 with a K-split tail (275 tiles; h3r has none: see below)
+    (9, 64, 0, 128, 20, 1),       # enc2.conv1 (dgrad: 64 columns at W = 20)
+    (6, 64, 0, 64, 10, 2),        # 64 columns at W = 10, dilation 2
 ])
 def test_conv_h4_equals_h3(n, c0, c1, cout, hw, dil):
     from superresolution_for_pdes_amd import hipops as H
@@ -75,6 +81,11 @@ def test_conv_h4_equals_h3(n, c0, c1, cout, hw, dil):
     names = ("y", "stats", "xsplit", "y_eval", "amax_eval", "dx", "dysplit", "bn_part", "dx_max", "dx_presplit",
              "bn_part_presplit", "dx_max_presplit")
     for name, a, b_ in zip(names, *outs):
+        if (name == "stats" or name.startswith("bn_part")) and hw == 40 and n == 44:
+            # h3r runs no K-split tail: its last-round tiles' reductions are summed in another order
+            # than conv_tail_fixup's (same y bits; statistics equal to fp32 rounding)
+            assert float((a - b_).abs().max()) <= 1e-6 * float(b_.abs().max()), name
+            continue
         assert torch.equal(a, b_), name
     # the pre-split dgrad reads the same pieces the fp32 one split: equal outputs as well
     assert torch.equal(outs[1][5], outs[1][9])
@@ -109,7 +120,8 @@ def test_conv_h4_accumulate_and_strided_output():
     (13, 512, 256, 256, 10, True),    # dec3.conv1: [b, att3(e3)] on h4
     (7, 256, 128, 128, 20, True),     # dec2.conv1: [up(d3), att2(e2)] on h4
     (13, 512, 256, 256, 10, False),   # the same on the h3 8-wave kernel
-    (3, 128, 64, 64, 40, True),       # dec1.conv1: [up(d2), att1(e1)] on h3r
+    (3, 128, 64, 64, 40, True),       # dec1.conv1: [up(d2), att1(e1)] on h4 (64-column tiles)
+    (3, 128, 64, 64, 40, False),      # the same on h3r
 ])
 def test_gated_second_input_equals_materialized(n, c0, c1, cout, hw, h4):
     """The decoder conv reading an AttentionGate's output through x1_gate (the gate (x * ca) * sa
