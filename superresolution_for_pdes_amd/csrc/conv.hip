@@ -173,6 +173,7 @@ typedef float c4x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256, 3) void conv_fwd_c4_kernel(ConvParams p) {
   constexpr int NPB = 4, NCB = 4;                  // 16-pixel blocks per wave, 16-channel blocks per tile
   __shared__ float red[4][64];
+  __shared__ __attribute__((aligned(16))) float stg[4][16 * 68];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l16 = lane & 15, lg = lane >> 4;       // B column (pixel) / K row (channel); D row group
   const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 64;
@@ -237,10 +238,29 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_c4_kernel(ConvParams p) {
         v[2] = ep_bn_relu(v[2], mu.z, is.z, ga.z, be.z);
         v[3] = ep_bn_relu(v[3], mu.w, is.w, ga.w, be.w);
       }
-      if (pn[pb] >= 0)
-        *reinterpret_cast<float4*>(p.y + (size_t)(m0 + wave * 64 + pb * 16 + l16) * p.ldy + c) =
-            make_float4(v[0], v[1], v[2], v[3]);
     }
+  }
+  // the output leaves through a per-wave LDS stage, 16 pixels at a time: a lane holds 4 channels of one
+  // pixel per accumulator (64-B pieces of 16 rows per store instruction); staged, each store
+  // instruction writes 4 whole 256-B rows (rows padded to 68 floats: conflict-free 16-B writes)
+  float* st = stg[wave];
+#pragma unroll
+  for (int pb = 0; pb < NPB; ++pb) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+      *reinterpret_cast<float4*>(st + l16 * 68 + cb * 16 + lg * 4) =
+          make_float4(acc[pb][cb][0], acc[pb][cb][1], acc[pb][cb][2], acc[pb][cb][3]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's stage writes are done
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = k * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(st + row * 68 + c4);
+      const int m = m0 + wave * 64 + pb * 16 + row;
+      if (m < p.P) *reinterpret_cast<float4*>(p.y + (size_t)m * p.ldy + n0 + c4) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the reads are back before the next block overwrites the stage
+    __builtin_amdgcn_wave_barrier();
   }
   if (p.ep_amax != nullptr) {
     float mx = 0.f;

@@ -6,7 +6,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 L=${1:-bridge.3,dec3.conv1,dec2.conv1,enc2.conv2}
-for D in 0 1 2 4 16 23 128; do
+for D in ${H4_DBG:-0 1 2 4 16 128}; do
   echo "== dbg $D"
   if [ $D = 0 ]; then unset SRPDE_LIB; else export SRPDE_LIB=$R/superresolution_for_pdes_amd/lib/dbg/libsrpde_dbg$D.so; fi
   timeout -k 10 120 python tools/conv_bench.py --layers $L --only fwd,dgrad --iters 10 2>&1 | grep -v amdgpu || exit 1
