@@ -128,6 +128,9 @@ def parse():
     ap.add_argument("--poisson-sizes", default="40:1024,80:1024,160:64,320:16,640:4",
                     help="n:B pairs for --workload poisson")
     ap.add_argument("--checkpoint", default=None, help="--workload cascade: model_state_dict checkpoint")
+    ap.add_argument("--cascade-fixture", default=None,
+                    help="--workload cascade: the reference's 20->640 output for these weights (npz key ml640_from20, "
+                         "every 3rd row / 5th column; tests/golden/cascade640_fixture.npz with the cascade20 state)")
     ap.add_argument("--ddp", action="store_true",
                     help="use the process group + DataParallel path even at world size 1 (RCCL smoke check)")
     return ap.parse_args()
@@ -359,6 +362,11 @@ def run_cascade(args, world, rank, dev):
     if rank != 0:
         return
     m = RC.cascade_metrics(pred.cpu().numpy(), data["u"][640])
+    ref_err = None
+    if args.cascade_fixture:
+        ref = np.load(args.cascade_fixture)["ml640_from20"].astype(np.float64)
+        pn = np.asarray(pred.cpu().numpy(), dtype=np.float64).reshape(640, 640)[::3, ::5]
+        ref_err = float(np.sqrt(np.mean((pn - ref) ** 2)) / np.sqrt(np.mean(ref ** 2)))
     ms = 1e3 * el / args.steps
     tiles = 1 + 4 + 16 + 64 + 256
     rec = {"metric": "20->640 cascade latency (5 levels, 256 tiles at the last)", "value": round(ms, 3),
@@ -369,7 +377,8 @@ def run_cascade(args, world, rank, dev):
            "config": {"workload": "config #5 cascade 20->640, eval-mode U-Net, subtrees sharded over ranks",
                       "tiles": tiles, "last_level_batch": 256 // world if world <= 16 else None,
                       "gt_solve_s": round(gt_s, 3), "rmse_vs_gt640": m["rmse"], "mae_vs_gt640": m["mae"],
-                      "tiles_per_s": round(tiles / (ms * 1e-3), 1)}}
+                      "tiles_per_s": round(tiles / (ms * 1e-3), 1),
+                      "rel_err_vs_reference_output": ref_err}}
     if not args.no_cpu_baseline and world == 1:
         st = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         rec["cpu_baseline"] = cpu_baseline_cascade(st, data, args.cpu_seconds)
