@@ -41,8 +41,9 @@ typedef struct ihipStream_t* hipStream_t;
  *      planes with a row stride of cout rounded up to 32) and round 4's additions
  *      (srpde_conv_h4_set, srpde_poisson_debug_abort)
  *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace
- *   6  srpde_conv_fwd: ep_mean, ep_invstd, ep_gamma, ep_beta, ep_amax before the workspace */
-#define SRPDE_ABI_VERSION 6
+ *   6  srpde_conv_fwd: ep_mean, ep_invstd, ep_gamma, ep_beta, ep_amax before the workspace
+ *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa */
+#define SRPDE_ABI_VERSION 7
 
 const char* srpde_last_error(void);
 int srpde_version(void);
@@ -94,7 +95,7 @@ int srpde_conv_h3r_set(int on);
  * (cout % 128 == 0) at W = 10 (dilation 1 or 2) and W = 20 (dilation 1): 1 = the h4 kernel
  * (conv_h4.hip: one-tap weight ring, fragments read a tap ahead; default, SRPDE_H4=0 turns it
  * off), 0 = the h3 8-wave kernel.  Bit-identical outputs, statistics and stored splits.  Returns
- * the previous value.  Tuning and tests. */
+ * the previous value (on < 0: a query, nothing changes).  Tuning and tests. */
 int srpde_conv_h4_set(int on);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
@@ -138,11 +139,18 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                       const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
-                      const float* x1_ca, const float* x1_sa, void* workspace, size_t ws_bytes, hipStream_t stream);
+                      const float* x1_ca, const float* x1_sa, const float* x0_up, int up_ld, int up_h, int up_w,
+                      void* workspace, size_t ws_bytes, hipStream_t stream);
 /* x1_ca [n][c1] / x1_sa [P] (nullable, together, c1 > 0): the second input is an AttentionGate's
  * input x (models.py:119-130) and the conv reads its gated output (x * ca[sample][c]) * sa[pixel]
  * (srpde_att_apply_fwd's expression, formed in the operand transform; xsplit_out and the statistics
  * are those of the gated input) -- the gated tensor is never written.
+ * x0_up (nullable; up_ld its row stride, up_h = h / 2, up_w = w / 2): x0 is the bilinear x2
+ * (align_corners) upsample of this [n][up_h][up_w][c0] tensor, formed in the operand transform from
+ * its low-res rows (models.py:70, 89, 92: the decoder's upsampled input is never written); bit-identical
+ * to reading srpde_upsample_bilinear_fwd's output.  Forward only, no in_scale, and the h4 shapes
+ * (W 20 with 128-column tiles, W 40 with 64); x0 / ldx0 are ignored for the x0 channels; amax0 must
+ * bound |up(x0_up)| (the source's max word does: interpolation is a convex combination).
  * ep_mean / ep_invstd / ep_gamma / ep_beta (nullable, eval mode; no stats / bn_part / accumulate):
  * the epilogue applies the following BatchNorm with its running statistics and the ReLU,
  * y = relu((conv + bias - mean) * invstd * gamma + beta) (srpde_bn_eval_prepare's mean / invstd),
@@ -305,6 +313,13 @@ int srpde_upsample_bilinear_bwd(const float* dout, int lddo, float* dx, int lddx
  * <= 64.  With srpde_att_channel_fwd's ca, srpde_att_apply_fwd then finishes the gate. */
 int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ldo, int n, int h, int w, int ho,
                                       int wo, int c, const float* wg, const float* bg, float* sa, hipStream_t stream);
+/* The spatial attention of the gate whose gating input is up(x) (srpde_upsample_bilinear_gate_fwd's sa),
+ * from the low-resolution x alone: sa[q] = sigmoid(up(x . wg)[q] + bg[0]) -- the 1x1 conv commutes with
+ * the bilinear upsample, so up(x) need not exist (the decoder conv reads it through srpde_conv_fwd_h3's
+ * x0_up).  Equal to the materialised form up to fp32 rounding.  workspace: n h w floats. */
+size_t srpde_upsample_gate_sa_workspace_size(int n, int h, int w);
+int srpde_upsample_gate_sa(const float* x, int ldx, int n, int h, int w, int ho, int wo, int c, const float* wg,
+                           const float* bg, float* sa, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* out[p][c] = x[p][c] * ca[n][c] * sa[p] (models.py:122, 128) */
 int srpde_att_apply_fwd(const float* x, int ldx, int n, int hw, int c, const float* ca, const float* sa, float* out,
                         int ldo, hipStream_t stream);

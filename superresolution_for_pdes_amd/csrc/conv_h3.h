@@ -3,6 +3,7 @@
 // the kernel argument block.  Arithmetic and layouts: conv_h3.hip header comment.
 #pragma once
 #include "conv_common.h"
+#include "resample.h"
 
 namespace srpde {
 
@@ -76,6 +77,11 @@ struct H3Args {
   // (x1[p][c] * ca[n][c]) * sa[p], n = p / (H W) -- att_apply_kernel's expression (pointwise.hip)
   const float* x1_ca;      // [N][c1]
   const float* x1_sa;      // [P]
+  // optional: x0 is up(x0_up), the bilinear x2 (align_corners) upsample of an [N][up_h][up_w] NHWC
+  // tensor (row stride up_ld), formed in the operand transform (models.py:70,89,92: the decoder's
+  // upsampled input is never written)
+  const float* up_src;
+  int up_ld, up_h, up_w;
 };
 
 // the gate above on 8 consecutive channels cc1.. (channel index inside x1) of pixel pix; rows
@@ -110,6 +116,7 @@ static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
 
 // h4 (conv_h4.hip): the 256 x 128 forward / dgrad kernel for the shapes it is instantiated for
 bool h4_supported(int w, int dil, int cout, bool bnb);
+bool h4_up_supported(int w, int dil, int cout);   // the upsampled-input forward (H3Args::up_src)
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes);
 bool h4_on();
 

@@ -1914,7 +1914,7 @@ int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
 
 int srpde_conv_h4_set(int on) {
   const int prev = h4_on() ? 1 : 0;
-  g_h4.store(on ? 1 : 0);
+  if (on >= 0) g_h4.store(on ? 1 : 0);   // on < 0: query only
   return prev;
 }
 
@@ -1966,8 +1966,14 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       int bn_ldy, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                       const float* bn_beta, void* bn_part, float* out_max, const float* ep_mean,
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
-                      const float* x1_ca, const float* x1_sa, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                      const float* x1_ca, const float* x1_sa, const float* x0_up, int up_ld, int up_h, int up_w,
+                      void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
+  SRPDE_CHECK_ARG(x0_up == nullptr || (up_h * 2 == h && up_w * 2 == w && up_ld % 4 == 0 && up_ld >= c0 &&
+                                       aligned16(x0_up) && in_scale == nullptr && ksize == 3 && sign == 1 &&
+                                       h4_on() && h4_up_supported(w, dil, cout)),
+                  "srpde_conv_fwd_h3: an upsampled x0 (x0_up) needs h = 2 up_h, w = 2 up_w, no in_scale, the forward, "
+                  "and a shape the h4 kernel is instantiated for (W 20 / 128 columns, W 40 / 64 columns)");
   SRPDE_CHECK_ARG((x1_ca == nullptr) == (x1_sa == nullptr) && (x1_ca == nullptr || c1 > 0),
                   "srpde_conv_fwd_h3: x1_ca / x1_sa go together and need a second input (c1 > 0)");
   SRPDE_CHECK_ARG(c1 == 0 || (x1 && amax1), "srpde_conv_fwd_h3: x1 / amax1 null with c1>0");
@@ -2005,6 +2011,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   a.in_shift = in_shift;
   a.x1_ca = x1_ca;
   a.x1_sa = x1_sa;
+  a.up_src = x0_up;
+  a.up_ld = up_ld; a.up_h = up_h; a.up_w = up_w;
   a.wide = ldy % 4 == 0 && aligned16(y);
   SRPDE_CHECK_ARG(bn_part == nullptr || (bn_y && bn_mean && bn_invstd && bn_gamma && bn_beta && !accumulate &&
                                           bn_ldy % 4 == 0 && cout % 4 == 0),
@@ -2019,7 +2027,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "bn_part, cout %% 4 == 0");
   p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
-  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
+  if (x0_up != nullptr || (h4_on() && h4_supported(w, dil, cout, false)))
+    return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);

@@ -99,10 +99,13 @@ struct H4Geom {
 // one work item of a persistent workgroup: a whole output tile, or one K-piece of a split tail tile
 struct H4Tile {
   int wg, piece, m0, n0, pix0, c_beg, c_end;
+  int lo;   // UP: the first low-res source pixel the tile's halo reads
   bool tail;
 };
 
-template <int W, int DIL, int BN, int SIGN, bool PRE>
+// UP: x0 is the bilinear x2 upsample of h.up_src (forward, non-PRE only), interpolated from low-res rows
+// DMA'd into F in the per-chunk convert
+template <int W, int DIL, int BN, int SIGN, bool PRE, bool UP = false>
 __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Args h) {
   using G = H4Geom<W, DIL, BN>;
   constexpr int BM = G::BM, WM = 8, WN = 1, SRB = 128;
@@ -124,6 +127,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   static_assert(APT <= 2 && TA >= 1, "A DMAs land before the next chunk's tile is read");
   static_assert(SSTRIDE + 64 < 65536 && ZREL < 65536, "16-bit fragment offsets");
   static_assert(2 * WM * BN * 4 + WM * 2048 <= AROWS * SR, "epilogue scratch fits S");
+  static_assert(!UP || (!PRE && SIGN > 0 && DIL == 1), "the upsampled input: forward, fp32 input");
+  // UP: the low-res rows of a tile's halo, at most (AROWS / W + 2) / 2 + 3 source image rows (two images
+  // when the tile crosses one's end), fit F's FROWS rows
+  static_assert(!UP || ((AROWS / W + 2) / 2 + 3) * (W / 2) <= G::FROWS, "upsample source rows fit F");
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
@@ -155,6 +162,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     t.pix0 = t.m0 - G::HALO;
     t.c_beg = t.tail ? (t.piece * nch) / p.tsplit : 0;
     t.c_end = t.tail ? ((t.piece + 1) * nch) / p.tsplit : nch;
+    t.lo = 0;
+    if constexpr (UP) {   // the low-res row of the tile's first in-tensor halo pixel, x = 0
+      const int pf = max(t.pix0, 0), HWh = p.H * W;
+      const int nn = pf / HWh, yy = (pf - nn * HWh) / W;
+      t.lo = nn * h.up_h * h.up_w + lerp_index(yy, h.up_h, p.H).i0 * h.up_w;
+    }
     return t;
   };
 
@@ -164,6 +177,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
 
   const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
+  const int Plo = UP ? p.N * h.up_h * h.up_w : 0;
+  const int32x4 rsu = make_rsrc(UP ? h.up_src : p.x0, UP ? (unsigned)((size_t)Plo * h.up_ld * 4) : 0u);
   const unsigned plane = (unsigned)p.Cout * (unsigned)p.K;   // fp16 elements per weight plane
   const int32x4 rsw = make_rsrc(h.wsp, 2u * plane * 2u);
   const int ld1 = p.c1 ? p.ldx1 : p.ldx0;
@@ -226,7 +241,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   // chunk k of row r at slot swz(r, k).  Every wave issues exactly the same DMAs per tap whatever the
   // tile: a piece past the tile (q >= NQ / NA) or with nothing to load (!real) is a zero fill into the
   // sink, so the vmcnt counts stay exact.
-  auto issue_a = [&](int pix0, int ch, int u, bool real, int buf) {
+  auto issue_a = [&](const H4Tile& t, int ch, int u, bool real, int buf) {
+    const int pix0 = t.pix0;
     const int q = wave + 8 * u;
     const bool qin = q < (PRE ? G::NQ : G::NA);
     if constexpr (PRE) {
@@ -243,6 +259,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       int ln = lane;   // laundered: formed per DMA, not hoisted into registers held across the loop
       asm volatile("" : "+v"(ln));
       const int r = q * 8 + (ln >> 3);
+      if (UP && !second) {   // F row r = low-res pixel t.lo + r
+        const int lp = t.lo + r;
+        const bool ok = real && qin && lp < Plo;
+        const unsigned voff = (unsigned)((lp * h.up_ld + swz(r, ln & 7) * 4) * 4);
+        dma16s(rsu, ok ? voff : OOB, (unsigned)(ch0 * 4), lds0 + (unsigned)(real && qin ? OFF_F + q * 1024 : OFF_SINK));
+        return;
+      }
       const int pix = pix0 + r;
       const bool ok = real && qin && pix >= 0 && pix < p.P;
       const unsigned voff = (unsigned)((pix * (second ? ld1 : p.ldx0) + swz(r, ln & 7) * 4) * 4);
@@ -283,9 +306,37 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       const int sg = tid + 512 * k;
       if (sg >= AROWS * 4) break;
       const int r = sg >> 2;
-      const char* f = lds + OFF_F + r * 128;
-      float4 v0 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8) * 16);
-      float4 v1 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8 + 1) * 16);
+      float4 v0, v1;
+      if (UP && ch * BK2 < p.c0) {
+        // the upsampled input: up(x)[pix] from the four low-res rows in F, upsample_gate_fwd_px_kernel's
+        // expression (bit-identical to the materialised tensor); rows outside the tensor are 0
+        const int pix = t.pix0 + r;
+        v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (pix >= 0 && pix < p.P) {
+          const int HWh = p.H * W, nn = pix / HWh, rem = pix - nn * HWh, oy = rem / W, ox = rem - oy * W;
+          const Lerp ly = lerp_index(oy, h.up_h, p.H), lx = lerp_index(ox, h.up_w, W);
+          const int b0 = nn * h.up_h * h.up_w - t.lo;
+          const int fa = min(b0 + ly.i0 * h.up_w + lx.i0, G::FROWS - 1), fb = min(b0 + ly.i0 * h.up_w + lx.i1, G::FROWS - 1);
+          const int fd = min(b0 + ly.i1 * h.up_w + lx.i0, G::FROWS - 1), ff = min(b0 + ly.i1 * h.up_w + lx.i1, G::FROWS - 1);
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const int k = 2 * c8 + hf;
+            const float4 a = *reinterpret_cast<const float4*>(lds + OFF_F + fa * 128 + swz(fa, k) * 16);
+            const float4 b = *reinterpret_cast<const float4*>(lds + OFF_F + fb * 128 + swz(fb, k) * 16);
+            const float4 d = *reinterpret_cast<const float4*>(lds + OFF_F + fd * 128 + swz(fd, k) * 16);
+            const float4 f = *reinterpret_cast<const float4*>(lds + OFF_F + ff * 128 + swz(ff, k) * 16);
+            float4 o;
+#define UPL(X) o.X = ly.l0 * (lx.l0 * a.X + lx.l1 * b.X) + ly.l1 * (lx.l0 * d.X + lx.l1 * f.X);
+            UPL(x) UPL(y) UPL(z) UPL(w)
+#undef UPL
+            (hf == 0 ? v0 : v1) = o;
+          }
+        }
+      } else {
+        const char* f = lds + OFF_F + r * 128;
+        v0 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8) * 16);
+        v1 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8 + 1) * 16);
+      }
       if (gate) gate8(v0, v1, h, t.pix0 + r, p.P, p.H * W, p.c1, ch * BK2 - p.c0 + c8 * 8);
       if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
         const int pix = t.pix0 + r;
@@ -351,7 +402,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       if constexpr (!(SRPDE_CONV_DBG & 1)) {   // (timing-only diagnostics, conv_common.h: 1 = no DMA in the taps)
         if constexpr (T * APT < APW) {
 #pragma unroll
-          for (int a = 0; a < APT; ++a) issue_a(tn.pix0, chn, T * APT + a, more, (gch + 1) & 1);
+          for (int a = 0; a < APT; ++a) issue_a(tn, chn, T * APT + a, more, (gch + 1) & 1);
         }
         constexpr int TP = T + PD;
         if constexpr (TP < 9) issue_b(cur.n0, ch, TP, (slot + PD) % NBR, true);
@@ -441,7 +492,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   int it = blockIdx.x;
   H4Tile cur = tile_of(it);
 #pragma unroll
-  for (int u = 0; u < APW; ++u) issue_a(cur.pix0, cur.c_beg, u, true, 0);
+  for (int u = 0; u < APW; ++u) issue_a(cur, cur.c_beg, u, true, 0);
 #pragma unroll
   for (int t = 0; t < PD; ++t) issue_b(cur.n0, cur.c_beg, t, t, true);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -568,7 +619,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
 }
 
 // ---------------------------------- host side ---------------------------------------
-template <int W, int DIL, int BN_, int SIGN, bool PRE>
+template <int W, int DIL, int BN_, int SIGN, bool PRE, bool UP = false>
 static int launch_h4_cfg(ConvParams p, H3Args h, hipStream_t st, void* ws, size_t ws_bytes) {
   using G = H4Geom<W, DIL, BN_>;
   constexpr int BM = G::BM, BN = G::BN;
@@ -587,7 +638,8 @@ static int launch_h4_cfg(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   // K-pieces of the split tail)
   const int nitems = T - p.ntail + p.ntail * p.tsplit;
   const int grid = G::PERSIST ? std::min(nitems, cus) : nitems;
-  hipLaunchKernelGGL((conv_fwd_h4_kernel<W, DIL, BN, SIGN, PRE>), dim3(grid), dim3(512), G::template lds<PRE>(), st, p, h);
+  hipLaunchKernelGGL((conv_fwd_h4_kernel<W, DIL, BN, SIGN, PRE, UP>), dim3(grid), dim3(512), G::template lds<PRE>(), st,
+                     p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h4)");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, 128>(p, st);
   return 0;
@@ -601,7 +653,19 @@ bool h4_supported(int w, int dil, int cout, bool bnb) {
   return (w == 10 && (dil == 1 || dil == 2)) || (w == 20 && dil == 1) || (w == 40 && dil == 1);
 }
 
+bool h4_up_supported(int w, int dil, int cout) {
+  return dil == 1 && cout % 64 == 0 && ((w == 20 && h4_bn(w, cout) == 128) || (w == 40 && h4_bn(w, cout) == 64));
+}
+
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes) {
+  if (h.up_src != nullptr) {   // the upsampled input: the decoder's first convs (forward)
+    if (!pre && p.sign > 0 && p.dil == 1 && p.W == 20 && h4_bn(20, p.Cout) == 128)
+      return launch_h4_cfg<20, 1, 128, 1, false, true>(p, h, st, ws, ws_bytes);
+    if (!pre && p.sign > 0 && p.dil == 1 && p.W == 40 && h4_bn(40, p.Cout) == 64)
+      return launch_h4_cfg<40, 1, 64, 1, false, true>(p, h, st, ws, ws_bytes);
+    set_error("srpde_conv_fwd_h3: no upsampled-input instantiation for W=%d dil=%d cout=%d", p.W, p.dil, p.Cout);
+    return kErrArg;
+  }
 #define H4_CASE(W_, D_, BN_)                                                                          \
   if (p.W == W_ && p.dil == D_ && h4_bn(W_, p.Cout) == BN_) {                                         \
     if (pre) return p.sign > 0 ? launch_h4_cfg<W_, D_, BN_, 1, true>(p, h, st, ws, ws_bytes)          \

@@ -5,6 +5,7 @@
 // Reference anchors (src/models.py): pool :69,:79-80; up :70,:89-93; AttentionGate
 // :103-130; final 1x1 + residual :61,:74,:98,:101; nn.MSELoss src/train_enhanced.py:307.
 #include "common.h"
+#include "resample.h"
 
 namespace srpde {
 
@@ -115,27 +116,6 @@ __global__ void maxpool2_bwd_kernel(const float* __restrict__ x, int ldx, const 
 }
 
 // ----------------------------- bilinear upsample x2 ------------------------------
-// align_corners=True: src = dst * (in-1)/(out-1) (float, as aten area_pixel_compute_scale),
-// i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
-struct Lerp { int i0, i1; float l0, l1; };
-__device__ __forceinline__ Lerp lerp_index(int o, int in, int out) {
-  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-  // rounded product, as aten's area_pixel_compute_source_index: with contraction on, the compiler
-  // may fuse src - i0 below into fma(scale, o, -i0) (it did once packed-FP32 ops were disabled), which
-  // moves the weights by up to an ulp of src (~2e-6 at src ~ 19) and the interpolated values with them
-  float src;
-  {
-#pragma clang fp contract(off)
-    src = scale * (float)o;
-  }
-  Lerp r;
-  r.i0 = (int)src;
-  r.i1 = r.i0 + (r.i0 < in - 1 ? 1 : 0);
-  r.l1 = src - (float)r.i0;
-  r.l0 = 1.f - r.l1;
-  return r;
-}
-
 __global__ void upsample_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out, int ldo, int N,
                                     int H, int W, int Ho, int Wo, int C) {
   const int C4 = C >> 2;
@@ -388,6 +368,35 @@ __global__ __launch_bounds__(256) void upsample_gate_fwd_px_kernel(const float* 
     for (int off = 1; off < (int)blockDim.x; off <<= 1) acc += __shfl_xor(acc, off, 64);
     if (on && threadIdx.x == 0) sa[q] = 1.f / (1.f + expf(-(acc + bias)));
   }
+}
+
+// The spatial attention of a gate whose gating input is up(x), from x at low resolution: the 1x1 conv
+// commutes with the bilinear upsample, sa = sigmoid(up(x . wg) + bg) (models.py:124-125 with
+// g = up(d), :89 / :92) -- for a decoder conv that reads up(x) without materialising it.  The dot
+// products reduce like upsample_gate_fwd_px_kernel's (one pixel per c/4 threads, shuffle tree).
+__global__ __launch_bounds__(256) void gate_dot_px_kernel(const float* __restrict__ x, int ldx, unsigned npix,
+                                                          const float* __restrict__ wg, float* __restrict__ t) {
+  const unsigned q = px_index();
+  const bool on = q < npix;
+  const int c = threadIdx.x * 4;
+  const float4 wv = *reinterpret_cast<const float4*>(wg + c);
+  const float4 o = on ? *reinterpret_cast<const float4*>(x + (size_t)q * ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float acc = o.x * wv.x + o.y * wv.y + o.z * wv.z + o.w * wv.w;
+  for (int off = 1; off < (int)blockDim.x; off <<= 1) acc += __shfl_xor(acc, off, 64);
+  if (on && threadIdx.x == 0) t[q] = acc;
+}
+
+__global__ __launch_bounds__(256) void up_sigmoid_kernel(const float* __restrict__ t, float* __restrict__ sa,
+                                                         unsigned npix, int H, int W, int Ho, int Wo,
+                                                         const float* __restrict__ bg) {
+  const unsigned q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= npix) return;
+  const unsigned ox = q % (unsigned)Wo, r = q / (unsigned)Wo, oy = r % (unsigned)Ho, n = r / (unsigned)Ho;
+  const Lerp ly = lerp_index(oy, H, Ho), lx = lerp_index(ox, W, Wo);
+  const float* b = t + (size_t)n * H * W;
+  const float a0 = b[ly.i0 * W + lx.i0], a1 = b[ly.i0 * W + lx.i1], d0 = b[ly.i1 * W + lx.i0], d1 = b[ly.i1 * W + lx.i1];
+  const float v = ly.l0 * (lx.l0 * a0 + lx.l1 * a1) + ly.l1 * (lx.l0 * d0 + lx.l1 * d1);
+  sa[q] = 1.f / (1.f + expf(-(v + bg[0])));
 }
 
 // gsa / gw (nullable): the attention gating gradient folded in, the upsampled tensor's gradient
@@ -1163,6 +1172,25 @@ int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ld
   hipLaunchKernelGGL(upsample_gate_fwd_px_kernel, g, b, 0, stream, x, ldx, out, ldo, (unsigned)(n * ho * wo), h, w,
                      ho, wo, wg, bg, sa);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_gate_fwd");
+  return 0;
+}
+
+size_t srpde_upsample_gate_sa_workspace_size(int n, int h, int w) { return (size_t)n * h * w * sizeof(float); }
+
+int srpde_upsample_gate_sa(const float* x, int ldx, int n, int h, int w, int ho, int wo, int c, const float* wg,
+                           const float* bg, float* sa, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(x && wg && bg && sa && workspace && ldx % 4 == 0 && c % 4 == 0 && c / 4 >= 1 && c / 4 <= 64 &&
+                      ((c / 4) & (c / 4 - 1)) == 0 && n > 0 && h > 0 && w > 0 && ho > 0 && wo > 0,
+                  "srpde_upsample_gate_sa: bad args (c / 4 a power of two <= 64)");
+  SRPDE_CHECK_ARG(ws_bytes >= srpde_upsample_gate_sa_workspace_size(n, h, w), "srpde_upsample_gate_sa: workspace");
+  float* t = static_cast<float*>(workspace);
+  dim3 g, b;
+  SRPDE_CHECK_ARG(px_geometry((long long)n * h * w, c, &g, &b), "srpde_upsample_gate_sa: bad geometry");
+  hipLaunchKernelGGL(gate_dot_px_kernel, g, b, 0, stream, x, ldx, (unsigned)(n * h * w), wg, t);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_gate_sa(dot)");
+  const unsigned np = (unsigned)(n * ho * wo);
+  hipLaunchKernelGGL(up_sigmoid_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, t, sa, np, h, w, ho, wo, bg);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_gate_sa(up)");
   return 0;
 }
 

@@ -122,6 +122,51 @@ def h3_capable(c0, c1, cout, w, dil, ksize=3):
     return _CONV_MATH == "h3" and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, ksize))
 
 
+class UpsampledInput:
+    """up(x): the bilinear x2 (align_corners) upsample of the NHWC rows ``x`` ([n h w, c]) -- models.py:70,
+    89, 92 -- that is not formed: the decoder conv reading it as x0 interpolates its operand tile from x's
+    low-res rows (srpde_conv_fwd_h3 x0_up).  ``materialize()`` forms it (srpde_upsample_bilinear_fwd)."""
+    __slots__ = ("x", "n", "h", "w", "_t")
+
+    def __init__(self, x, n, h, w):
+        self.x, self.n, self.h, self.w, self._t = x, n, h, w, None
+
+    @property
+    def shape(self):
+        return (self.n * 4 * self.h * self.w, self.x.shape[1])
+
+    @property
+    def device(self):
+        return self.x.device
+
+    @property
+    def _srpde_amax(self):   # a bound on |up(x)|: interpolation is a convex combination
+        return amax_of(self.x)
+
+    def materialize(self):
+        if self._t is None:
+            self._t = tag_amax(upsample_fwd(self.x, self.n, self.h, self.w, 2 * self.h, 2 * self.w),
+                               getattr(self.x, "_srpde_amax", None))
+        return self._t
+
+
+def conv_fwd_up_capable(c0, c1, cout, w, dil):
+    """Whether conv_fwd takes an UpsampledInput x0 for this shape (the h4 instantiations)."""
+    return (_CONV_MATH == "h3" and dil == 1 and ((w == 20 and cout % 128 == 0) or (w == 40 and cout % 64 == 0))
+            and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, 3))
+            and bool(query("srpde_conv_h4_set", -1)))
+
+
+def upsample_gate_sa(x, n, h, w, ho, wo, wg, bg):
+    """The spatial attention of the gate whose gating input is up(x), from x alone (srpde_upsample_gate_sa)."""
+    sa = empty(n * ho * wo, device=x.device)
+    ws = _scratch(int(query("srpde_upsample_gate_sa_workspace_size", n, h, w)), x.device)
+    px, ldx = _pl(x)
+    call("srpde_upsample_gate_sa", px, ldx, n, h, w, ho, wo, x.shape[1], wg.data_ptr(), bg.data_ptr(), sa.data_ptr(),
+         ws.data_ptr(), ws.numel(), stream_ptr())
+    return sa
+
+
 def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accumulate=False, stats=None,
              planes_out=None, in_affine=None, bn_bwd=None, out_max=None, ep_bn=None, x1_gate=None):
     """Convolution (sign +1) or its input gradient (sign -1, dgrad-packed weights).  h3 only:
@@ -132,8 +177,15 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     ``ep_bn = (mean, invstd, gamma, beta, amax)`` (eval mode) applies the following BatchNorm and
     ReLU in the epilogue, so ``y`` is the activation, and writes max|y| into ``amax``.
     ``x1_gate = (ca [n, c1], sa [P])``: x1 is an AttentionGate's input and the conv reads its gated
-    output (x1 * ca) * sa, formed in the operand transform (the gated tensor is never written)."""
-    p0, ld0 = _pl(x0)
+    output (x1 * ca) * sa, formed in the operand transform (the gated tensor is never written).
+    ``x0`` may be an UpsampledInput (h4 shapes, forward): its operand is interpolated from x0.x's rows."""
+    up = x0 if isinstance(x0, UpsampledInput) else None
+    if up is not None and not (_CONV_MATH == "h3" and sign == 1 and in_affine is None
+                               and conv_fwd_up_capable(x0.shape[1], x1.shape[1] if x1 is not None else 0, cout, w,
+                                                       dil)):
+        x0 = up.materialize()
+        up = None
+    p0, ld0 = _pl(x0.x if up is not None else x0)
     if x1 is not None:
         p1, ld1 = _pl(x1)
         c1 = x1.shape[1]
@@ -153,7 +205,8 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
              *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), _p(x1_gate[0] if x1_gate else None),
-             _p(x1_gate[1] if x1_gate else None), ws.data_ptr(), ws.numel(), stream_ptr())
+             _p(x1_gate[1] if x1_gate else None), p0 if up is not None else 0, ld0 if up is not None else 0,
+             up.h if up is not None else 0, up.w if up is not None else 0, ws.data_ptr(), ws.numel(), stream_ptr())
         if ep_bn is not None:
             tag_amax(y, ep_bn[4])
         if planes_out is not None:

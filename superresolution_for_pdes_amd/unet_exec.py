@@ -410,6 +410,8 @@ _FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
 # the gates' spatial attention formed by the upsample that produces their gating input
 # (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
 _FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
+# inference: the decoder's first convs read up(d) from d's rows (H.UpsampledInput; SRPDE_FUSE_UP=0: formed)
+_FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "1") != "0"
 # enc1's / enc2's gate channel branch from the BN + ReLU + pool pass (srpde_bn_relu_pool_att_fwd, one
 # block per sample; SRPDE_FUSE_ATT_CH=0: a separate pass over the activation)
 _FUSE_ATT_CH = os.environ.get("SRPDE_FUSE_ATT_CH", "1") != "0"
@@ -668,8 +670,15 @@ def _att_fwd(att, x, g, n, hw, early=None, sa=None):
     return H.att_gate_fwd(x, g, n, hw, chan, s0.weight, s0.bias)
 
 
-def _upsample_for_gate(d, att, n, h, w, ho, wo):
-    """up(d) for the decoder, and (SRPDE_FUSE_SA) the spatial attention of ``att`` whose gate it is."""
+def _upsample_for_gate(d, att, n, h, w, ho, wo, conv=None, c1=0, fuse=False):
+    """up(d) for the decoder, and (SRPDE_FUSE_SA) the spatial attention of ``att`` whose gate it is.
+    ``fuse`` (inference; ``conv`` the decoder conv reading up(d) as x0 beside ``c1`` gated channels):
+    up(d) is not formed -- an UpsampledInput the conv interpolates from d's rows (SRPDE_FUSE_UP=0: off),
+    the gate's spatial attention computed from d at low resolution (srpde_upsample_gate_sa)."""
+    if (fuse and _FUSE_UP and _FUSE_SA and _FUSE_ATT_APPLY and d.is_cuda and conv is not None
+            and H.conv_fwd_up_capable(d.shape[1], c1, conv.out_channels, wo, 1)):
+        s0 = att.spatial_attention[0]
+        return H.UpsampledInput(d, n, h, w), H.upsample_gate_sa(d, n, h, w, ho, wo, s0.weight, s0.bias)
     if _FUSE_SA and d.shape[1] in (128, 256) and d.is_cuda:
         s0 = att.spatial_attention[0]
         return H.upsample_gate_fwd(d, n, h, w, ho, wo, s0.weight, s0.bias)
@@ -734,10 +743,11 @@ def unet_forward(m, x, training, save=False):
     # decoder with attention, virtual concat
     e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3, early=ch3, sa=sa3)
     d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
-    u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2)
+    fuse_up = not training and not save   # inference: the decoder convs read up(d) without it being formed
+    u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2, m.dec2.conv1, e2.shape[1], fuse_up)
     e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2, sa=sa2)
     d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
-    u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w)
+    u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w, m.dec1.conv1, e1.shape[1], fuse_up)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1, sa=sa1)
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
     # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)

@@ -162,3 +162,54 @@ def test_gated_second_input_equals_materialized(n, c0, c1, cout, hw, h4):
         H.set_h4(prev)
     for name, a, b_ in zip(("y", "stats", "xsplit", "y_eval", "amax_eval"), *outs):
         assert torch.equal(a, b_), name
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,hw", [
+    (9, 256, 128, 128, 20),    # dec2.conv1: [up(d3), att2(e2)]
+    (5, 128, 64, 64, 40),      # dec1.conv1: [up(d2), att1(e1)]
+    (44, 128, 64, 64, 40),     # many tiles per persistent workgroup, image boundaries inside tiles
+])
+def test_upsampled_input_equals_materialized(n, c0, c1, cout, hw):
+    """The decoder conv reading up(d) through x0_up (the bilinear x2 upsample formed in the operand
+    transform from d's low-res rows, models.py:70,89,92) equals, bit for bit, the same conv reading
+    the tensor srpde_upsample_bilinear_fwd writes (same operand scale: the source's max word): output,
+    BN statistics, stored input split, eval epilogue output and max word.  The gate's spatial attention
+    from d at low resolution (srpde_upsample_gate_sa) equals the materialised form's to fp32 rounding."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator(device=DEV).manual_seed(5)
+    hl = hw // 2
+    d = torch.randn(n * hl * hl, c0, device=DEV, generator=g)
+    e = torch.randn(n * hw * hw, c1, device=DEV, generator=g)
+    ca = torch.sigmoid(torch.randn(n, c1, device=DEV, generator=g))
+    cin = c0 + c1
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, _ = H.pack_conv_weights(w, cin, True, False)
+    wg = torch.randn(1, c0, 1, 1, device=DEV, generator=g) * 0.1
+    bg = torch.randn(1, device=DEV, generator=g)
+    emean, einv = torch.randn(cout, device=DEV, generator=g) * 0.1, torch.rand(cout, device=DEV, generator=g) + 0.5
+    ega, ebe = torch.randn(cout, device=DEV, generator=g), torch.randn(cout, device=DEV, generator=g) * 0.1
+    d._srpde_amax = H.amax_of(d)
+    e._srpde_amax = H.amax_of(e)
+    u, sa_ref = H.upsample_gate_fwd(d, n, hl, hl, hw, hw, wg, bg)
+    sa = H.upsample_gate_sa(d, n, hl, hl, hw, hw, wg, bg)
+    P = n * hw * hw
+    prev = H.set_h4(True)
+    outs = []
+    try:
+        for x0 in (u, H.UpsampledInput(d, n, hl, hl)):
+            y = torch.empty(P, cout, device=DEV)
+            stats, _, _ = H.conv_stats_buffer(n, hw, hw, cout, DEV, c0, c1, 1)
+            xp = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, e, wf, b, y, n, hw, hw, cout, 3, 1, 1, False, stats, xp, x1_gate=(ca, sa_ref))
+            ye = torch.empty(P, cout, device=DEV)
+            eam = torch.zeros(1, dtype=torch.int32, device=DEV)
+            H.conv_fwd(x0, e, wf, b, ye, n, hw, hw, cout, 3, 1, 1, False, None, ep_bn=(emean, einv, ega, ebe, eam),
+                       x1_gate=(ca, sa_ref))
+            torch.cuda.synchronize()
+            outs.append((y, stats, xp, ye, eam))
+    finally:
+        H.set_h4(prev)
+    for name, a, b_ in zip(("y", "stats", "xsplit", "y_eval", "amax_eval"), *outs):
+        assert torch.equal(a, b_), name
+    assert float((sa - sa_ref).abs().max()) <= 1e-6, float((sa - sa_ref).abs().max())

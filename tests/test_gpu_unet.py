@@ -424,3 +424,25 @@ def test_eval_epilogue_bn_matches_separate_passes(B):
     err = float((outs[0] - outs[1]).norm() / outs[1].norm())
     print(f"eval epilogue vs separate: rel {err:.3e}, bit-equal {torch.equal(outs[0], outs[1])}")
     assert err <= 1e-6, err
+
+
+def test_eval_fused_upsample_matches_materialized():
+    """Inference forward with the decoder's upsampled inputs read from the low-res rows (unet_exec._FUSE_UP:
+    up(d3) / up(d2) never formed, the gates' spatial attention from d at low resolution) against the
+    materialised upsample: the conv operands are bit-identical (tests/test_gpu_h4.py), the spatial
+    attention moves by fp32 rounding, so the outputs agree to 1e-6."""
+    from superresolution_for_pdes_amd import unet_exec
+    m = make_model(False)
+    x = torch.randn(24, 3, 40, 40, generator=torch.Generator().manual_seed(2)).to(DEV)
+    x[:, 1] = 1.0
+    outs = []
+    saved = unet_exec._FUSE_UP
+    try:
+        for on in (True, False):
+            unet_exec._FUSE_UP = on
+            with torch.no_grad():
+                outs.append(m(x).double().cpu())
+    finally:
+        unet_exec._FUSE_UP = saved
+    err = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    assert err <= 1e-6, err
