@@ -42,7 +42,8 @@ typedef struct ihipStream_t* hipStream_t;
  *      (srpde_conv_h4_set, srpde_poisson_debug_abort)
  *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace
  *   6  srpde_conv_fwd: ep_mean, ep_invstd, ep_gamma, ep_beta, ep_amax before the workspace
- *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa */
+ *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa;
+ *      srpde_conv_head_eval */
 #define SRPDE_ABI_VERSION 7
 
 const char* srpde_last_error(void);
@@ -320,6 +321,17 @@ int srpde_upsample_bilinear_gate_fwd(const float* x, int ldx, float* out, int ld
 size_t srpde_upsample_gate_sa_workspace_size(int n, int h, int w);
 int srpde_upsample_gate_sa(const float* x, int ldx, int n, int h, int w, int ho, int wo, int c, const float* wg,
                            const float* bg, float* sa, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* The output head in inference, one pass (models.py:59-61, 98-101, eval mode): out[p] =
+ * final(relu(bn2(out_conv2(z))))[p] + xin[n][0][q], z = [n h w][32] (row stride ldz) with its max|z|
+ * word, out_conv2's h3 forward planes [2][16][288] / wexp[16] (srpde_split_weights_h3) and bias,
+ * out_bn2's eval constants (srpde_bn_eval_prepare's mean / invstd, gamma, beta), final's weight [16] /
+ * bias [1], xin the U-Net input (NCHW, xin_c channels).  out_conv2's values equal the h3 kernels';
+ * the 16-channel dot sums in another order than srpde_head_fwd.  Replaces srpde_conv_fwd_h3 (out_conv2,
+ * ep_*) + srpde_head_fwd.  Needs w <= 63. */
+int srpde_conv_head_eval(const float* z, int ldz, const unsigned* amax_z, const void* wsplit, const int* wexp,
+                         const float* bias, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                         const float* bn_beta, const float* wf, const float* bf, const float* xin, int xin_c, int n,
+                         int h, int w, float* out, hipStream_t stream);
 /* out[p][c] = x[p][c] * ca[n][c] * sa[p] (models.py:122, 128) */
 int srpde_att_apply_fwd(const float* x, int ldx, int n, int hw, int c, const float* ca, const float* sa, float* out,
                         int ldo, hipStream_t stream);

@@ -756,6 +756,17 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
 
 
 # ------------------------------------- head ----------------------------------------
+def conv_head_eval(z, wpack, bias, mean, invstd, gamma, beta, wf, bf, xin, n, h, w):
+    """out_conv2 -> BN (eval) -> ReLU -> final -> + residual in one pass (srpde_conv_head_eval) -> [n h w]."""
+    planes, wexp = wpack.h3
+    out = empty(n * h * w, device=z.device)
+    pz, ldz = _pl(z)
+    call("srpde_conv_head_eval", pz, ldz, amax_of(z).data_ptr(), planes.data_ptr(), wexp.data_ptr(), _p(bias),
+         mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), wf.data_ptr(), bf.data_ptr(),
+         xin.data_ptr(), xin.shape[1], n, h, w, out.data_ptr(), stream_ptr())
+    return out
+
+
 def head_fwd(z, wf, bf, xin, n, hw):
     out = empty(n * hw, device=z.device)
     pz, ldz = _pl(z)

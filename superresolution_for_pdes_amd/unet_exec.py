@@ -410,6 +410,9 @@ _FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
 # the gates' spatial attention formed by the upsample that produces their gating input
 # (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
 _FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
+# inference: out_conv2 + out_bn2 + ReLU + final + residual in one kernel (srpde_conv_head_eval; SRPDE_FUSE_HEAD=0:
+# out_conv2 on the conv kernels, then srpde_head_fwd)
+_FUSE_HEAD = os.environ.get("SRPDE_FUSE_HEAD", "1") != "0"
 # inference: the decoder's first convs read up(d) from d's rows (H.UpsampledInput; SRPDE_FUSE_UP=0: formed)
 _FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "1") != "0"
 # enc1's / enc2's gate channel branch from the BN + ReLU + pool pass (srpde_bn_relu_pool_att_fwd, one
@@ -765,6 +768,15 @@ def unet_forward(m, x, training, save=False):
         o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots, in_affine=o1aff)
     else:
         o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots, in_affine=d1aff)
+        if (getattr(slots, "eval_epilogue", False) and _FUSE_HEAD and o1.shape[1] == 32
+                and m.out_conv2.out_channels == 16 and H.h3_capable(32, 0, 16, w, 1)):
+            # inference: out_conv2 -> out_bn2 -> ReLU -> final -> + residual in one pass (o2 never written)
+            bn = m.out_bn2
+            mean, invstd = _eval_stats(bn)
+            wf = _fwd_weights(m.out_conv2, 32, 32, 0, w, 1)
+            out = H.conv_head_eval(o1, wf, m.out_conv2.bias, mean, invstd, bn.weight, bn.bias, m.final.weight,
+                                   m.final.bias, x, n, h, w)
+            return out.view(n, 1, h, w), None
         o2, S.out2 = _cbr_fwd(m.out_conv2, m.out_bn2, o1, None, n, h, w, training, 1, slots)
     out = H.head_fwd(o2, m.final.weight, m.final.bias, x, n, hw1)
     if not save:

@@ -446,3 +446,25 @@ def test_eval_fused_upsample_matches_materialized():
         unet_exec._FUSE_UP = saved
     err = float((outs[0] - outs[1]).norm() / outs[1].norm())
     assert err <= 1e-6, err
+
+
+def test_eval_fused_head_matches_separate_passes():
+    """Inference forward with out_conv2 -> out_bn2 -> ReLU -> final -> residual in one kernel
+    (unet_exec._FUSE_HEAD, srpde_conv_head_eval) against out_conv2 on the conv kernels + srpde_head_fwd:
+    out_conv2's values are the same h3 arithmetic; the final 16-channel dot sums in another order, so the
+    outputs agree to fp32 rounding (1e-6 relative), and both sit within the reference bar."""
+    from superresolution_for_pdes_amd import unet_exec
+    m = make_model(False)
+    x = torch.randn(20, 3, 40, 40, generator=torch.Generator().manual_seed(3)).to(DEV)
+    x[:, 1] = 1.0
+    outs = []
+    saved = unet_exec._FUSE_HEAD
+    try:
+        for on in (True, False):
+            unet_exec._FUSE_HEAD = on
+            with torch.no_grad():
+                outs.append(m(x).double().cpu())
+    finally:
+        unet_exec._FUSE_HEAD = saved
+    err = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    assert err <= 1e-6, err
