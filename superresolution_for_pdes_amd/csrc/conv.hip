@@ -200,22 +200,27 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_c4_kernel(ConvParams p) {
   for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[pb][cb] = c4x4{0.f, 0.f, 0.f, 0.f};
+  // every tap's operand loads issued before the first MFMA (unconditional loads of a clamped address,
+  // the out-of-image ones zeroed after): one memory round trip per wave instead of one per tap
+  float xb[9][NPB];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int oy = (t / 3 - 1) * p.dil * p.sign, ox = (t % 3 - 1) * p.dil * p.sign;
-    float xb[NPB];
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb) {
       const int iy = py[pb] + oy, ix = px[pb] + ox;
-      xb[pb] = (pn[pb] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-                   ? p.x0[(size_t)(pn[pb] + iy * p.W + ix) * 4 + lg] : 0.f;
+      const bool ok = pn[pb] >= 0 && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      const float v = p.x0[(size_t)(ok ? pn[pb] + iy * p.W + ix : 0) * 4 + lg];
+      xb[t][pb] = ok ? v : 0.f;
     }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int pb = 0; pb < NPB; ++pb)
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
-        acc[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][cb], xb[pb], acc[pb][cb], 0, 0, 0);
-  }
+        acc[pb][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][cb], xb[t][pb], acc[pb][cb], 0, 0, 0);
   // lane: pixel m0 + 64 wave + 16 pb + l16, channels n0 + 16 cb + 4 lg + 0..3
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {

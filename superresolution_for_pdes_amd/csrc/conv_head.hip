@@ -52,6 +52,12 @@ __global__ __launch_bounds__(256, 4) void conv_head_eval_kernel(HeadArgs a) {
     bh[t] = *reinterpret_cast<const half8*>(a.wsp + o);
     bl[t] = *reinterpret_cast<const half8*>(a.wsp + 16 * 288 + o);
   }
+  // the channel scale to undo and the BN / head constants of this lane's channel n = l16: loaded with
+  // the tile, not after the MFMAs
+  const int we = a.wexp[l16], e = ea + we;
+  const float bn = a.bias ? a.bias[l16] : 0.f;
+  const float mu = a.mean[l16], is = a.invstd[l16], ga = a.gamma[l16], be = a.beta[l16], wfn = a.wf[l16];
+  const float bfv = a.bf[0];
   // the split halo tile: task (row r, 8 channels c8); rows outside the tensor are zero.  Every task's
   // loads are issued before any is split (HEAD_IT tasks per thread: w <= 63), not one round trip each
   if (tid < 32) reinterpret_cast<float*>(lds + zrel)[tid] = 0.f;
@@ -78,13 +84,8 @@ __global__ __launch_bounds__(256, 4) void conv_head_eval_kernel(HeadArgs a) {
   }
   __syncthreads();
 
-  // the channel scale to undo and the BN / head constants of this lane's channel n = l16
-  const int we = a.wexp[l16], e = ea + we;
   const bool wide = e > 126 || e < -126;
   const float ia = exp2i(-ea), cs = wide ? exp2i(-we) : exp2i(-e);
-  const float bn = a.bias ? a.bias[l16] : 0.f;
-  const float mu = a.mean[l16], is = a.invstd[l16], ga = a.gamma[l16], be = a.beta[l16], wfn = a.wf[l16];
-  const float bfv = a.bf[0];
 
 #pragma unroll
   for (int i = 0; i < HEAD_RB; ++i) {
