@@ -222,7 +222,50 @@ def cpu_baseline_poisson(seconds, sizes=(40, 80)):
     return out
 
 
-def run_poisson(args, world, rank, dev):
+def measure_traffic_poisson(sizes):
+    """HBM bytes per launch of the Poisson kernels (cg_lds_kernel, gcg_coop_kernel), measured now:
+    two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; --kernel-trace only) over this script solving
+    `sizes` once, FETCH_SIZE doubled (MI355X_MICROARCH.md's gfx950 correction).  Child processes under
+    a hard time limit, started before this process touches the GPU.  -> dict or None."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return {"error": "rocprofv3 not found"}
+    d = tempfile.mkdtemp(prefix="srpde_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", c, "--kernel-trace", "--output-format", "csv",
+                   "-d", d, "-o", f"p{i}", "--", sys.executable, os.path.abspath(__file__), "--workload", "poisson",
+                   "--poisson-sizes", sizes, "--steps", "1", "--no-cpu-baseline", "--no-live-traffic"]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                return {"error": f"PMC pass {c} rc {r.returncode}: {r.stderr[-300:]}"}
+        vals = {}
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                for k in ("cg_lds", "gcg_coop_kernel"):   # cg_lds_kernel<NPT> / cg_lds_n_kernel<N, T>
+                    if k in r["Kernel_Name"]:
+                        vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+        out = {"sizes": sizes}
+        for k in ("cg_lds", "gcg_coop_kernel"):
+            fe, wr = vals.get((k, "FETCH_SIZE")), vals.get((k, "WRITE_SIZE"))
+            if fe and wr:
+                out[k] = round(1024 * (2 * sum(fe) / len(fe) + sum(wr) / len(wr)))
+        if len(out) == 1:
+            out["error"] = f"no counter rows for the CG kernels ({len(vals)} series)"
+        return out
+    except Exception as e:   # noqa: BLE001 -- the bench line must not depend on the profiler
+        return {"error": f"PMC measurement failed: {e}"}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def run_poisson(args, world, rank, dev, pmc=None):
     """Config #3: batched on-device CG (HIP) solves/s.  Each rank solves its own B problems
     per size (independent units, weak scaling, no collective)."""
     import numpy as np
@@ -258,24 +301,39 @@ def run_poisson(args, world, rank, dev):
         if n <= 128:   # LDS-resident: fp64 VALU bound, 19 flop / point / iteration
             lv["fp64_tflops"] = round(19 * pts_it / t / 1e12, 3)
             lv["fp64_frac"] = round(19 * pts_it / t / 78.6e12, 4)
-        else:          # grid CG: HBM bound, 88 B / point / iteration
-            lv["hbm_gbs"] = round(88 * pts_it / t / 1e9, 1)
-            lv["hbm_frac"] = round(88 * pts_it / t / 8.0e12, 4)
+        else:
+            # grid CG: every point's state stays on chip for the whole solve (registers + LDS, DESIGN
+            # 3.6), so HBM moves only f, theta, u (24 B / point / solve) and the edge rows exchanged per
+            # iteration; the bound is the iteration's latency chain (one grid barrier + two round
+            # trips), reported per iteration of the slowest problem in the batch
+            lv["max_iters"] = int(it.max())
+            lv["us_per_iter"] = round(1e6 * t / max(1, int(it.max())), 2)
         levels[n] = lv
     if rank != 0:
         return
-    head = levels.get(80) or next(iter(levels.values()))
-    big = max(levels)
+    hn = 80 if 80 in levels else min(levels)
+    head = levels[hn]
     rec = {"metric": "Poisson CG solves/s (batched fp64 5-point, rtol 1e-12)",
            "value": head["solves_per_s"], "unit": "solves/s", "n_gpus": world, "steps": args.steps,
            "warmup": 1, "ms_per_step": head["ms_per_batch"], "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f64",
            "data": "synthetic: f = sin(2 pi k1 x) sin(2 pi k2 y), k ~ U(0.5,12), theta ~ U(0.5,2), in HBM",
-           "config": {"workload": "config #3 on-device data-gen solve, headline n=80 B=1024/GPU",
-                      "levels": {str(k): v for k, v in levels.items()}},
-           "roofline": {"bound": "hbm", "kernel": f"poisson_cg_grid[n={big}]",
-                        "achieved": levels[big].get("hbm_gbs"), "peak": 8000.0, "unit": "GB/s",
-                        "frac": levels[big].get("hbm_frac"), "traffic": None}}
+           "config": {"workload": f"config #3 on-device data-gen solve, headline n={hn} B={head['B']}/GPU",
+                      "levels": {str(k): v for k, v in levels.items()}}}
+    if hn <= 128:   # the headline kernel: the LDS-resident CG, fp64 VALU bound (dense fp64 vector peak)
+        rec["roofline"] = {"bound": "fp64-valu",
+                           "kernel": "cg_lds_n_kernel<80, 960>" if hn == 80 else f"cg_lds_kernel[n={hn}]",
+                           "achieved": head["fp64_tflops"],
+                           "peak": 78.6, "unit": "TFLOP/s", "frac": head["fp64_frac"],
+                           "traffic": (pmc or {}).get("cg_lds"),
+                           "traffic_note": "HBM bytes per launch (one batch), rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                           "measured by this run; algorithmic 24 B per point (f, theta in, u out) = "
+                                           f"{24 * head['B'] * hn * hn} B"}
+        if pmc and pmc.get("error"):
+            rec["roofline"]["traffic_note"] += f"; live measurement unavailable: {pmc['error']}"
+        if pmc and pmc.get("gcg_coop_kernel"):
+            rec["grid_cg_traffic"] = {"kernel": "gcg_coop_kernel", "bytes_per_launch": pmc["gcg_coop_kernel"],
+                                      "sizes": pmc.get("sizes")}
     if not args.no_cpu_baseline and world == 1:
         cb = cpu_baseline_poisson(min(args.cpu_seconds, 10.0))
         rec["cpu_baseline"] = {"value": round(cb[80], 2), "unit": "solves/s", "cores": 1, "kind": "port",
@@ -459,6 +517,13 @@ def main():
     if (ws is None and args.workload == "train" and not args.no_live_traffic and args.traffic_json is None
             and not args.ddp):
         live_traffic = measure_traffic_live(args.roofline_layer)   # before this process touches the GPU
+    pmc_poisson = None
+    if ws is None and args.workload == "poisson" and not args.no_live_traffic:
+        head = [s for s in args.poisson_sizes.split(",") if int(s.split(":")[0]) <= 128]
+        # the headline LDS CG only: a counter-collection run that made a cooperative launch (the grid
+        # CG) crashed at process exit after writing its counters (profiles/r04q_poisson_pmc.txt)
+        if head:
+            pmc_poisson = measure_traffic_poisson(next((s for s in head if s.startswith("80:")), head[0]))
     # RCCL prints its version block on fd 1 at communicator creation: keep fd 1 for the JSON line
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")
@@ -488,7 +553,10 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.workload != "train":
-        (run_poisson if args.workload == "poisson" else run_cascade)(args, world, rank, dev)
+        if args.workload == "poisson":
+            run_poisson(args, world, rank, dev, pmc_poisson)
+        else:
+            run_cascade(args, world, rank, dev)
         if use_pg:
             dist.destroy_process_group()
         return

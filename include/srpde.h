@@ -11,7 +11,7 @@
  * Conventions
  *  - All tensor arguments are caller-owned DEVICE pointers; the library never allocates,
  *    frees or synchronises the host (one exception: srpde_poisson_cg_batched for a single problem
- *    too large for one cooperative grid, n > ~1400).  Scratch is passed in as (workspace, ws_bytes), its
+ *    too large for one cooperative grid, n > 1024).  Scratch is passed in as (workspace, ws_bytes), its
  *    size queried with the matching *_workspace_size() function.
  *  - Activations are NHWC fp32 ("channels-last").  A view is (pointer, ld): ld = floats
  *    between consecutive pixels, so channel slices of a wider tensor (virtual concat) need

@@ -28,19 +28,33 @@ constexpr int CG_MAXT = 1024;
 // fp64 wave reduction on the DPP network (no LDS round trips): butterfly within quads, rotations
 // within 16-lane rows, then the GFX9 row broadcasts fold the four rows into lane 63, read back as a
 // wave-uniform value.  Fixed order: every wave of every block sums identically.
-template <int CTRL, int ROWS>
+// FULL: the pattern writes every lane, so no `old` operand is needed (mov_dpp: no zeroing or copy
+// move before it); the row broadcasts write only the masked rows and keep 0 elsewhere
+template <int CTRL, int ROWS, bool FULL = true>
 __device__ __forceinline__ double dpp_f64(double v) {
   const int lo = __double2loint(v), hi = __double2hiint(v);
+  if (FULL)
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, CTRL, ROWS, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(lo, CTRL, ROWS, 0xf, false));
   return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, ROWS, 0xf, false),
                           __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWS, 0xf, false));
+}
+// the sum of lanes 0..15 (the rest contribute 0), wave-uniform
+__device__ __forceinline__ double row0_sum_dpp(double v) {
+  v += dpp_f64<0xB1, 0xf>(v);
+  v += dpp_f64<0x4E, 0xf>(v);
+  v += dpp_f64<0x124, 0xf>(v);
+  v += dpp_f64<0x128, 0xf>(v);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 0), hi = __builtin_amdgcn_readlane(__double2hiint(v), 0);
+  return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_f64<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
   v += dpp_f64<0x124, 0xf>(v);   // row_ror:4
   v += dpp_f64<0x128, 0xf>(v);   // row_ror:8   (every lane: its row's sum)
-  v += dpp_f64<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
-  v += dpp_f64<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3 (lane 63: the wave's sum)
+  v += dpp_f64<0x142, 0xa, false>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc, false>(v);   // row_bcast:31 into rows 2, 3 (lane 63: the wave's sum)
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63), hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
   return __hiloint2double(hi, lo);
 }
@@ -53,8 +67,20 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* slots) 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
   if (lane == 0) { slots[w] = a; slots[16 + w] = b; }
   __syncthreads();
-  a = wave_sum_dpp(lane < nw ? slots[lane] : 0.0);
-  b = wave_sum_dpp(lane < nw ? slots[16 + lane] : 0.0);
+  // nw <= 16 wave sums: one 16-lane row reduces them (same order in every wave)
+  a = row0_sum_dpp(lane < nw ? slots[lane] : 0.0);
+  b = row0_sum_dpp(lane < nw ? slots[16 + lane] : 0.0);
+}
+
+// The Chronopoulos-Gear scalars of the next iteration from gamma_new = <r, r>, delta_new = <A r, r>:
+// beta = gamma_new / gamma, alpha = gamma_new / (delta_new - beta gamma_new / alpha), the latter
+// multiplied through by c = gamma alpha so that the two divisions are independent (one division
+// latency on the iteration's critical path instead of three)
+__device__ __forceinline__ void cg_scalars(double gn, double dn, double& gamma, double& alpha, double& beta) {
+  const double c = gamma * alpha;
+  beta = gn / gamma;
+  alpha = (gn * c) / (dn * c - gn * gn);
+  gamma = gn;
 }
 
 // Chronopoulos-Gear CG (the same Krylov iterates as textbook CG, rearranged so that both inner
@@ -85,7 +111,7 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
     x[k] = 0.0; p[k] = 0.0; s[k] = 0.0; w[k] = 0.0;
     if (i < N2) {
       const int yy = i / n, xx = i - yy * n;
-      li[k] = (yy + 1) * ld + xx + 1;
+      li[k] = yy * ld + xx;   // the point's up-left corner in rl: every neighbour at a positive offset
       r[k] = -f[off + i] / theta[off + i];
     } else {
       li[k] = -1;
@@ -100,8 +126,8 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       if (li[k] >= 0) {
-        const int c = li[k];
-        w[k] = (4.0 * r[k] - rl[c - 1] - rl[c + 1] - rl[c - ld] - rl[c + ld]) * inv_h2;
+        const double* q = rl + li[k];
+        w[k] = (4.0 * r[k] - q[ld] - q[ld + 2] - q[1] - q[2 * ld + 1]) * inv_h2;
         g += r[k] * r[k];
         d += w[k] * r[k];
       }
@@ -116,7 +142,7 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
   };
 #pragma unroll
   for (int k = 0; k < NPT; ++k)
-    if (li[k] >= 0) rl[li[k]] = r[k];
+    if (li[k] >= 0) rl[li[k] + ld + 1] = r[k];
   __syncthreads();
   double gamma, delta;
   apply_reduce(gamma, delta);
@@ -124,23 +150,27 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
   const double g0 = gamma;
   double alpha = gamma / delta, beta = 0.0;
   int it = 0;
-  while (gamma > stop && it < maxit) {
+  auto step = [&]() {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       p[k] = r[k] + beta * p[k];
       s[k] = w[k] + beta * s[k];
       x[k] += alpha * p[k];
       r[k] -= alpha * s[k];
-      if (li[k] >= 0) rl[li[k]] = r[k];
+      if (li[k] >= 0) rl[li[k] + ld + 1] = r[k];
     }
     ++it;
     __syncthreads();   // r visible to the neighbours' stencils (all reads of the old r are done:
                        // they precede the reduction barrier every thread has passed)
     double gn, dn;
     apply_reduce(gn, dn);
-    beta = gn / gamma;
-    alpha = gn / (dn - beta * gn / alpha);
-    gamma = gn;
+    cg_scalars(gn, dn, gamma, alpha, beta);
+  };
+  // two iterations per trip: one per trip rotated the loop-carried vectors through register copies
+  while (gamma > stop && it < maxit) {
+    step();
+    if (!(gamma > stop && it < maxit)) break;
+    step();
   }
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -148,6 +178,91 @@ __global__ __launch_bounds__(CG_MAXT) void cg_lds_kernel(const double* __restric
     if (i < N2) u[off + i] = x[k];
   }
   if (threadIdx.x == 0) {
+    if (iters) iters[blockIdx.x] = it;
+    if (resid) resid[blockIdx.x] = sqrt(gamma / (g0 > 0.0 ? g0 : 1.0));
+  }
+}
+
+// cg_lds_kernel with the grid size a compile-time constant (used at n = 80):
+// T = (T / n) rows of n points per slab, point k of a lane NPT = ceil(n / (T / n)) slabs down, so one
+// LDS address register serves all of a lane's points and every neighbour read is an immediate offset
+// (the generic kernel held NPT addresses and spilled at n = 80: 19 VGPRs, scratch reloads inside the
+// stencil).  Same recurrence, expressions and reduction order as cg_lds_kernel.
+template <int N, int T>
+__global__ __launch_bounds__(T) void cg_lds_n_kernel(const double* __restrict__ f, const double* __restrict__ theta,
+                                                     double* __restrict__ u, double rtol, int maxit,
+                                                     int* __restrict__ iters, double* __restrict__ resid) {
+  constexpr int LD = N + 2, RPS = T / N, NPT = (N + RPS - 1) / RPS, SLAB = RPS * LD, N2 = N * N;
+  static_assert(T % N == 0 && T % 64 == 0 && T <= CG_MAXT, "slab layout");
+  __shared__ double rl[LD * LD];
+  __shared__ double slots[64];
+  const size_t off = (size_t)blockIdx.x * N2;
+  const double inv_h2 = (double)(N - 1) * (double)(N - 1);
+  const int tid = threadIdx.x, row = tid / N, col = tid - row * N;
+  const bool last_ok = (NPT - 1) * RPS + row < N;   // points k < NPT - 1 always exist
+  double* qb = rl + row * LD + col;                 // point k's up-left corner: qb + k * SLAB
+
+  for (int e = tid; e < LD * LD; e += T) rl[e] = 0.0;
+  double x[NPT], r[NPT], p[NPT], s[NPT], w[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    x[k] = 0.0; p[k] = 0.0; s[k] = 0.0; w[k] = 0.0;
+    r[k] = (k < NPT - 1 || last_ok) ? -f[off + tid + k * T] / theta[off + tid + k * T] : 0.0;
+  }
+  __syncthreads();   // ghost ring zeroed before interior writes
+  int par = 0;
+  auto apply_reduce = [&](double& gamma, double& delta) {
+    double g = 0.0, d = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (k < NPT - 1 || last_ok) {
+        const double* q = qb + k * SLAB;
+        w[k] = (4.0 * r[k] - q[LD] - q[LD + 2] - q[1] - q[2 * LD + 1]) * inv_h2;
+        g += r[k] * r[k];
+        d += w[k] * r[k];
+      }
+    }
+    block_sum2(g, d, slots + 32 * par);
+    par ^= 1;
+    gamma = g;
+    delta = d;
+  };
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (k < NPT - 1 || last_ok) qb[k * SLAB + LD + 1] = r[k];
+  __syncthreads();
+  double gamma, delta;
+  apply_reduce(gamma, delta);
+  const double stop = rtol * rtol * gamma;
+  const double g0 = gamma;
+  double alpha = gamma / delta, beta = 0.0;
+  int it = 0;
+  auto step = [&]() {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      p[k] = r[k] + beta * p[k];
+      s[k] = w[k] + beta * s[k];
+      x[k] += alpha * p[k];
+      r[k] -= alpha * s[k];
+      if (k < NPT - 1 || last_ok) qb[k * SLAB + LD + 1] = r[k];
+    }
+    ++it;
+    __syncthreads();
+    double gn, dn;
+    apply_reduce(gn, dn);
+    cg_scalars(gn, dn, gamma, alpha, beta);
+  };
+  // two iterations per trip: the loop-carried vectors keep their registers (one iteration per trip
+  // rotated them through copies, ~45 moves per iteration)
+  while (gamma > stop && it < maxit) {
+    step();
+    if (!(gamma > stop && it < maxit)) break;
+    step();
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (k < NPT - 1 || last_ok) u[off + tid + k * T] = x[k];
+  if (tid == 0) {
     if (iters) iters[blockIdx.x] = it;
     if (resid) resid[blockIdx.x] = sqrt(gamma / (g0 > 0.0 ? g0 : 1.0));
   }
@@ -312,8 +427,8 @@ __global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restr
 // serialised atomics per barrier instead of one per block on a single address.
 constexpr int COOP_GRP = 16;
 struct GridCoop {
-  double *r, *p0, *p1;          // [B][N2]
-  double *rrp, *pqp;            // [B][nb] per-block partials
+  double *er[2], *ew[2], *es[2];   // [B][N2] by parity: r, w = A r, s = A p at a block's edge points
+  double *gp[2], *dp[2];           // [B][nb] by parity: per-block partials of gamma = <r, r>, delta = <w, r>
   unsigned long long* bar;      // [0] groups arrived, [1 + g] blocks of group g arrived
   unsigned* ctl;                // [0] problems converged, [1] abort
   int n, nb, B, ngrp;
@@ -393,119 +508,215 @@ __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long 
   return *sflag == 0;
 }
 
-__global__ __launch_bounds__(GCG_T) void gcg_coop_kernel(const double* __restrict__ f,
+// Chronopoulos-Gear CG (cg_lds_kernel's recurrence) with ONE grid barrier per iteration.  After the
+// barrier every block sums the (gamma, delta) partials, forms alpha / beta, updates its points
+// (p = r + beta p, s = w + beta s, x += alpha p, r -= alpha s) and computes w = A r with the new r.  A
+// neighbour point in another block is not read after it was updated -- that would cost a barrier --
+// but recomputed from its owner's (r, w, s) of the previous iteration, stored at the owner's edge
+// points, with the owner's fused expressions (so the same bits as the owner holds).  Edge values and
+// partials alternate between two buffers by iteration parity: a block that is already writing
+// iteration k + 1's never overwrites what a slower block still reads of iteration k.
+//
+// A block is 1024 threads x NPT points: p, s, w in registers, x in LDS (read once at the end), r in
+// LDS with a halo of n points either side (the previous block's last row, the next block's
+// first), so the stencil reads LDS only, branch-free behind a per-thread neighbour mask.  NPT = 8
+// (8192-point blocks) puts 4 problems at 640^2 or 64 at 160^2 into one co-resident grid of one block
+// per CU; the halo loads of an iteration are issued before its partial sums, so the two round trips
+// overlap.
+constexpr int GCC_T = 1024, GCC_HQ = 2;   // halo points per thread: 2 n <= 2 * 1024 (3 spilled at NPT = 8)
+__host__ __device__ constexpr size_t gcc_lds_bytes(int npt, int n) {
+  return ((size_t)2 * GCC_T * npt + 2 * (size_t)n) * sizeof(double);
+}
+
+template <int NPT>
+__global__ __launch_bounds__(GCC_T) void gcg_coop_kernel(const double* __restrict__ f,
                                                          const double* __restrict__ theta, double* __restrict__ u,
                                                          int* __restrict__ iters, GridCoop g, int maxit) {
-  __shared__ double sh[8];
+  constexpr int PTS = GCC_T * NPT, NW = GCC_T / 64;
+  extern __shared__ double lds_d[];
+  __shared__ double sh[2 * NW + 2];
   __shared__ int sflag;
-  __shared__ double pl[GCG_PTS];   // this block's new search direction (the in-block stencil reads)
+  const int tid = threadIdx.x;
   const int b = blockIdx.x / g.nb, j = blockIdx.x - b * g.nb;
   const int n = g.n, N2 = n * n;
   const size_t off = (size_t)b * N2;
-  const int lo = j * GCG_PTS, hi = min(N2, lo + GCG_PTS);
-  // r and p of the block's first / last n points are what the neighbouring blocks' stencils read:
-  // only those are written to (and read from) the coherent global copies
-  auto edge = [&](int i) { return i < lo + n || i >= hi - n; };
+  const int lo = j * PTS, hi = min(N2, lo + PTS), cnt = hi - lo;
+  double* rl = lds_d;               // rl[q + n]: r at point lo + q, q in [-n, cnt + n)
+  double* xl = lds_d + PTS + 2 * n; // xl[q]
   unsigned long long epoch = 0;
   const double inv_h2 = (double)(n - 1) * (double)(n - 1);
-  const double* rpart = g.rrp + (size_t)b * g.nb;
-  const double* qpart = g.pqp + (size_t)b * g.nb;
-  double* rv = g.r + off;
-  double x[GCG_NPT], r[GCG_NPT], p[GCG_NPT], q[GCG_NPT];
-  double s = 0.0;
+
+  // neighbour mask, bits 4 k + (left, right, up, down) of point k
+  unsigned nbm = 0;
 #pragma unroll
-  for (int k = 0; k < GCG_NPT; ++k) {
-    const int i = lo + k * GCG_T + threadIdx.x;
-    x[k] = 0.0; p[k] = 0.0; q[k] = 0.0; r[k] = 0.0;
-    if (i < hi) {
-      r[k] = -f[off + i] / theta[off + i];
-      if (edge(i)) {
-        st_ag(rv + i, r[k]);
-        st_ag(g.p0 + off + i, 0.0);
-      }
-      s += r[k] * r[k];
+  for (int k = 0; k < NPT; ++k) {
+    const int q = k * GCC_T + tid;
+    if (q < cnt) {
+      const int i = lo + q, yy = i / n, xx = i - yy * n;
+      nbm |= ((xx > 0 ? 1u : 0u) | (xx < n - 1 ? 2u : 0u) | (yy > 0 ? 4u : 0u) | (yy < n - 1 ? 8u : 0u)) << (4 * k);
     }
   }
-  write_part_ag(s, sh, g.rrp + (size_t)b * g.nb + j);
+  // halo point h of this thread: rl index and grid point (-1: outside the grid)
+  int hidx[GCC_HQ], hpt[GCC_HQ];
+#pragma unroll
+  for (int q = 0; q < GCC_HQ; ++q) {
+    const int h = tid + q * GCC_T;
+    hidx[q] = h < n ? h : cnt + h;
+    const int pt = h < n ? lo - n + h : hi + (h - n);
+    hpt[q] = (h < 2 * n && pt >= 0 && pt < N2) ? pt : -1;
+    if (h < 2 * n) rl[hidx[q]] = 0.0;
+  }
+  auto is_edge = [&](int q) { return q < n || q >= cnt - n; };
+
+  // r lives in rl only (the register copy made NPT = 8 spill)
+  double p[NPT], s[NPT], w[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int q = k * GCC_T + tid;
+    p[k] = 0.0; s[k] = 0.0; w[k] = 0.0;
+    if (q < cnt) {
+      const double r0 = -f[off + lo + q] / theta[off + lo + q];
+      rl[q + n] = r0;
+      xl[q] = 0.0;
+      if (is_edge(q)) st_ag(g.er[0] + off + lo + q, r0);
+    }
+  }
   bool ok = coop_sync(g, ++epoch, &sflag);
-  const double bb = sum_parts_ag(rpart, g.nb, sh);
-  double rr = bb, rr_old = 1.0;
+
+  // w = A r from rl; (gamma, delta) partials and the edge (r, w, s) of parity `par`
+  auto apply = [&](int par, int lt) {
+    double gs = 0.0, ds = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int q = k * GCC_T + lt, c = q + n;
+      if (q < cnt) {
+        const unsigned m = nbm >> (4 * k);
+        const double rc = rl[c];
+        double acc = 0.0;
+        acc += (m & 1u) ? rl[c - 1] : 0.0;
+        acc += (m & 2u) ? rl[c + 1] : 0.0;
+        acc += (m & 4u) ? rl[c - n] : 0.0;
+        acc += (m & 8u) ? rl[c + n] : 0.0;
+        w[k] = (4.0 * rc - acc) * inv_h2;
+        gs += rc * rc;
+        ds += w[k] * rc;
+        if (is_edge(q)) {
+          const size_t e = off + lo + q;
+          st_ag(g.er[par] + e, rc);
+          st_ag(g.ew[par] + e, w[k]);
+          st_ag(g.es[par] + e, s[k]);
+        }
+      }
+    }
+    gs = wave_sum(gs);
+    ds = wave_sum(ds);
+    if ((tid & 63) == 0) { sh[tid >> 6] = gs; sh[NW + (tid >> 6)] = ds; }
+    __syncthreads();
+    if (tid == 0) {
+      double tg = 0.0, td = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < NW; ++k) { tg += sh[k]; td += sh[NW + k]; }
+      st_ag(g.gp[par] + (size_t)b * g.nb + j, tg);
+      st_ag(g.dp[par] + (size_t)b * g.nb + j, td);
+    }
+  };
+
+  if (ok) {
+#pragma unroll
+    for (int q = 0; q < GCC_HQ; ++q)
+      if (hpt[q] >= 0) rl[hidx[q]] = ld_ag(g.er[0] + off + hpt[q]);
+    __syncthreads();
+    apply(0, tid);
+  }
+  ok = ok && coop_sync(g, ++epoch, &sflag);
+  double gamma = 0.0, stop = 0.0, alpha = 0.0, beta = 0.0;
   bool done = false;
   int it_done = maxit;
   for (int k = 0; ok; ++k) {
-    // A (gcg_a_kernel): convergence, beta, p <- r + beta p, q = A p, <p, q> partials
-    if (!done && (rr <= g.rtol * g.rtol * bb || k >= maxit)) {
+    const int par = k & 1;
+    // per-thread offsets re-derived every iteration: hoisted, they were 64-bit addresses per array and
+    // parity (NPT = 8 spilled)
+    int lt = tid;
+    asm volatile("" : "+v"(lt));
+    int hp[GCC_HQ];
+#pragma unroll
+    for (int q = 0; q < GCC_HQ; ++q) { hp[q] = hpt[q]; asm volatile("" : "+v"(hp[q])); }
+    double hr[GCC_HQ], hw[GCC_HQ], hs[GCC_HQ];
+    if (!done) {
+#pragma unroll
+      for (int q = 0; q < GCC_HQ; ++q) {
+        hr[q] = hw[q] = hs[q] = 0.0;
+        if (hp[q] >= 0) {
+          const size_t e = off + hp[q];
+          hr[q] = ld_ag(g.er[par] + e);
+          hw[q] = ld_ag(g.ew[par] + e);
+          hs[q] = ld_ag(g.es[par] + e);
+        }
+      }
+    }
+    // both partial sums in one pass (one round trip)
+    double gs = 0.0, ds = 0.0;
+    for (int t = tid; t < g.nb; t += GCC_T) {
+      gs += ld_ag(g.gp[par] + (size_t)b * g.nb + t);
+      ds += ld_ag(g.dp[par] + (size_t)b * g.nb + t);
+    }
+    gs = wave_sum(gs);
+    ds = wave_sum(ds);
+    if ((tid & 63) == 0) { sh[tid >> 6] = gs; sh[NW + (tid >> 6)] = ds; }
+    __syncthreads();
+    // one thread adds the wave sums (every thread doing it held all 32 in registers: NPT = 8 spilled)
+    if (tid == 0) {
+      double tg = 0.0, td = 0.0;
+#pragma unroll 1
+      for (int t = 0; t < NW; ++t) { tg += sh[t]; td += sh[NW + t]; }
+      sh[2 * NW] = tg;
+      sh[2 * NW + 1] = td;
+    }
+    __syncthreads();
+    const double gn = sh[2 * NW], dn = sh[2 * NW + 1];
+    if (k == 0) {
+      stop = g.rtol * g.rtol * gn;
+      alpha = gn / dn;
+      beta = 0.0;
+    } else if (!done) {
+      beta = gn / gamma;
+      alpha = gn / (dn - beta * gn / alpha);
+    }
+    if (!done) gamma = gn;
+    if (!done && (gamma <= stop || k >= maxit)) {
       done = true;
       it_done = k;
-      if (j == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(g.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j == 0 && tid == 0) __hip_atomic_fetch_add(g.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!done) {
-      const double beta = k == 0 ? 0.0 : rr / rr_old;
-      const double* po = ((k & 1) ? g.p1 : g.p0) + off;
-      double* pn = ((k & 1) ? g.p0 : g.p1) + off;
 #pragma unroll
-      for (int kk = 0; kk < GCG_NPT; ++kk) {
-        const int i = lo + kk * GCG_T + threadIdx.x;
-        if (i < hi) {
-          const double pc = r[kk] + beta * p[kk];
-          p[kk] = pc;
-          pl[i - lo] = pc;
-          if (edge(i)) st_ag(pn + i, pc);
+      for (int kk = 0; kk < NPT; ++kk) {
+        const int q = kk * GCC_T + tid;
+        if (q < cnt) {
+          const double rk = rl[q + n];
+          p[kk] = __builtin_fma(beta, p[kk], rk);
+          s[kk] = __builtin_fma(beta, s[kk], w[kk]);
+          xl[q] = __builtin_fma(alpha, p[kk], xl[q]);
+          rl[q + n] = __builtin_fma(-alpha, s[kk], rk);
         }
       }
+#pragma unroll
+      for (int q = 0; q < GCC_HQ; ++q)
+        if (hp[q] >= 0) rl[hidx[q]] = __builtin_fma(-alpha, __builtin_fma(beta, hs[q], hw[q]), hr[q]);
       __syncthreads();
-      // a neighbour in another block: its p = r + beta p_old from that block's stored copies (the
-      // same expression on the same values, so the same bits as its owner holds)
-      auto pv = [&](int jj) { return (jj >= lo && jj < hi) ? pl[jj - lo] : ld_ag(rv + jj) + beta * ld_ag(po + jj); };
-      s = 0.0;
-#pragma unroll
-      for (int kk = 0; kk < GCG_NPT; ++kk) {
-        const int i = lo + kk * GCG_T + threadIdx.x;
-        if (i < hi) {
-          const int yy = i / n, xx = i - yy * n;
-          double nb = 0.0;
-          if (xx > 0) nb += pv(i - 1);
-          if (xx < n - 1) nb += pv(i + 1);
-          if (yy > 0) nb += pv(i - n);
-          if (yy < n - 1) nb += pv(i + n);
-          q[kk] = (4.0 * p[kk] - nb) * inv_h2;
-          s += p[kk] * q[kk];
-        }
-      }
-      write_part_ag(s, sh, g.pqp + (size_t)b * g.nb + j);
+      apply(par ^ 1, lt);
     }
     ok = coop_sync(g, ++epoch, &sflag);
     // every increment of ctl[0] precedes this barrier and the next one follows these reads: all
     // blocks read the same count and leave together
     if (!ok || __hip_atomic_load(g.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)g.B) break;
-    // B (gcg_b_kernel): alpha, x += alpha p, r -= alpha q, <r, r> partials
-    if (!done) {
-      const double alpha = rr / sum_parts_ag(qpart, g.nb, sh);
-      s = 0.0;
-#pragma unroll
-      for (int kk = 0; kk < GCG_NPT; ++kk) {
-        const int i = lo + kk * GCG_T + threadIdx.x;
-        if (i < hi) {
-          x[kk] += alpha * p[kk];
-          r[kk] = r[kk] - alpha * q[kk];
-          if (edge(i)) st_ag(rv + i, r[kk]);
-          s += r[kk] * r[kk];
-        }
-      }
-      write_part_ag(s, sh, g.rrp + (size_t)b * g.nb + j);
-    }
-    ok = coop_sync(g, ++epoch, &sflag);
-    if (!done) {
-      rr_old = rr;
-      rr = sum_parts_ag(rpart, g.nb, sh);
-    }
   }
 #pragma unroll
-  for (int k = 0; k < GCG_NPT; ++k) {
-    const int i = lo + k * GCG_T + threadIdx.x;
-    if (i < hi) u[off + i] = x[k];
+  for (int k = 0; k < NPT; ++k) {
+    const int q = k * GCC_T + tid;
+    if (q < cnt) u[off + lo + q] = xl[q];
   }
-  if (j == 0 && threadIdx.x == 0 && iters) iters[b] = ok ? it_done : -1;
+  if (j == 0 && tid == 0 && iters) iters[b] = ok ? it_done : -1;
 }
 
 static GridCG carve(void* ws, int B, int n) {
@@ -535,7 +746,7 @@ static size_t grid_ws_bytes(int B, int n) {
   const size_t N2 = (size_t)n * n;
   const size_t nb = (N2 + GCG_PTS - 1) / GCG_PTS;
   return (4 * B * N2 + 4 * (size_t)B * nb) * sizeof(double) + 2 * (size_t)B * sizeof(int) + 64 +
-         coop_ctl_bytes(B, n);
+         coop_ctl_bytes(B, n) + (2 * B * N2 + 1) * sizeof(double);   // + the cooperative CG's s edges
 }
 // past carve()'s last array (iters), 8-byte aligned
 static unsigned long long* coop_ctl(void* ws, int B, int n) {
@@ -588,6 +799,13 @@ size_t srpde_poisson_workspace_size(int B, int n) { return n <= 128 ? 0 : grid_w
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream) {
   SRPDE_CHECK_ARG(f && theta && u && B > 0 && n >= 2 && n <= 128, "srpde_poisson_cg_lds: bad args (n<=128)");
+  if (n == 80) {   // config #3's headline size: the compile-time layout (at 20 / 40 the slab layout's
+                   // 320-thread blocks ran 2.3x / 1.2x slower than the generic kernel's 128 / 448)
+    hipLaunchKernelGGL((cg_lds_n_kernel<80, 960>), dim3(B), dim3(960), 0, stream, f, theta, u, rtol, maxit, iters,
+                       resid);
+    SRPDE_LAUNCH_CHECK("srpde_poisson_cg_lds");
+    return 0;
+  }
   const int npt = lds_npt(n);
   int T = ceil_div((long long)n * n, npt);
   T = (T + 63) / 64 * 64;
@@ -641,44 +859,61 @@ int srpde_poisson_cg_grid_finish(double* u, int* iters, int B, int n, int maxit,
   return 0;
 }
 
-// co-resident blocks of gcg_coop_kernel on this device (0: no cooperative launch)
-static int coop_capacity() {
-  static const int cap = [] {
-    int dev = 0, cus = 0, per = 0, coop = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&gcg_coop_kernel), GCG_T, 0) !=
-        hipSuccess)
-      return 0;
-    return coop ? per * cus : 0;
-  }();
-  return cap;
+static const void* coop_kernel(int npt) {
+  switch (npt) {
+    case 2: return reinterpret_cast<const void*>(&gcg_coop_kernel<2>);
+    case 4: return reinterpret_cast<const void*>(&gcg_coop_kernel<4>);
+    default: return reinterpret_cast<const void*>(&gcg_coop_kernel<8>);
+  }
 }
 
-// Problems per cooperative launch at this n (0: one problem does not fit the co-resident grid, or
-// n > GCG_PTS: the kernel's stencil takes the neighbours at i -+ n from the adjacent block only)
-int srpde_poisson_coop_problems(int n) {
-  if (n > GCG_PTS) return 0;
-  const long long nb = ceil_div((long long)n * n, GCG_PTS);
-  return nb <= coop_capacity() ? (int)(coop_capacity() / nb) : 0;
+// co-resident blocks of gcg_coop_kernel<npt> at this n on this device (0: no cooperative launch)
+static int coop_capacity(int npt, int n) {
+  int dev = 0, cus = 0, per = 0, coop = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coop_kernel(npt), GCC_T, gcc_lds_bytes(npt, n)) !=
+      hipSuccess)
+    return 0;
+  return coop ? per * cus : 0;
 }
+
+static int coop_blocks(int npt, int n) { return (int)ceil_div((long long)n * n, (long long)GCC_T * npt); }
+static int coop_per_launch(int npt, int n) {
+  if (2 * n > GCC_HQ * GCC_T || n > GCC_T * npt) return 0;   // halo: the adjacent blocks' rows, <= 2 points per thread
+  const int cap = coop_capacity(npt, n), nb = coop_blocks(npt, n);
+  return nb <= cap ? cap / nb : 0;
+}
+
+// Problems per cooperative launch at this n with the largest blocks (0: one problem does not fit the
+// co-resident grid)
+int srpde_poisson_coop_problems(int n) { return coop_per_launch(8, n); }
 
 // test hook: every cooperative grid-CG launch starts with its abort word set (iters = -1 for every
 // problem of the launch, u undefined), so a caller's abort handling can be exercised
 static std::atomic<int> g_debug_abort{0};
 
-// the whole grid CG of problems [b0, b0 + cnt) in one cooperative launch (workspace carved for B)
+// the whole grid CG of problems [b0, b0 + cnt) in one cooperative launch of gcg_coop_kernel<npt>
+// (workspace carved for B: the polled CG's 2048-point partial arrays hold the larger blocks' too)
 static int coop_solve(const double* f, const double* theta, double* u, int* iters, int b0, int cnt, int B, int n,
-                      double rtol, int maxit, void* ws, hipStream_t stream) {
+                      int npt, double rtol, int maxit, void* ws, hipStream_t stream) {
   const GridCG c = carve(ws, B, n);
   const size_t N2 = (size_t)n * n;
+  const int nb = coop_blocks(npt, n);
   GridCoop g;
-  g.r = c.r + b0 * N2; g.p0 = c.p0 + b0 * N2; g.p1 = c.p1 + b0 * N2;
-  g.rrp = c.rrp0 + (size_t)b0 * c.nb; g.pqp = c.pqp + (size_t)b0 * c.nb;
-  g.n = n; g.nb = c.nb; g.B = cnt; g.rtol = rtol;
-  g.ngrp = ceil_div((long long)cnt * c.nb, COOP_GRP);
-  g.bar = coop_ctl(ws, B, n);
+  // edge values by parity in the polled CG's x / r / p0 / p1 arrays and two more past the ctl words;
+  // the partials in its four [B][nb] arrays
+  unsigned long long* ctl_all = coop_ctl(ws, B, n);
+  double* extra = reinterpret_cast<double*>(reinterpret_cast<char*>(ctl_all) + coop_ctl_bytes(B, n));
+  g.er[0] = c.x + b0 * N2; g.er[1] = c.r + b0 * N2;
+  g.ew[0] = c.p0 + b0 * N2; g.ew[1] = c.p1 + b0 * N2;
+  g.es[0] = extra + b0 * N2; g.es[1] = extra + B * N2 + b0 * N2;
+  g.gp[0] = c.rrp0 + (size_t)b0 * nb; g.gp[1] = c.rrp1 + (size_t)b0 * nb;
+  g.dp[0] = c.pqp + (size_t)b0 * nb; g.dp[1] = c.bbp + (size_t)b0 * nb;
+  g.n = n; g.nb = nb; g.B = cnt; g.rtol = rtol;
+  g.ngrp = ceil_div((long long)cnt * nb, COOP_GRP);
+  g.bar = ctl_all;
   g.ctl = reinterpret_cast<unsigned*>(g.bar + 1 + g.ngrp);
   hipError_t e = hipMemsetAsync(g.bar, 0, (g.ngrp + 2) * sizeof(unsigned long long), stream);
   if (e == hipSuccess && g_debug_abort.load(std::memory_order_relaxed))
@@ -689,8 +924,7 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   double* ub = u + b0 * N2;
   int* ib = iters ? iters + b0 : nullptr;
   void* args[] = {&fb, &tb, &ub, &ib, &g, &maxit};
-  e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&gcg_coop_kernel), dim3(cnt * c.nb), dim3(GCG_T), args,
-                                 0, stream);
+  e = hipLaunchCooperativeKernel(coop_kernel(npt), dim3(cnt * nb), dim3(GCC_T), args, gcc_lds_bytes(npt, n), stream);
   if (e != hipSuccess) {
     set_error("srpde_poisson_cg_batched: cooperative launch failed: %s", hipGetErrorString(e));
     return (int)e;
@@ -704,7 +938,7 @@ int srpde_poisson_debug_abort(int on) { return g_debug_abort.exchange(on ? 1 : 0
 // launch of the LDS-resident CG; n > 128 runs the grid CG as cooperative launches (one per group of
 // srpde_poisson_coop_problems(n) problems), whose grid barriers replace the launch boundaries and
 // whose device-side convergence count ends the loop -- nothing returns to the host.  Only a single
-// problem too large for the co-resident grid (n > ~1400 on MI355X) still runs the launch-per-iteration
+// problem too large for the co-resident grid (n > 1024: the halo bound) still runs the launch-per-iteration
 // grid CG polled from the host every 128 iterations (that case synchronises `stream`).
 // ws: srpde_poisson_workspace_size.
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
@@ -713,10 +947,24 @@ int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, in
   if (n <= srpde_poisson_lds_max_n())
     return srpde_poisson_cg_lds(f, theta, u, B, n, rtol, maxit, iters_out, nullptr, stream);
   SRPDE_CHECK_ARG(workspace && ws_bytes >= grid_ws_bytes(B, n), "srpde_poisson_cg_batched: workspace too small");
-  const int per = srpde_poisson_coop_problems(n);
+  // Block size: every problem in one launch first; then the smallest blocks that keep the grid to at
+  // most half the co-resident capacity -- fewer points per CU against a barrier over more arrivals
+  // (per iteration, one problem: 640^2 12.0 / 9.4 / 9.9 us at 2048 / 4096 / 8192-point blocks,
+  // 160^2 7.0 / 7.5 / 9.0 us; profiles/r04q_poisson_npt.txt); else the largest blocks (fewest launches)
+  int npt = 8;
+  for (int pass = 0; pass < 2 && npt == 8; ++pass)
+    for (int c : {2, 4}) {
+      const int per = coop_per_launch(c, n);
+      if (per >= B && (pass == 1 || 2LL * B * coop_blocks(c, n) <= (long long)per * coop_blocks(c, n))) {
+        npt = c;
+        break;
+      }
+    }
+  const int per = coop_per_launch(npt, n);
   if (per > 0) {
     for (int b0 = 0; b0 < B; b0 += per) {
-      const int rc = coop_solve(f, theta, u, iters_out, b0, std::min(per, B - b0), B, n, rtol, maxit, workspace, stream);
+      const int rc = coop_solve(f, theta, u, iters_out, b0, std::min(per, B - b0), B, n, npt, rtol, maxit, workspace,
+                                stream);
       if (rc != 0) return rc;
     }
     return 0;

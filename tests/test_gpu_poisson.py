@@ -87,15 +87,18 @@ def _polled_grid_cg(f, th, rtol, maxit):
 
 
 @pytest.mark.parametrize("n,B", [(129, 3), (320, 0), (200, 5)])
-def test_cooperative_grid_cg_equals_polled(n, B):
-    """n > 128: srpde_poisson_cg_batched runs the grid CG as cooperative launches whose grid barriers
-    replace the launch boundaries (stream-ordered, no host poll).  Same partial sums, reduction order
-    and expressions as the launch-per-iteration kernels: u and the iteration counts are bit-identical
-    to the polled split entries, per problem, across launch groups (B = 0 here means one more problem
-    than fit one cooperative launch at this n) and with a problem that converges at once (zero forcing)
-    and one stopped by maxit."""
+def test_cooperative_grid_cg_matches_polled(n, B):
+    """n > 128: srpde_poisson_cg_batched runs the grid CG as cooperative launches with one grid
+    barrier per iteration: Chronopoulos-Gear CG (gamma = <r, r> and delta = <Ar, r> in one reduction:
+    the same Krylov iterates as textbook CG in exact arithmetic), where the polled split
+    entries run textbook CG with two launch boundaries per iteration.  Bar: after the same number of
+    iterations the two u agree to 1e-9 relative (the two recurrences' rounding differs), both
+    converge to the solver's tolerance in iteration counts within 2% + 2, per problem, across launch
+    groups (B = 0 here means one more problem than fit one cooperative launch at this n), with a
+    problem that converges at once (zero forcing) and one stopped by maxit."""
     from superresolution_for_pdes_amd import poisson as P
     from superresolution_for_pdes_amd._lib import query
+    from oracle import poisson_ref as R
     per = int(query("srpde_poisson_coop_problems", n))
     assert per >= 1
     if B == 0:
@@ -107,13 +110,25 @@ def test_cooperative_grid_cg_equals_polled(n, B):
     for maxit in (20 * n * n, 37):
         u, it = P.solve_batched(f, th, maxit=maxit, return_iters=True)
         u2, it2 = _polled_grid_cg(f, th, P.DEFAULT_RTOL, maxit)
-        assert torch.equal(it, it2), (it.tolist(), it2.tolist())
-        assert torch.equal(u, u2)
         assert int(it[B // 2]) == 0 and float(u[B // 2].abs().max()) == 0.0
+        a, a2 = it.tolist(), it2.tolist()
         if maxit == 37:
-            assert int(it.max()) == 37
+            assert a == a2 and max(a) == 37, (a, a2)
+            for b in range(B):
+                if b != B // 2:
+                    d = float((u[b] - u2[b]).norm() / u2[b].norm())
+                    assert d < 1e-9, (b, d)
         else:
-            assert int(it.max()) < 10 * n
+            assert max(a) < 10 * n
+            for b in range(B):
+                assert abs(a[b] - a2[b]) <= 0.02 * a2[b] + 2, (a, a2)
+            fn, tn, un = f.cpu().numpy(), th.cpu().numpy(), u.cpu().numpy()
+            for b in range(B):
+                if b != B // 2:
+                    res = np.linalg.norm(R.apply_operator(un[b], tn[b]) - fn[b]) / np.linalg.norm(fn[b])
+                    assert res < 1e-9, (b, res)
+                    d = float((u[b] - u2[b]).norm() / u2[b].norm())
+                    assert d < 1e-10, (b, d)
 
 
 def test_aborted_grid_barrier_raises():

@@ -1,16 +1,18 @@
-"""Average SQ counters per dispatch of the conv main kernels, grouped by (kernel, grid size)
-(distinguishes layers of one instantiation).  python tools/pmc_by_grid.py DIR"""
+"""Average SQ counters per dispatch of the conv main kernels (or the kernels matching PATTERN),
+grouped by (kernel, grid size) (distinguishes layers of one instantiation).
+    python tools/pmc_by_grid.py DIR [PATTERN]"""
 import collections
 import csv
 import glob
 import re
 import sys
 
+pat = sys.argv[2] if len(sys.argv) > 2 else r"srpde::conv_\w+_kernel"
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if not re.search(r"srpde::conv_\w+_kernel", k) or "fixup" in k:
+        if not re.search(pat, k) or "fixup" in k:
             continue
         key = (re.sub(r"\(.*", "", k).replace("void srpde::", ""), r.get("Grid_Size", "?"))
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
