@@ -1550,23 +1550,21 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
     for (int e = threadIdx.x; e < 4 * span; e += 256) T[e] = src[e];
     __syncthreads();
     const float* t = T + (threadIdx.x >> 6) * span;
-    auto v = [&](int k) {
-      const int tap = k / cin_pad, c = k - tap * cin_pad;
-      return c < cin_real ? t[c * 9 + tap] : 0.f;
-    };
+    // max |w| over the staged source itself (the zero padding adds nothing): no per-element division
     float m = 0.f;
-    for (int k = lane; k < K; k += 64) m = fmaxf(m, fabsf(v(k)));
+    for (int k = lane; k < span; k += 64) m = fmaxf(m, fabsf(t[k]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     const int e = h3_exp(__float_as_uint(m));
     const float sc = exp2i(e);
     _Float16* hi = planes + (size_t)r * K;
     _Float16* lo = planes + (size_t)rows * K + (size_t)r * K;
-    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k of one tap per lane
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {   // 8 consecutive k of one tap per lane (cin_pad % 8 == 0)
+      const int tap = k0 / cin_pad, c0 = k0 - tap * cin_pad;
       half8 hv, lv;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float x = v(k0 + i) * sc;
+        const float x = (c0 + i < cin_real ? t[(c0 + i) * 9 + tap] : 0.f) * sc;
         const _Float16 h = (_Float16)x;
         hv[i] = h;
         lv[i] = (_Float16)(x - (float)h);
@@ -1589,10 +1587,9 @@ __global__ __launch_bounds__(256) void prepare_weights_h3_kernel(const long long
     __syncthreads();
     const int cq = (threadIdx.x >> 6) * 9;   // this wave's row within the staged columns
     float m = 0.f;
-    for (int k = lane; k < K; k += 64) {
-      const int tap = k / cout_pad, n = k - tap * cout_pad;
-      m = fmaxf(m, fabsf(T[n * 37 + cq + tap]));
-    }
+    for (int n = lane; n < cout_pad; n += 64)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) m = fmaxf(m, fabsf(T[n * 37 + cq + tap]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     const int e = h3_exp(__float_as_uint(m));

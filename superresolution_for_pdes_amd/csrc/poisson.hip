@@ -73,13 +73,16 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* slots) 
 }
 
 // The Chronopoulos-Gear scalars of the next iteration from gamma_new = <r, r>, delta_new = <A r, r>:
-// beta = gamma_new / gamma, alpha = gamma_new / (delta_new - beta gamma_new / alpha), the latter
-// multiplied through by c = gamma alpha so that the two divisions are independent (one division
-// latency on the iteration's critical path instead of three)
+// beta = gamma_new / gamma, alpha = gamma_new / (delta_new - beta gamma_new / alpha) = gn c / D with
+// c = gamma alpha, D = delta_new c - gamma_new^2; both from ONE division, 1 / (gamma D) (the three
+// chained divisions were ~35 of an iteration's ~200 VALU instructions per wave, all on its critical
+// path).  Magnitudes: gamma D ~ gamma^3, far inside fp64's range for rtol >= 1e-30.
 __device__ __forceinline__ void cg_scalars(double gn, double dn, double& gamma, double& alpha, double& beta) {
   const double c = gamma * alpha;
-  beta = gn / gamma;
-  alpha = (gn * c) / (dn * c - gn * gn);
+  const double D = dn * c - gn * gn;
+  const double rr = 1.0 / (gamma * D);
+  beta = gn * D * rr;
+  alpha = gn * c * gamma * rr;
   gamma = gn;
 }
 
