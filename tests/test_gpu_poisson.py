@@ -131,6 +131,25 @@ def test_cooperative_grid_cg_matches_polled(n, B):
                     assert d < 1e-10, (b, d)
 
 
+@pytest.mark.parametrize("n", [1024, 1030])
+def test_grid_cg_at_the_cooperative_size_bound(n):
+    """n = 1024 is the largest grid the cooperative CG takes (two halo points per thread: 2n <= 2048);
+    n = 1030 runs the polled launch-per-iteration kernels.  Both converge: residual of the 5-point
+    operator against the oracle's matrix-free form <= 1e-8 of |f| (the condition number is ~2e6 here:
+    fp64 CG's attainable residual, eps * kappa, is ~4e-10)."""
+    from superresolution_for_pdes_amd import poisson as P
+    from superresolution_for_pdes_amd._lib import query
+    from oracle import poisson_ref as R
+    assert (int(query("srpde_poisson_coop_problems", n)) > 0) == (n <= 1024)
+    f = P.forcing_batched(np.array([[3.25, 5.5]]), n)
+    th = torch.from_numpy(np.random.default_rng(n).uniform(0.5, 2.0, (1, n, n))).cuda()
+    u, it = P.solve_batched(f, th, return_iters=True)
+    fn, tn, un = f.cpu().numpy()[0], th.cpu().numpy()[0], u.cpu().numpy()[0]
+    res = np.linalg.norm(R.apply_operator(un, tn) - fn) / np.linalg.norm(fn)
+    assert res < 1e-8, res
+    assert 0 < int(it[0]) < 10 * n
+
+
 def test_aborted_grid_barrier_raises():
     """a cooperative grid-CG launch that gives up at a grid barrier marks its problems
     iters = -1 and leaves u unconverged; solve_batched must raise instead of returning that u (the
