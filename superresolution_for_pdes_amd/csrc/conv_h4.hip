@@ -59,6 +59,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 #ifndef H4_PRIO
 #define H4_PRIO 0
 #endif
+// A/B switch: the tap barrier after every second tap (taps 1, 3, 5, 7, 8 of a chunk) where the weight
+// ring has >= 6 slots; the prefetch distance drops by one tap (PD = slots - 2) so that the two taps
+// between barriers never DMA into a slot a slower wave still reads.  Measured: no change (30 conv
+// passes 15.463 -> 15.447 ms, forward within noise; run-to-run race check clean;
+// profiles/r04s_h4_bar2_ab.txt) -- the per-tap overhead is not the barrier
+#ifndef H4_BAR2
+#define H4_BAR2 0
+#endif
 
 template <int W, int DIL, int BN_>
 struct H4Geom {
@@ -116,13 +124,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
   constexpr int OFF_F = G::template off_f<PRE>(), OFF_B = G::template off_b<PRE>();
   constexpr int OFF_SINK = G::template off_sink<PRE>();   // target of the zero-fill DMAs that keep vmcnt counts exact
   constexpr int APW = G::template apw<PRE>();   // A-tile DMAs per wave and chunk
-  constexpr int NBR = G::template nbr<PRE>(), PD = NBR - 1;   // weight ring slots, prefetch distance (taps)
+  constexpr int NBR = G::template nbr<PRE>();   // weight ring slots
+  constexpr bool BAR2 = H4_BAR2 && NBR >= 6;    // a tap barrier after every second tap (H4_BAR2 above)
+  constexpr int PD = BAR2 ? NBR - 2 : NBR - 1;  // prefetch distance (taps)
   static_assert(NBR >= 4 && G::template lds<PRE>() <= 160 * 1024, "LDS");
   // a tap-end wait leaves the DMAs of the last WIN taps in flight (see the barrier in tap()); the next
   // chunk's A pieces, APT per tap in taps 0 .. TA-1, must have landed by PRE's tap 8 (it reads them) /
   // by the convert after tap 8
-  constexpr int WIN = PD - 2;
-  constexpr int TA = (PRE ? 10 : 11) - PD;
+  // (BAR2: a wait must also cover the window's second tap, so one tap fewer stays in flight)
+  constexpr int WIN = BAR2 ? PD - 3 : PD - 2;
+  constexpr int TA = (PRE ? 8 : 9) - WIN;
   constexpr int APT = (APW + TA - 1) / TA;
   static_assert(APT <= 2 && TA >= 1, "A DMAs land before the next chunk's tile is read");
   static_assert(SSTRIDE + 64 < 65536 && ZREL < 65536, "16-bit fragment offsets");
@@ -479,10 +490,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     // a bare s_barrier: no lgkmcnt(0) drain of the next tap's fragment reads still in flight (they read
     // slot tau + 1 and the S tile, which no DMA issued after this barrier writes); the asm is a
     // compiler memory barrier, so no LDS read moves above it
-    if constexpr (SRPDE_CONV_DBG & 2)   // diagnostics: 2 = no tap barrier
+    if constexpr (BAR2 && T % 2 == 0 && T != 8) {
+      // no barrier: the last one (tap T - 1, or tap 8 of the previous chunk) covered this window's reads
+    } else if constexpr (SRPDE_CONV_DBG & 2) {   // diagnostics: 2 = no tap barrier
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCUR) : "memory");
-    else
+    } else {
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NCUR) : "memory");
+    }
   };
 
   // persistent: workgroup b takes items b, b + grid, ...; the first tile's first chunk and the weights of
