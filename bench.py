@@ -308,6 +308,11 @@ def run_poisson(args, world, rank, dev, pmc=None):
             # trips), reported per iteration of the slowest problem in the batch
             lv["max_iters"] = int(it.max())
             lv["us_per_iter"] = round(1e6 * t / max(1, int(it.max())), 2)
+            # SURVEY 8(d)'s convention for a streamed CG (88 B / point / iteration: SpMV, updates and
+            # direction through HBM): the rate this solve equals under it (above 1 of the HBM peak because
+            # the state never leaves the chip)
+            lv["hbm_equiv_gbs_88B"] = round(88 * pts_it / t / 1e9, 1)
+            lv["hbm_equiv_frac_88B"] = round(88 * pts_it / t / 8.0e12, 4)
         levels[n] = lv
     if rank != 0:
         return
