@@ -399,14 +399,15 @@ size_t srpde_poisson_workspace_size(int B, int n);
  * for B problems at once): f, theta, u are [B][n][n] fp64 device arrays, iters_out [B] int32
  * (nullable; -1 marks a problem whose cooperative launch aborted at a stuck grid barrier).
  * n <= srpde_poisson_lds_max_n(): one stream-ordered launch, no workspace.  Larger n: grid CG with
- * workspace (srpde_poisson_workspace_size bytes), run as cooperative launches of
- * srpde_poisson_coop_problems(n) problems each -- stream-ordered, the host never waits.  Only when
- * that count is 0 (one problem larger than the co-resident grid) the call drives the split entry
- * points below and polls convergence every 128 iterations, synchronising `stream`. */
+ * workspace (srpde_poisson_workspace_size bytes), run as cooperative launches (Chronopoulos-Gear CG,
+ * one grid barrier per iteration, block size chosen per (B, n)) -- stream-ordered, the host never
+ * waits.  Only when srpde_poisson_coop_problems(n) is 0 (n > 1024) the call drives the split entry
+ * points below (textbook CG) and polls convergence every 128 iterations, synchronising `stream`. */
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream);
-/* Problems per cooperative grid-CG launch at this n; 0 when one problem does not fit the
- * co-resident grid or n > 2048 (the stencil's neighbour rows must lie in the adjacent block). */
+/* Problems per cooperative grid-CG launch at this n with its largest (8192-point) blocks; 0 when one
+ * problem does not fit the co-resident grid or n > 1024 (a block's two halo rows, the neighbours'
+ * edge rows, take at most two points per thread). */
 int srpde_poisson_coop_problems(int n);
 /* Test hook: 1 = every following cooperative grid-CG launch starts aborted (iters_out = -1 for its
  * problems, u undefined), 0 = normal.  Returns the previous setting.  Exercises callers' handling of
