@@ -11,4 +11,4 @@ for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmcp_$T -o p$i -- python $R/bench.py --workload poisson --poisson-sizes 80:1024 --steps 2 --no-cpu-baseline --no-live-traffic > $R/gpurun_out/pmcp_${T}_$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $R/gpurun_out/pmcp_${T}_$i.log; exit 1; }
 done
 cd $R
-python tools/pmc_by_grid.py gpurun_out/pmcp_$T "cg_lds_kernel" | tee gpurun_out/pmcp_$T.txt
+python tools/pmc_by_grid.py gpurun_out/pmcp_$T "cg_lds" | tee gpurun_out/pmcp_$T.txt
