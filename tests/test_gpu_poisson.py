@@ -86,7 +86,7 @@ def _polled_grid_cg(f, th, rtol, maxit):
     return u, it
 
 
-@pytest.mark.parametrize("n,B", [(129, 3), (320, 0), (200, 5)])
+@pytest.mark.parametrize("n,B", [(129, 3), (320, 0), (200, 5), (345, 2)])
 def test_cooperative_grid_cg_matches_polled(n, B):
     """n > 128: srpde_poisson_cg_batched runs the grid CG as cooperative launches with one grid
     barrier per iteration: Chronopoulos-Gear CG (gamma = <r, r> and delta = <Ar, r> in one reduction:
@@ -95,7 +95,8 @@ def test_cooperative_grid_cg_matches_polled(n, B):
     iterations the two u agree to 1e-9 relative (the two recurrences' rounding differs), both
     converge to the solver's tolerance in iteration counts within 2% + 2, per problem, across launch
     groups (B = 0 here means one more problem than fit one cooperative launch at this n), with a
-    problem that converges at once (zero forcing) and one stopped by maxit."""
+    problem that converges at once (zero forcing) and one stopped by maxit.  n = 345, B = 2 runs
+    2048-point blocks whose last one (345^2 mod 2048 = 241 points) is shorter than a grid row."""
     from superresolution_for_pdes_amd import poisson as P
     from superresolution_for_pdes_amd._lib import query
     from oracle import poisson_ref as R
