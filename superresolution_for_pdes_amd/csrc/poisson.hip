@@ -482,6 +482,10 @@ __device__ __forceinline__ void write_part_ag(double v, double* sh, double* dst)
 // coherent memory side and never by a CU's L1 or an XCD's L2 (MI355X_MICROARCH.md, "Valid forms":
 // sc1 stores drained by vmcnt + sc1 loads behind a counter poll); it is not a guarantee of the HIP
 // memory model, and a port to another target must restore the release / acquire fences.
+// the poll interval of a waiting block (s_sleep units of 64 cycles); A/B builds override it
+#ifndef SRPDE_COOP_SLEEP
+#define SRPDE_COOP_SLEEP 2
+#endif
 __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long epoch, int* sflag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores have landed
   __syncthreads();
@@ -502,7 +506,7 @@ __device__ __forceinline__ bool coop_sync(const GridCoop& g, unsigned long long 
         ab = 1;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(SRPDE_COOP_SLEEP);
     }
     *sflag = ab;
   }
