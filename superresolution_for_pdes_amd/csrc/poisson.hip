@@ -428,7 +428,10 @@ __global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restr
 // bar[1 + g] counts the arrivals of block group g (COOP_GRP consecutive blocks), the last arriver of
 // a group bumps bar[0], and every block waits for bar[0] to reach epoch x groups -- COOP_GRP + groups
 // serialised atomics per barrier instead of one per block on a single address.
-constexpr int COOP_GRP = 16;
+#ifndef SRPDE_COOP_GRP
+#define SRPDE_COOP_GRP 16
+#endif
+constexpr int COOP_GRP = SRPDE_COOP_GRP;   // A/B builds override it
 struct GridCoop {
   double *er[2], *ew[2], *es[2];   // [B][N2] by parity: r, w = A r, s = A p at a block's edge points
   double *gp[2], *dp[2];           // [B][nb] by parity: per-block partials of gamma = <r, r>, delta = <w, r>
