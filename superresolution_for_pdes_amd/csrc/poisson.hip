@@ -429,7 +429,7 @@ __global__ void gcg_finish_kernel(GridCG g, double* __restrict__ u, int* __restr
 // a group bumps bar[0], and every block waits for bar[0] to reach epoch x groups -- COOP_GRP + groups
 // serialised atomics per barrier instead of one per block on a single address.
 #ifndef SRPDE_COOP_GRP
-#define SRPDE_COOP_GRP 16
+#define SRPDE_COOP_GRP 4
 #endif
 constexpr int COOP_GRP = SRPDE_COOP_GRP;   // A/B builds override it
 struct GridCoop {
