@@ -43,8 +43,10 @@ typedef struct ihipStream_t* hipStream_t;
  *   5  srpde_conv_fwd_h3: x1_ca, x1_sa before the workspace
  *   6  srpde_conv_fwd: ep_mean, ep_invstd, ep_gamma, ep_beta, ep_amax before the workspace
  *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa;
- *      srpde_conv_head_eval */
-#define SRPDE_ABI_VERSION 7
+ *      srpde_conv_head_eval
+ *   8  srpde_conv_h3_stats_rows_for, srpde_conv_h5_set (the h5 forward writes 80-row statistics),
+ *      srpde_conv_head_eval_supported */
+#define SRPDE_ABI_VERSION 8
 
 const char* srpde_last_error(void);
 int srpde_version(void);
@@ -87,6 +89,16 @@ int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize)
 /* Rows per BatchNorm-statistics block written by srpde_conv_fwd_h3 (stats / bn_part buffers
  * hold ceil(P / rows) blocks); the other conv families use srpde_conv_stats_rows_per_block. */
 int srpde_conv_h3_stats_rows(void);
+/* Rows per BatchNorm-statistics block srpde_conv_fwd_h3 writes for the FORWARD of this shape (input
+ * channels c0 + c1 -> cout at h x w, dilation dil): 80 where the h5 kernel takes it (w = 40, h % 8 == 0,
+ * cout 64 or 32, c0 + c1 a multiple of 64), else srpde_conv_h3_stats_rows().  Dgrad partials (bn_part)
+ * keep srpde_conv_h3_stats_rows(). */
+int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil);
+/* Kernel choice of srpde_conv_fwd_h3 for the shapes above: 1 = the h5 kernel (conv_h5.hip: tiles of 8
+ * image rows, weights in registers; default), 0 = h4 / h3.  The conv outputs are equal bit for bit; the
+ * statistics come in 80-row instead of 128-row blocks (allocate them with the current choice).  Returns
+ * the previous value (on < 0: query only).  Tuning and tests. */
+int srpde_conv_h5_set(int on);
 /* Kernel choice of srpde_conv_fwd_h3 for output tiles of <= 64 channels: 1 = the register-staged
  * 4-wave kernel, two workgroups per CU (default; SRPDE_H3R=0 turns it off), 0 = the 8-wave
  * kernel.  Both compute the same outputs, statistics and stored splits bit for bit (outside a
@@ -328,6 +340,9 @@ int srpde_upsample_gate_sa(const float* x, int ldx, int n, int h, int w, int ho,
  * bias [1], xin the U-Net input (NCHW, xin_c channels).  out_conv2's values equal the h3 kernels';
  * the 16-channel dot sums in another order than srpde_head_fwd.  Replaces srpde_conv_fwd_h3 (out_conv2,
  * ep_*) + srpde_head_fwd.  Needs w <= 63. */
+/* 1 if srpde_conv_head_eval takes images of width w (its halo tile needs w <= 63), else 0: wider images
+ * run out_conv2 on srpde_conv_fwd_h3 and the head separately. */
+int srpde_conv_head_eval_supported(int w);
 int srpde_conv_head_eval(const float* z, int ldz, const unsigned* amax_z, const void* wsplit, const int* wexp,
                          const float* bias, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                          const float* bn_beta, const float* wf, const float* bf, const float* xin, int xin_c, int n,

@@ -120,4 +120,10 @@ bool h4_up_supported(int w, int dil, int cout);   // the upsampled-input forward
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes);
 bool h4_on();
 
+// h5 (conv_h5.hip): the W = 40 forward into 64 / 32 channels (8-row tiles, weights in registers)
+bool h5_supported(int c0, int c1, int cout, int h, int w, int dil);
+int h5_set(int on);
+int h5_stats_rows();
+int launch_fwd_h5(const ConvParams& p, const H3Args& h, hipStream_t st);
+
 }  // namespace srpde

@@ -1909,6 +1909,12 @@ extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
 
+int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil) {
+  return h5_supported(c0, c1, cout, h, w, dil) ? h5_stats_rows() : H3_SRB;
+}
+
+int srpde_conv_h5_set(int on) { return h5_set(on); }
+
 int srpde_conv_h4_set(int on) {
   const int prev = h4_on() ? 1 : 0;
   if (on >= 0) g_h4.store(on ? 1 : 0);   // on < 0: query only
@@ -2024,6 +2030,16 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "bn_part, cout %% 4 == 0");
   p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
+  // h5 takes the forward of the shapes srpde_conv_h3_stats_rows_for reports 80-row statistics for
+  if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr &&
+      h5_supported(c0, c1, cout, h, w, dil)) {
+    if (ldy % 4 == 0 && aligned16(y) && (c1 == 0 || ldx1 % 4 == 0)) return launch_fwd_h5(p, a, stream);
+    SRPDE_CHECK_ARG(stats == nullptr, "srpde_conv_fwd_h3: the h5 shape (w=40, cout=%d) needs a 16-byte aligned y "
+                    "with ldy %% 4 == 0 when it writes statistics", cout);
+  }
+  SRPDE_CHECK_ARG(x0_up == nullptr || stats == nullptr || !h5_supported(c0, c1, cout, h, w, dil),
+                  "srpde_conv_fwd_h3: an upsampled x0 with statistics at an h5 shape (w=40, cout=%d): the statistics "
+                  "blocks would not be the srpde_conv_h3_stats_rows_for ones", cout);
   if (x0_up != nullptr || (h4_on() && h4_supported(w, dil, cout, false)))
     return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
   if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {

@@ -143,6 +143,10 @@ using namespace srpde;
 
 extern "C" {
 
+int srpde_conv_head_eval_supported(int w) {
+  return (w > 0 && w <= 63 && (size_t)(HEAD_BM + 2 * (w + 1)) * HEAD_SR + 128 <= 80 * 1024) ? 1 : 0;
+}
+
 int srpde_conv_head_eval(const float* z, int ldz, const unsigned* amax_z, const void* wsplit, const int* wexp,
                          const float* bias, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                          const float* bn_beta, const float* wf, const float* bf, const float* xin, int xin_c, int n,
@@ -160,7 +164,8 @@ int srpde_conv_head_eval(const float* z, int ldz, const unsigned* amax_z, const 
   a.wf = wf; a.bf = bf; a.xin = xin; a.xin_c = xin_c;
   a.N = n; a.H = h; a.W = w; a.P = n * h * w; a.out = out;
   const size_t lds = (size_t)(HEAD_BM + 2 * (w + 1)) * HEAD_SR + 128;
-  SRPDE_CHECK_ARG(w <= 63 && lds <= 80 * 1024, "srpde_conv_head_eval: image rows too wide for the tile (w=%d > 63)", w);
+  SRPDE_CHECK_ARG(srpde_conv_head_eval_supported(w), "srpde_conv_head_eval: image rows too wide for the tile (w=%d > 63)",
+                  w);
   hipLaunchKernelGGL(conv_head_eval_kernel, dim3(ceil_div(a.P, HEAD_BM)), dim3(256), lds, stream, a);
   SRPDE_LAUNCH_CHECK("srpde_conv_head_eval");
   return 0;

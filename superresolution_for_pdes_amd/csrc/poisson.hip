@@ -16,6 +16,9 @@
 //               block re-reduces the previous launch's partials in the same order, so all
 //               blocks agree on alpha/beta without a grid barrier or host round trip.
 //               A sticky per-problem `done` flag makes extra launches no-ops.
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <atomic>
 #include "common.h"
 
@@ -689,8 +692,7 @@ __global__ __launch_bounds__(GCC_T) void gcg_coop_kernel(const double* __restric
       alpha = gn / dn;
       beta = 0.0;
     } else if (!done) {
-      beta = gn / gamma;
-      alpha = gn / (dn - beta * gn / alpha);
+      cg_scalars(gn, dn, gamma, alpha, beta);   // the LDS kernels' one-division form (same rounding)
     }
     if (!done) gamma = gn;
     if (!done && (gamma <= stop || k >= maxit)) {
@@ -877,16 +879,28 @@ static const void* coop_kernel(int npt) {
   }
 }
 
-// co-resident blocks of gcg_coop_kernel<npt> at this n on this device (0: no cooperative launch)
+// co-resident blocks of gcg_coop_kernel<npt> at this n on this device (0: no cooperative launch), cached per
+// (device, npt, LDS bytes): a solve asks up to six times
 static int coop_capacity(int npt, int n) {
-  int dev = 0, cus = 0, per = 0, coop = 0;
+  int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const size_t lds = gcc_lds_bytes(npt, n);
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, size_t>, int> cache;
+  const auto key = std::make_tuple(dev, npt, lds);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int cus = 0, per = 0, coop = 0;
   (void)hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coop_kernel(npt), GCC_T, gcc_lds_bytes(npt, n)) !=
-      hipSuccess)
-    return 0;
-  return coop ? per * cus : 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, coop_kernel(npt), GCC_T, lds) != hipSuccess) return 0;
+  const int cap = coop ? per * cus : 0;
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = cap;
+  return cap;
 }
 
 static int coop_blocks(int npt, int n) { return (int)ceil_div((long long)n * n, (long long)GCC_T * npt); }

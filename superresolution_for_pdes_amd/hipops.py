@@ -99,7 +99,8 @@ def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
     """BN-statistics partials for the forward conv of input channels (c0, c1) -> cout: the
     kernel family that will run decides the row-block size.  -> (buffer, blocks, rows/block)."""
     h3 = h3_capable(c0, c1, cout, w, dil)
-    rows = int(query("srpde_conv_h3_stats_rows")) if h3 else int(query("srpde_conv_stats_rows_per_block", cout))
+    rows = (int(query("srpde_conv_h3_stats_rows_for", c0, c1, cout, h, w, dil)) if h3
+            else int(query("srpde_conv_stats_rows_per_block", cout)))
     nblk = -(-(n * h * w) // rows)
     buf = empty(nblk, cout, 2, device=device)
     buf._srpde_rows = rows
@@ -116,6 +117,12 @@ def set_h4(on: bool) -> bool:
     """Kernel choice for 128-column h3 tiles at W = 10 / 20: the h4 kernel (conv_h4.hip) or the h3
     8-wave one (bit-identical).  Returns the previous choice."""
     return bool(query("srpde_conv_h4_set", int(bool(on))))
+
+
+def set_h5(on: bool) -> bool:
+    """Kernel choice for the W = 40 forward into 64 / 32 channels: the h5 kernel (conv_h5.hip) or h4 / h3
+    (equal conv outputs; 80- vs 128-row statistics blocks).  Returns the previous choice."""
+    return bool(query("srpde_conv_h5_set", int(bool(on))))
 
 
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
@@ -180,9 +187,14 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     output (x1 * ca) * sa, formed in the operand transform (the gated tensor is never written).
     ``x0`` may be an UpsampledInput (h4 shapes, forward): its operand is interpolated from x0.x's rows."""
     up = x0 if isinstance(x0, UpsampledInput) else None
+    c1_ = x1.shape[1] if x1 is not None else 0
     if up is not None and not (_CONV_MATH == "h3" and sign == 1 and in_affine is None
-                               and conv_fwd_up_capable(x0.shape[1], x1.shape[1] if x1 is not None else 0, cout, w,
-                                                       dil)):
+                               and conv_fwd_up_capable(x0.shape[1], c1_, cout, w, dil)
+                               # statistics: the upsampled-input kernel writes h3 row blocks, so a shape whose
+                               # statistics blocks are h5's reads the formed tensor
+                               and (stats is None or int(query("srpde_conv_h3_stats_rows_for", x0.shape[1], c1_,
+                                                                 cout, h, w, dil))
+                                    == int(query("srpde_conv_h3_stats_rows")))):
         x0 = up.materialize()
         up = None
     p0, ld0 = _pl(x0.x if up is not None else x0)
@@ -195,8 +207,11 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
     if _CONV_MATH == "h3" and query("srpde_conv_h3_supported", x0.shape[1], c1, cout, w, dil, ksize):
         planes, wexp = getattr(wpack, "h3", None) or split_weights_h3(wpack, cout)
-        for buf in (stats, bn_bwd[5] if bn_bwd is not None else None):
-            if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
+        rows_fwd = (int(query("srpde_conv_h3_stats_rows_for", x0.shape[1], c1, cout, h, w, dil)) if sign == 1
+                    else int(query("srpde_conv_h3_stats_rows")))
+        for buf, rows in ((stats, rows_fwd), (bn_bwd[5] if bn_bwd is not None else None,
+                                              int(query("srpde_conv_h3_stats_rows")))):
+            if buf is not None and getattr(buf, "_srpde_rows", None) != rows:
                 raise ValueError("statistics buffer not laid out for the h3 kernel (use conv_stats_buffer "
                                  "with the input channels / bn_bwd_partials)")
         a0 = amax_of(x0)

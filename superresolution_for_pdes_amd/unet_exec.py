@@ -279,6 +279,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
                      x1_gate=x1_gate)
         mom = bn.momentum if bn.momentum is not None else 0.0
         _buffers_ready(dev)
+        _RS_EPOCH[0] += 1   # the finalize below rewrites the running statistics torch's version counters miss
         if not activate:   # the fused consumer's (scale, shift), from the same launch (SRPDE_FIN_AFFINE=0: two)
             slot = slots.take()
             if _FIN_AFFINE:
@@ -356,10 +357,12 @@ def _eval_stats(bn):
     """(mean, 1 / sqrt(var + eps)) of a BatchNorm's running statistics for the eval forward, cached
     until they change (srpde_bn_eval_prepare: one tiny launch per BN layer per forward otherwise)."""
     rm, rv = bn.running_mean, bn.running_var
+    if not _EVAL_STATS_CACHE or rm.is_inference() or rv.is_inference():
+        # (inference tensors -- buffers of a model built or loaded under torch.inference_mode() -- have no
+        # version counter to key a cache on)
+        return H.bn_eval_prepare(rm, rv, bn.eps)
     key = (rm.data_ptr(), rm._version, rv.data_ptr(), rv._version, float(bn.eps), _RS_EPOCH[0])
     c = getattr(bn, "_srpde_eval_stats", None)
-    if not _EVAL_STATS_CACHE:
-        return H.bn_eval_prepare(rm, rv, bn.eps)
     if c is None or c[0] != key:
         c = (key, H.bn_eval_prepare(rm, rv, bn.eps))
         bn._srpde_eval_stats = c
@@ -769,7 +772,8 @@ def unet_forward(m, x, training, save=False):
     else:
         o1, S.out1 = _cbr_fwd(m.out_conv1, m.out_bn1, d1, None, n, h, w, training, 1, slots, in_affine=d1aff)
         if (getattr(slots, "eval_epilogue", False) and _FUSE_HEAD and o1.shape[1] == 32
-                and m.out_conv2.out_channels == 16 and H.h3_capable(32, 0, 16, w, 1)):
+                and m.out_conv2.out_channels == 16 and H.h3_capable(32, 0, 16, w, 1)
+                and H.query("srpde_conv_head_eval_supported", w)):
             # inference: out_conv2 -> out_bn2 -> ReLU -> final -> + residual in one pass (o2 never written)
             bn = m.out_bn2
             mean, invstd = _eval_stats(bn)

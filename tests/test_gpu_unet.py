@@ -468,3 +468,41 @@ def test_eval_fused_head_matches_separate_passes():
         unet_exec._FUSE_HEAD = saved
     err = float((outs[0] - outs[1]).norm() / outs[1].norm())
     assert err <= 1e-6, err
+
+
+@pytest.mark.parametrize("hw", [64, 80])
+def test_eval_forward_wide_images_match_oracle(hw):
+    """Inference on images wider than the fused head's tile (srpde_conv_head_eval takes w <= 63,
+    srpde_conv_head_eval_supported): out_conv2 then runs on the conv kernels + srpde_head_fwd, and the
+    forward still equals the fp64 oracle (64..191-pixel rows used to raise)."""
+    from oracle.unet_ref import unet_forward as ref_fwd, clone_state
+    st = fixture_state_torch(torch.float64)
+    x = torch.randn(2, 3, hw, hw, generator=torch.Generator().manual_seed(hw))
+    m = make_model(False)
+    with torch.no_grad():
+        out = m(x.to(DEV)).cpu().double()
+        ref = ref_fwd(clone_state(st), x.double(), False)
+    assert rmse(out, ref) < 2e-5
+
+
+def test_convblock_eval_after_train_step_uses_new_running_stats():
+    """A standalone ConvBlock: eval forward (caches the BN running statistics), one train-mode forward (its
+    finalize kernels rewrite them, invisible to torch's version counters), eval again -- the second eval
+    must use the new statistics (the eval cache used to serve the old ones).  Reference: torch's
+    own eval-mode block on the running statistics the HIP train step left."""
+    from superresolution_for_pdes_amd.models import ConvBlock
+    torch.manual_seed(1)
+    blk = ConvBlock(64, 64).to(DEV)
+    x = torch.randn(4, 64, 20, 20, device=DEV)
+    with torch.no_grad():
+        blk.eval()
+        blk(x)
+        blk.train()
+        blk(x + 1.0)
+        blk.eval()
+        y = blk(x)
+    ref = torch.nn.Sequential(blk.conv1, blk.bn1, torch.nn.ReLU(), blk.conv2, blk.bn2, torch.nn.ReLU())
+    ref64 = __import__("copy").deepcopy(ref).double().eval().cpu()
+    with torch.no_grad():
+        yr = ref64(x.double().cpu())
+    assert rmse(y.cpu().double(), yr) <= 1e-5 * float(yr.std())
