@@ -33,6 +33,18 @@ namespace srpde {
 
 __device__ floatx4 h5_bload(int32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
+// 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds) with a uniform byte offset in soffset and the wave-uniform LDS
+// destination in M0 (conv_h4.hip dma16s): inline asm, invisible to the compiler's waitcnt pass -- the issuing
+// (loader) waves count these loads themselves
+__device__ __forceinline__ void h5_dma16(int32x4 rsrc, unsigned voff, unsigned soff, unsigned lds_addr) {
+  asm volatile(
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %1, %2 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(soff)), "{m0}"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
+
 namespace {
 constexpr int kW = 40;                       // image width (compile-time: the pad geometry)
 constexpr int kTR = 8;                       // image rows per tile
@@ -43,19 +55,20 @@ constexpr int kSR = 160;                     // bytes per halo-image row: hi 64 
 constexpr int kSBUF = kSROWS * kSR;          // 67200 B per buffer
 constexpr int kNPB = 5;                      // 16-pixel blocks per wave
 constexpr int kSRB = 80;                     // rows per BN-statistics partial (one wave's pixels)
-constexpr int kLDS = 2 * kSBUF + 64;         // two buffers + the max|y| reduction scratch
+constexpr int kOffW = 2 * kSBUF;             // the weight ring: 3 slots of one tap [2 planes][64 rows][64 B]
+constexpr int kWSLOT = 8192;
+constexpr int kOffP = kOffW + 3 * kWSLOT;     // per output channel: wexp, bias, eval BN mean / invstd / gamma / beta
+constexpr int kOffA = kOffP + 6 * 64 * 4;     // the fused input BN's scale / shift per input channel (<= 192)
+constexpr int kOffR = kOffA + 2 * 192 * 4;    // the max|y| reduction
+constexpr int kLDS = kOffR + 64;
 constexpr int kHaloPix = (kTR + 2) * kW;     // 400 halo pixels converted per chunk (4 units of 8 channels each)
 }  // namespace
 
-// weight register slots: the B fragments of tap tau + H5_WSLOTS - 1 are loaded at tap tau (18 taps per
-// chunk pair must be a multiple of it)
-#ifndef H5_WSLOTS
-#define H5_WSLOTS 2
-#endif
-static_assert(18 % H5_WSLOTS == 0, "weight slots");
 // timing-only diagnostics (results wrong when non-zero; an A/B library is built with
 // SRPDE_EXTRA_FLAGS=-DH5_DBG=<bits>): 1 = no convert in the taps, 2 = no MFMAs, 4 = no epilogue stores,
-// 8 = no weight loads in the taps
+// 8 = no weight loads in the taps, 16 = phase timestamps (every wave stores s_memtime before and after every tap
+// barrier and around the epilogue of its SECOND tile into room past the output: y + P * ldy + 512 * blockIdx.x +
+// 64 * wave 64-bit words; tools/h5_phase_ts.py)
 #ifndef H5_DBG
 #define H5_DBG 0
 #endif
@@ -85,12 +98,13 @@ constexpr int H5_AFF = 1;     // fused input BN + ReLU (H3Args::in_scale / in_sh
 constexpr int H5_GATE = 2;    // attention-gated second input (H3Args::x1_ca / x1_sa)
 constexpr int H5_TRAIN = 4;   // BN statistics partials + the stored input split (ConvParams::stats, H3Args::xsplit)
 constexpr int H5_EPBN = 8;    // eval-mode BN + ReLU epilogue + max|y| (ConvParams::ep_*)
+constexpr int H5_ACC = 16;    // y += conv (ConvParams::accumulate)
 
 // NCB: 16-channel output blocks per wave (2: Cout 64, 1: Cout 32); MODE: H5_* bits
 template <int NCB, int MODE>
 __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Args h) {
   constexpr bool AFF = (MODE & H5_AFF) != 0, GATE = (MODE & H5_GATE) != 0;
-  constexpr bool TRAIN = (MODE & H5_TRAIN) != 0, EPBN = (MODE & H5_EPBN) != 0;
+  constexpr bool TRAIN = (MODE & H5_TRAIN) != 0, EPBN = (MODE & H5_EPBN) != 0, ACC = (MODE & H5_ACC) != 0;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -117,6 +131,30 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
+  // the epilogue's per-channel parameters and the fused input BN's scale / shift, staged in LDS once (the
+  // epilogue then issues no global loads, whose waits would also wait for the weight DMAs)
+  {
+    float* prm = reinterpret_cast<float*>(lds + kOffP);
+    if (tid < p.Cout) {
+      const int c = tid;
+      prm[c] = __int_as_float(h.wexp[c]);
+      prm[64 + c] = p.bias != nullptr ? p.bias[c] : 0.f;
+      if constexpr (EPBN) {
+        prm[128 + c] = p.ep_mean[c];
+        prm[192 + c] = p.ep_invstd[c];
+        prm[256 + c] = p.ep_gamma[c];
+        prm[320 + c] = p.ep_beta[c];
+      }
+    }
+    if constexpr (AFF) {
+      float* aff = reinterpret_cast<float*>(lds + kOffA);
+      if (tid < p.Cin) {
+        aff[tid] = h.in_scale[tid];
+        aff[192 + tid] = h.in_shift[tid];
+      }
+    }
+  }
+
   // the lane's B fragment (pixel 16 j + l16 of the wave's 80, 8 channels at 16 lq) of tap (ky, kx) is
   // at halo-image row (r + ky) * 42 + x + kx, r / x the pixel's tile row / column
   unsigned ab0[kNPB], ab1[kNPB];
@@ -128,135 +166,185 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     ab1[j] = ab0[j] + kSBUF;
   }
 
-  // weights: [2][Cout][K] planes, K = tap * Cin + channel; the lane's A fragment of output block cb is
-  // row 16 cb + l16, 8 channels at 8 lq of the tap's 32-channel chunk
+  // Roles: waves 4 .. 7 DMA the weights into the LDS ring, waves 0 .. 3 load and convert the halo tiles.  The
+  // MFMA work is the same for every wave; a SIMD runs one wave of each role (waves w and w + 4).
+  const bool loader = wave >= 4;
+
+  // weights: [2][Cout][K] planes, K = tap * Cin + channel.  A tap's tile ([2][Cout][32] fp16, 8 KiB at
+  // Cout 64) goes through a 3-slot LDS ring: at tap tau every wave reads its A fragments of tap tau + 1 into
+  // registers, and the loader waves DMA tap tau + 3 into the slot tap tau used (its fragments were read
+  // during tau - 1); before the barrier of tap tau + 1 a loader waits for its DMA of tap tau + 2 (issued at
+  // tau - 1).  One barrier per tap.  Ring rows are the 64-B k-rows of conv_h4.hip with the same 16-B chunk
+  // swizzle (swzh), conflict-free reads.  Piece pc (1 KiB, one DMA): plane pc / (2 NCB), 16-row block
+  // pc % (2 NCB); lane -> row (lane >> 2), slot lane & 3 holding source chunk swzh(row, lane & 3).  Loader
+  // wave 4 + k DMAs pieces NCB k .. NCB k + NCB - 1.
   const unsigned plane = (unsigned)p.Cout * (unsigned)p.K;
   const int32x4 rsw = make_rsrc(h.wsp, 2u * plane * 2u);
-  unsigned wvo[NCB];
+  unsigned wsrc[NCB], wdst[NCB];   // per piece of this loader wave: source bytes (tap 0, chunk 0), ring offset
 #pragma unroll
-  for (int c = 0; c < NCB; ++c) wvo[c] = ((16u * (unsigned)(cp * NCB + c) + (unsigned)l16) * (unsigned)p.K + 8u * lq) * 2u;
-  half8 wh[H5_WSLOTS][NCB], wl[H5_WSLOTS][NCB];   // taps tau .. tau + PD (slot tau % H5_WSLOTS)
-  auto wload = [&](auto slot_tag, int ch, int tt) {
-    constexpr int S = decltype(slot_tag)::value;
-    const int so = (tt * p.Cin + ch * 32) * 2;
+  for (int k = 0; k < NCB; ++k) {
+    const int pc = (wave & 3) * NCB + k, pl = pc / (2 * NCB), rb = pc % (2 * NCB);
+    const int r = rb * 16 + (lane >> 2);
+    wsrc[k] = ((unsigned)pl * plane + (unsigned)r * (unsigned)p.K + (unsigned)swzh(r, lane & 3) * 8u) * 2u;
+    wdst[k] = (unsigned)(kOffW + pl * (NCB * 2048) + rb * 1024);   // + slot * kWSLOT (+ lane * 16 by the DMA)
+  }
+  const unsigned lds0 = lds_addr_of(lds);
+  const unsigned wfr = (unsigned)(kOffW + l16 * 64 + swzh(l16, lq) * 16);        // A fragment, + cb * 1024
+  auto wdma = [&](int ch, int tt, int slot) {
+#pragma unroll
+    for (int k = 0; k < NCB; ++k) h5_dma16(rsw, wsrc[k], (unsigned)((tt * p.Cin + ch * 32) * 2), lds0 + wdst[k] + slot * kWSLOT);
+  };
+  half8 wh[2][NCB], wl[2][NCB];               // A fragments of taps tau (slot tau % 2) and tau + 1
+  auto wfrag = [&](auto r_tag, int slot) {
+    constexpr int R = decltype(r_tag)::value;
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
-      wh[S][c] = h5_half8(h5_bload(rsw, (int)wvo[c], so, 0));
-      wl[S][c] = h5_half8(h5_bload(rsw, (int)wvo[c], so + (int)(plane * 2u), 0));
+      const unsigned a = wfr + slot * kWSLOT + (cp * NCB + c) * 1024;
+      wh[R][c] = *reinterpret_cast<const half8*>(lds + a);
+      wl[R][c] = *reinterpret_cast<const half8*>(lds + a + NCB * 2048);
     }
   };
+  floatx4 stg[8];   // the converters' staged halo loads
 
-  // ---- the convert: halo pixel (iy, x), iy = 0 .. 9 (tile rows -1 .. 8), 8 channels c8 per unit;
-  // unit i of a lane is halo pixel 128 i + tid / 4 (i = 3 only for tid < 64: 400 pixels)
+  // ---- the convert (waves 0 .. 3): halo pixel (iy, x), iy = 0 .. 9 (tile rows -1 .. 8), 8 channels c8 per
+  // unit; unit i of a lane is halo pixel 64 i + tid / 4, i = 0 .. 6 (unit 6: tid < 64 only, 400 pixels);
+  // group 0 = units 0 .. 3 (loaded at tap 0 of a chunk, converted at tap 3), group 1 = units 4 .. 6 (tap 3 -> 6)
   const int c8 = tid & 3;
   const int32x4 rs0 = make_rsrc(p.x0, (unsigned)((size_t)p.P * p.ldx0 * 4));
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const unsigned xplane = (unsigned)p.P * (unsigned)p.Cin;
-  floatx4 cv[2][2];
   auto unit_pos = [&](int i, int ttile, int& iy, int& x, int& gp, bool& valid) {
-    const int pi = i * 128 + (tid >> 2);
+    const int pi = i * 64 + (tid >> 2);
     iy = pi / kW;
     x = pi - kW * iy;
     const int kk = ttile - (ttile / tps) * tps;
     valid = !(iy == 0 && kk == 0) && !(iy == kTR + 1 && kk == tps - 1);
     gp = ttile * kM + (iy - 1) * kW + x;
   };
-  auto cv_issue = [&](auto g_tag, int ttile, int tch) {
-    constexpr int G = decltype(g_tag)::value;
+  // unit U's two loads live in staging slot U % 4 (units 4 .. 6 reuse the slots of units 0 .. 2)
+  auto cv_issue = [&](auto u_tag, int ttile, int tch) {
+    constexpr int U = decltype(u_tag)::value, SS = U % 4;
     const bool second = tch * 32 >= p.c0;
     const int ld = second ? p.ldx1 : p.ldx0;
     const int cb = (second ? tch * 32 - p.c0 : tch * 32) + c8 * 8;
-    h5_for<0, 2>([&](auto u_tag) {
-      constexpr int U = decltype(u_tag)::value, I = 2 * G + U;
-      int iy, x, gp;
-      bool valid;
-      unit_pos(I, ttile, iy, x, gp, valid);
-      // unit 3 exists for tid < 64 only (400 halo pixels); a zero fill past it
-      const bool on = I < 3 || (tid >> 2) + 384 < kHaloPix;
-      const unsigned vo = (on && valid) ? (unsigned)((gp * ld + cb) * 4) : OOB;
-      cv[U][0] = h5_bload(second ? rs1 : rs0, (int)vo, 0, 0);
-      cv[U][1] = h5_bload(second ? rs1 : rs0, (int)(vo + 16u), 0, 0);
-    });
+    int iy, x, gp;
+    bool valid;
+    unit_pos(U, ttile, iy, x, gp, valid);
+    const bool on = U < 6 || (tid >> 2) + 384 < kHaloPix;   // unit 6: tid < 64; a zero fill past it
+    const unsigned vo = (on && valid) ? (unsigned)((gp * ld + cb) * 4) : OOB;
+    stg[2 * SS] = h5_bload(second ? rs1 : rs0, (int)vo, 0, 0);
+    stg[2 * SS + 1] = h5_bload(second ? rs1 : rs0, (int)(vo + 16u), 0, 0);
   };
-  auto cv_process = [&](auto g_tag, int ttile, int tch) {
-    constexpr int G = decltype(g_tag)::value;
+  auto cv_process = [&](auto u_tag, int ttile, int tch) {
+    constexpr int U = decltype(u_tag)::value, SS = U % 4;
+    if (U == 6 && (tid >> 2) + 384 >= kHaloPix) return;   // (uniform per wave: unit 6 is wave 0's)
     const int buf = tch & 1;
     const bool second = tch * 32 >= p.c0;
-    const bool gate = GATE && second;
-    float4 s0, s1, t0, t1;
-    if constexpr (AFF) {
-      const int cc = tch * 32 + c8 * 8;
-      s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
-      s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
-      t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
-      t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
-    }
-    h5_for<0, 2>([&](auto u_tag) {
-      constexpr int U = decltype(u_tag)::value, I = 2 * G + U;
-      if (I < 3 || (tid >> 2) + 384 < kHaloPix) {   // (uniform per wave: unit 3 is wave 0's)
-        int iy, x, gp;
-        bool valid;
-        unit_pos(I, ttile, iy, x, gp, valid);
-        float4 v0 = make_float4(cv[U][0][0], cv[U][0][1], cv[U][0][2], cv[U][0][3]);
-        float4 v1 = make_float4(cv[U][1][0], cv[U][1][1], cv[U][1][2], cv[U][1][3]);
-        if (gate) gate8(v0, v1, h, valid ? gp : -1, p.P, HW, p.c1, tch * 32 - p.c0 + c8 * 8);
-        if constexpr (AFF) {   // fused BN + ReLU of the producer; rows outside the sample stay 0
-          const bool inside = valid;
+    int iy, x, gp;
+    bool valid;
+    unit_pos(U, ttile, iy, x, gp, valid);
+    float4 v0 = make_float4(stg[2 * SS][0], stg[2 * SS][1], stg[2 * SS][2], stg[2 * SS][3]);
+    float4 v1 = make_float4(stg[2 * SS + 1][0], stg[2 * SS + 1][1], stg[2 * SS + 1][2], stg[2 * SS + 1][3]);
+    if (GATE && second) gate8(v0, v1, h, valid ? gp : -1, p.P, HW, p.c1, tch * 32 - p.c0 + c8 * 8);
+    if constexpr (AFF) {   // fused BN + ReLU of the producer; rows outside the sample stay 0
+      const float* aff = reinterpret_cast<const float*>(lds + kOffA) + tch * 32 + c8 * 8;
+      const float4 s0 = *reinterpret_cast<const float4*>(aff), s1 = *reinterpret_cast<const float4*>(aff + 4);
+      const float4 t0 = *reinterpret_cast<const float4*>(aff + 192), t1 = *reinterpret_cast<const float4*>(aff + 196);
+      const bool inside = valid;
 #define AFF(V, S, T, X) V.X = inside ? fmaxf(V.X * S.X + T.X, 0.f) : 0.f;
-          AFF(v0, s0, t0, x) AFF(v0, s0, t0, y) AFF(v0, s0, t0, z) AFF(v0, s0, t0, w)
-          AFF(v1, s1, t1, x) AFF(v1, s1, t1, y) AFF(v1, s1, t1, z) AFF(v1, s1, t1, w)
+      AFF(v0, s0, t0, x) AFF(v0, s0, t0, y) AFF(v0, s0, t0, z) AFF(v0, s0, t0, w)
+      AFF(v1, s1, t1, x) AFF(v1, s1, t1, y) AFF(v1, s1, t1, z) AFF(v1, s1, t1, w)
 #undef AFF
-        }
-        half8 hv, lv;
-        split2h(v0, v1, sa, hv, lv);
-        char* dst = lds + buf * kSBUF + (iy * kPW + x + 1) * kSR + c8 * 16;
-        *reinterpret_cast<half8*>(dst) = hv;
-        *reinterpret_cast<half8*>(dst + 64) = lv;
-        if (TRAIN && iy >= 1 && iy <= kTR) {   // the tile's own pixels: the stored input split
-          _Float16* o = h.xsplit + (size_t)gp * p.Cin + tch * 32 + c8 * 8;
-          *reinterpret_cast<half8*>(o) = hv;
-          *reinterpret_cast<half8*>(o + xplane) = lv;
-        }
-      }
-    });
+    }
+    half8 hv, lv;
+    split2h(v0, v1, sa, hv, lv);
+    char* dst = lds + buf * kSBUF + (iy * kPW + x + 1) * kSR + c8 * 16;
+    *reinterpret_cast<half8*>(dst) = hv;
+    *reinterpret_cast<half8*>(dst + 64) = lv;
+    if (TRAIN && iy >= 1 && iy <= kTR) {   // the tile's own pixels: the stored input split
+      _Float16* o = h.xsplit + (size_t)gp * p.Cin + tch * 32 + c8 * 8;
+      *reinterpret_cast<half8*>(o) = hv;
+      *reinterpret_cast<half8*>(o + xplane) = lv;
+    }
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  using I6 = std::integral_constant<int, 6>;
 
   floatx4 acc[NCB][kNPB], part[NCB][kNPB];
   half8 xh[3], xl[3];   // fragment window (see tap)
   float amax_run = 0.f;
+  int tile_no = 0, nts = 0;
+  auto stamp = [&]() {
+    if constexpr ((H5_DBG & 16) != 0) {
+      if (tile_no == 1 && nts < 64) {
+        const unsigned long long tv = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        reinterpret_cast<unsigned long long*>(p.y + (size_t)p.P * p.ldy)[(size_t)blockIdx.x * 512 + wave * 64 + nts] = tv;
+      }
+      ++nts;
+    }
+  };
 
   // one tap T (0 .. 17) of the chunk pair (cc, cc + 1) of tile t: chunk cc + T / 9 from halo buffer T / 9
   auto tap = [&](auto T_tag, int cc, int t, bool has_next) {
     constexpr int T = decltype(T_tag)::value;
-    constexpr int B = T / 9, TT = T % 9, SL = T % H5_WSLOTS;
+    constexpr int B = T / 9, TT = T % 9, SL = T % 2;
     const int ch = cc + B;
-    // weights of tap T + 2 into slot (T + 2) % 3 (the chunk after the last is chunk 0 of the next tile)
-    {
-      constexpr int T2 = T + H5_WSLOTS - 1;
-      int ch2 = cc + T2 / 9;
-      if (ch2 >= nch) ch2 -= nch;
-      if constexpr (!(H5_DBG & 8)) wload(std::integral_constant<int, T2 % H5_WSLOTS>{}, ch2, T2 % 9);
+    // one barrier per tap: after it the ring slot of tap T + 1 is complete (DMA'd at tap T - 2, waited for by
+    // its loader just below) and the slot of tap T (read during tap T - 1) free
+    stamp();
+    if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCB) : "memory");   // DMA of tap T + 1 landed
+    asm volatile("s_barrier" ::: "memory");
+    stamp();
+    if constexpr (!(H5_DBG & 8)) {
+      wfrag(std::integral_constant<int, (T + 1) % 2>{}, (T + 1) % 3);   // A fragments of tap T + 1
+      if (loader) {
+        constexpr int T3 = T + 3;
+        int ch3 = cc + T3 / 9;
+        if (ch3 >= nch) ch3 -= nch;
+        wdma(ch3, T3 % 9, T % 3);                                       // tap T + 3 into tap T's slot
+      }
     }
+    __builtin_amdgcn_sched_barrier(0);
     // the convert of the chunk that follows this one (buffer B ^ 1): this tile's ch + 1, or the next
     // tile's chunk 0; loads at tap 0 / 3, split + LDS writes at tap 3 / 6 (a load group is waited for
     // three taps after its issue, when the weights issued after it are)
     const bool cv_next_tile = ch + 1 >= nch;
     const bool cv_on = (!cv_next_tile || has_next) && !(H5_DBG & 1);
     const int cv_tile = cv_next_tile ? t + 1 : t, cv_ch = cv_next_tile ? 0 : ch + 1;
-    if constexpr (TT == 0) {
-      if (cv_on) cv_issue(std::integral_constant<int, 0>{}, cv_tile, cv_ch);
-    }
-    if constexpr (TT == 3) {
-      if (cv_on) {
-        cv_process(std::integral_constant<int, 0>{}, cv_tile, cv_ch);
-        cv_issue(std::integral_constant<int, 1>{}, cv_tile, cv_ch);
+    // schedule (one or two units converted per tap, loads two to three taps ahead): tap 0 loads units 0 .. 3;
+    // tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5, 6, 7 convert
+    // 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk is read.
+    if (!loader && cv_on) {
+      if constexpr (TT == 0) {
+        cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
+        cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
       }
+      if constexpr (TT == 2) {
+        cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
+        cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
+      }
+      if constexpr (TT == 3) cv_process(I2{}, cv_tile, cv_ch);
+      if constexpr (TT == 4) {
+        cv_process(I3{}, cv_tile, cv_ch);
+        cv_issue(I6{}, cv_tile, cv_ch);
+      }
+      if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
+      if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
+      if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
     }
-    if constexpr (TT == 6) {
-      if (cv_on) cv_process(std::integral_constant<int, 1>{}, cv_tile, cv_ch);
-    }
-    if constexpr (TT == 0) {
-      if (B == 1 || cc > 0) {   // fold the previous chunk's partial chain (two-level accumulation)
+    if constexpr (TT == 0) {   // fold the previous chunk's partial chain (two-level accumulation)
+      if (B == 1 && cc == 0) {   // the tile's first chunk: 0 + part (no zeroing pass)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c)
+#pragma unroll
+          for (int j = 0; j < kNPB; ++j) acc[c][j] = part[c][j];
+      } else if (B == 1 || cc > 0) {
 #pragma unroll
         for (int c = 0; c < NCB; ++c)
 #pragma unroll
@@ -280,12 +368,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[SL][c], xh[SX], c0, 0, 0, 0);
         part[c][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[SL][c], xh[SX], c0, 0, 0, 0);
       }
-      if constexpr (TT == 8 && J == 3) {
-        // every wave has read the last fragments of this chunk (blocks 3, 4 of tap 8 in flight to its
-        // registers) and written its share of the next chunk: after the barrier the next chunk's buffer
-        // is complete and this chunk's buffer free
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
       {
         const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
         xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
@@ -297,63 +379,64 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     });
   };
 
-  // prologue: the first tile's chunk 0 into buffer 0, the weights of taps 0 and 1
-  cv_issue(std::integral_constant<int, 0>{}, t_beg, 0);
-  cv_process(std::integral_constant<int, 0>{}, t_beg, 0);
-  cv_issue(std::integral_constant<int, 1>{}, t_beg, 0);
-  cv_process(std::integral_constant<int, 1>{}, t_beg, 0);
-  h5_for<0, H5_WSLOTS - 1>([&](auto s_tag) { wload(s_tag, 0, decltype(s_tag)::value); });
+  // prologue: the first tile's chunk 0 into buffer 0, the ring's first taps
+  __syncthreads();   // (the staged parameters, before the first convert reads them)
+  if (!loader) {
+    cv_issue(I0{}, t_beg, 0); cv_issue(I1{}, t_beg, 0); cv_issue(I2{}, t_beg, 0); cv_issue(I3{}, t_beg, 0);
+    cv_process(I0{}, t_beg, 0); cv_process(I1{}, t_beg, 0); cv_process(I2{}, t_beg, 0); cv_process(I3{}, t_beg, 0);
+    cv_issue(I4{}, t_beg, 0); cv_issue(I5{}, t_beg, 0); cv_issue(I6{}, t_beg, 0);
+    cv_process(I4{}, t_beg, 0); cv_process(I5{}, t_beg, 0); cv_process(I6{}, t_beg, 0);
+  } else {   // the ring's taps 0, 1, 2
+    wdma(0, 0, 0);
+    wdma(0, 1, 1);
+    wdma(0, 2, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
+  wfrag(std::integral_constant<int, 0>{}, 0);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     xh[j] = *reinterpret_cast<const half8*>(lds + ab0[j]);
     xl[j] = *reinterpret_cast<const half8*>(lds + ab0[j] + 64);
   }
+  // (tap 0's DMA overwrites ring slot 0: this wave's reads of it are complete before the barrier)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   const float ia = exp2i(-ea);
   for (int t = t_beg; t < t_end; ++t) {
     const bool has_next = t + 1 < t_end;
-#pragma unroll
-    for (int c = 0; c < NCB; ++c)
-#pragma unroll
-      for (int j = 0; j < kNPB; ++j) acc[c][j] = floatx4{};
     for (int cc = 0; cc < nch; cc += 2) {
       h5_for<0, 18>([&](auto T_tag) { tap(T_tag, cc, t, has_next); });
     }
 
     // ---- epilogue: scales, bias, (eval) BN + ReLU, 16-B stores, (train) BN statistics
+    stamp();
     const int pix0 = t * kM + 80 * q;   // the wave's first pixel
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
       const int col0 = 16 * (cp * NCB + c) + 4 * lq;
       float v[kNPB][4];
-      const int4 we = *reinterpret_cast<const int4*>(h.wexp + col0);
-      const float4 bi = p.bias != nullptr ? *reinterpret_cast<const float4*>(p.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* prm = reinterpret_cast<const float*>(lds + kOffP) + col0;
+      const int4 we = *reinterpret_cast<const int4*>(prm);
+      const float4 bi = *reinterpret_cast<const float4*>(prm + 64);
       const int wer[4] = {we.x, we.y, we.z, we.w};
       const float bir[4] = {bi.x, bi.y, bi.z, bi.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // the operand scales undone: acc * 2^-(ea + wexp), in two exact steps where 2^-(ea + wexp) is no
+        // normal float (conv_fwd_h4_kernel); pm = 1 or 2^-ea (a multiply by 1 is exact: same bits)
         const int e = ea + wer[r];
-        float cs;
-        bool pre = false;
-        if (e > 126 || e < -126) {   // (conv_fwd_h4_kernel: the operand scale undone in two steps)
-          pre = true;
-          cs = exp2i(-wer[r]);
-        } else {
-          cs = exp2i(-e);
-        }
+        const bool two = e > 126 || e < -126;
+        const float cs = exp2i(two ? -wer[r] : -e), pm = two ? ia : 1.f;
 #pragma unroll
-        for (int j = 0; j < kNPB; ++j) {
-          float a = acc[c][j][r] + part[c][j][r];   // the last chunk's fold
-          if (pre) a *= ia;
-          v[j][r] = __builtin_fmaf(a, cs, bir[r]);
-        }
+        for (int j = 0; j < kNPB; ++j)
+          v[j][r] = __builtin_fmaf((acc[c][j][r] + part[c][j][r]) * pm, cs, bir[r]);   // the last chunk's fold
       }
       if constexpr (EPBN) {   // eval-mode BN + ReLU (ConvParams::ep_*)
-        const float4 mu = *reinterpret_cast<const float4*>(p.ep_mean + col0);
-        const float4 is = *reinterpret_cast<const float4*>(p.ep_invstd + col0);
-        const float4 ga = *reinterpret_cast<const float4*>(p.ep_gamma + col0);
-        const float4 be = *reinterpret_cast<const float4*>(p.ep_beta + col0);
+        const float4 mu = *reinterpret_cast<const float4*>(prm + 128);
+        const float4 is = *reinterpret_cast<const float4*>(prm + 192);
+        const float4 ga = *reinterpret_cast<const float4*>(prm + 256);
+        const float4 be = *reinterpret_cast<const float4*>(prm + 320);
         const float mur[4] = {mu.x, mu.y, mu.z, mu.w}, isr[4] = {is.x, is.y, is.z, is.w};
         const float gar[4] = {ga.x, ga.y, ga.z, ga.w}, ber[4] = {be.x, be.y, be.z, be.w};
 #pragma unroll
@@ -368,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
       for (int j = 0; j < kNPB; ++j) {
         float4* dst = reinterpret_cast<float4*>(p.y + (size_t)(pix0 + 16 * j + l16) * p.ldy + col0);
         float4 o = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
-        if (p.accumulate) {
+        if constexpr (ACC) {
           const float4 prev = *dst;
           o = make_float4(prev.x + o.x, prev.y + o.y, prev.z + o.z, prev.w + o.w);
         }
@@ -400,11 +483,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         }
       }
     }
+    stamp();
+    ++tile_no;
+    nts = 0;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last (unused) weight DMAs, before the workgroup ends
   if (EPBN && p.ep_amax != nullptr) {   // max|y| of the workgroup's tiles -> one atomicMax
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amax_run = fmaxf(amax_run, __shfl_xor(amax_run, o, 64));
-    float* red = reinterpret_cast<float*>(lds + 2 * kSBUF);
+    float* red = reinterpret_cast<float*>(lds + kOffR);
     if (lane == 0) red[wave] = amax_run;
     __syncthreads();
     if (tid == 0) {
@@ -443,6 +530,14 @@ template <int NCB>
 static int launch_h5_ncb(const ConvParams& p, const H3Args& h, int grid, hipStream_t st) {
   const bool aff = h.in_scale != nullptr, gate = h.x1_ca != nullptr, epbn = p.ep_mean != nullptr;
   const bool train = p.stats != nullptr || h.xsplit != nullptr;
+  if (p.accumulate) {   // (not in the U-Net's forward: the plain conv only)
+    if (aff || gate || train || epbn) {
+      set_error("srpde_conv_fwd_h3(h5): accumulate only without in_scale / gate / statistics / ep");
+      return kErrArg;
+    }
+    launch_h5_variant<NCB, H5_ACC>(p, h, grid, st);
+    return 0;
+  }
   // the U-Net's uses: eval (BN + ReLU epilogue, gated concat input), train (statistics + stored split,
   // fused input BN or gated concat input), and the plain conv
   if (!aff && !gate && !train && epbn) launch_h5_variant<NCB, H5_EPBN>(p, h, grid, st);
