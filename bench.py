@@ -493,6 +493,40 @@ def measure_traffic_live(layer):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def measure_step_traffic(batch):
+    """HBM bytes per dispatch of every kernel of the training step, measured now on this build: two rocprofv3
+    PMC passes (FETCH_SIZE, WRITE_SIZE -- separate runs, --kernel-trace only) over tools/step_once.py (the same
+    step as the timed region), reduced by tools/kernel_traffic.py (FETCH_SIZE x2, the guide's gfx950
+    correction).  Child processes under hard time limits, started before this process touches the GPU.
+    -> ({kernel name: record} or None, source note)."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="srpde_pmcs_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for i, c in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", c, "--kernel-trace", "--output-format", "csv",
+                   "-d", d, "-o", f"s{i}", "--", sys.executable, os.path.join(ROOT, "tools", "step_once.py"),
+                   "--steps", "1", "--batch", str(batch)]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            if r.returncode != 0:
+                return None, f"PMC pass {c} failed (rc {r.returncode})"
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kernel_traffic.py"), d],
+                           capture_output=True, text=True, timeout=120)
+        return (json.loads(r.stdout.strip().splitlines()[-1]),
+                "measured by this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
+                "tools/step_once.py (one warm-up + one training step), FETCH_SIZE x2 + WRITE_SIZE per dispatch, "
+                "averaged over the kernel's dispatches (tools/kernel_traffic.py)")
+    except Exception as e:   # noqa: BLE001 -- the bench line must not depend on the profiler
+        return None, f"PMC measurement failed: {e}"
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def launch_ranks(args):
     """``--gpus N > 1`` without a launcher: start ``torch.distributed.run`` with N ranks (one process
     per GPU) as a CHILD process -- this process has made no GPU call yet and makes none -- relay the
@@ -522,6 +556,9 @@ def main():
     if (ws is None and args.workload == "train" and not args.no_live_traffic and args.traffic_json is None
             and not args.ddp):
         live_traffic = measure_traffic_live(args.roofline_layer)   # before this process touches the GPU
+    step_traffic = (None, "not measured (--no-live-traffic / N > 1)")
+    if ws is None and args.workload == "train" and not args.no_live_traffic and not args.ddp:
+        step_traffic = measure_step_traffic(args.batch)
     pmc_poisson = None
     if ws is None and args.workload == "poisson" and not args.no_live_traffic:
         head = [s for s in args.poisson_sizes.split(",") if int(s.split(":")[0]) <= 128]
@@ -605,6 +642,12 @@ def main():
     # launches are bracketed with HIP events on the compute stream (the stream they run on)
     timed = []
     X.TIMED_LAYERS[args.roofline_layer] = timed
+    # every conv launch of the timed region is bracketed with HIP events on its stream and labelled with the
+    # kernel it ran (hipops.LAUNCH_TAP, srpde_last_kernel): the roofline prices the kernel with the largest
+    # total time
+    from superresolution_for_pdes_amd import hipops as H
+    launches = []
+    H.LAUNCH_TAP = launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -615,13 +658,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    H.LAUNCH_TAP = None
     X.TIMED_LAYERS.pop(args.roofline_layer, None)
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt)
     # after the timed region: the forward alone (every rank runs it; rank 0 reports)
-    from superresolution_for_pdes_amd import hipops as H
     math = H.conv_math()
     # dense MFMA peak of the instruction the kernel runs, in fp32-product units: fp32 MFMA
     # 157.3 TF; bf16 / fp16 MFMA run at 16x that (2516.8 TF), divided by the partial
@@ -630,12 +673,23 @@ def main():
     fwd_roof = forward_roofline(model, x, peak)
 
     if rank == 0:
-        kern_ms = [a.elapsed_time(b) for a, b in timed]
+        kern_ms = [a.elapsed_time(b) for a, b, _ in timed]
         kern_avg = sum(kern_ms) / max(len(kern_ms), 1)
         cin, cout, hw = next((c, o, h) for n, c, o, h in CONV3 if n == args.roofline_layer)
         flops_launch = conv_flops(cin, cout, hw) * B
         achieved = flops_launch / (kern_avg * 1e-3) / 1e12 if kern_avg > 0 else None
-        kname = {"h3": "conv_fwd_h3"}.get(math, "conv_fwd_v2")
+        kname = timed[0][2] if timed else {"h3": "conv_fwd_h3"}.get(math, "conv_fwd_v2")
+        # per kernel over the timed region: launches, total ms (event pairs on the launching stream: the main
+        # kernel plus the entry's small fixup / slab-reduction launches), algorithmic FLOP of its calls
+        fam = {}
+        for kn, fl, a, b in launches:
+            r = fam.setdefault(kn, [0, 0.0, 0.0])
+            r[0] += 1
+            r[1] += a.elapsed_time(b)
+            r[2] += fl
+        table = sorted(fam.items(), key=lambda kv: -kv[1][1])
+        top_name, (top_n, top_ms, top_fl) = table[0]
+        top_ach = top_fl / (top_ms * 1e-3) / 1e12
         traffic, tfile, tsource = None, args.traffic_json or default_traffic_json(), None
         if live_traffic is not None and live_traffic[0] and math == "h3":
             traffic, tsource = live_traffic
@@ -671,13 +725,26 @@ def main():
             "config": {"workload": "UNet 20->40 train step, fp32, batch 1024/GPU, 40x40",
                        "global_batch": world * B, "per_gpu_batch": B, "hw": "40x40",
                        "parallelism": f"dp{world}", "final_loss": round(float(loss.detach()), 6)},
-            "roofline": {"bound": "mfma", "kernel": f"{kname}[{args.roofline_layer}]",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": traffic,
-                         "traffic_source": tsource,
-                         "launch_ms": round(kern_avg, 4),
-                         "algorithmic_flop_per_launch": flops_launch,
+            "roofline": {"bound": "mfma",
+                         "kernel": top_name,
+                         "kernel_note": "the conv kernel with the largest total time in the timed region (HIP events "
+                                        "around every conv entry call on its stream, kernel names from "
+                                        "srpde_last_kernel); achieved = the algorithmic FLOP of its calls / their time",
+                         "achieved": round(top_ach, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(top_ach / peak, 4),
+                         "launch_ms": round(top_ms / top_n, 4),
+                         "launches": top_n, "algorithmic_flop": top_fl,
+                         "traffic": ((step_traffic[0] or {}).get(top_name) or {}).get("bytes_per_dispatch"),
+                         "traffic_source": step_traffic[1],
+                         "traffic_detail": (step_traffic[0] or {}).get(top_name),
+                         "kernels": [{"kernel": k, "launches": v[0], "ms": round(v[1], 3),
+                                      "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1),
+                                      "frac": round(v[2] / (v[1] * 1e-3) / 1e12 / peak, 4)} for k, v in table[:12]],
+                         "layer": {"kernel": f"{kname}[{args.roofline_layer}]",
+                                   "achieved": round(achieved, 2) if achieved else None,
+                                   "frac": round(achieved / peak, 4) if achieved else None,
+                                   "launch_ms": round(kern_avg, 4), "algorithmic_flop_per_launch": flops_launch,
+                                   "traffic": traffic, "traffic_source": tsource},
                          "step": {"algorithmic_flop": step_flop, "achieved": round(step_ach, 2),
                                   "frac": round(step_ach / peak, 4)},
                          "forward": fwd_roof},

@@ -45,10 +45,14 @@ typedef struct ihipStream_t* hipStream_t;
  *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa;
  *      srpde_conv_head_eval
  *   8  srpde_conv_h3_stats_rows_for, srpde_conv_h5_set (the h5 forward writes 80-row statistics),
- *      srpde_conv_head_eval_supported */
+ *      srpde_conv_head_eval_supported, srpde_last_kernel */
 #define SRPDE_ABI_VERSION 8
 
 const char* srpde_last_error(void);
+/* Name of the main kernel the last conv entry point (srpde_conv_fwd*, srpde_conv_dgrad_h3_bnb, srpde_conv_wgrad*,
+ * srpde_conv_head_eval) launched on this thread, as profilers print it, e.g. "conv_fwd_h5_kernel<2, 8>" (template
+ * arguments included, namespace and parameter list dropped).  Diagnostics / per-kernel roofline accounting. */
+const char* srpde_last_kernel(void);
 int srpde_version(void);
 
 /* ---- convolution: nn.Conv2d 3x3 (dilation 1|2) / 1x1 -------------------------------

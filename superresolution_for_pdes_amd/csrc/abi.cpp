@@ -7,6 +7,14 @@
 namespace srpde {
 
 static thread_local char g_err[512] = "";
+static thread_local char g_kern[192] = "";
+
+void note_kernel(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_kern, sizeof(g_kern), fmt, ap);
+  va_end(ap);
+}
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -20,6 +28,8 @@ void set_error(const char* fmt, ...) {
 extern "C" {
 
 const char* srpde_last_error(void) { return srpde::g_err; }
+
+const char* srpde_last_kernel(void) { return srpde::g_kern; }
 
 int srpde_version(void) { return SRPDE_ABI_VERSION; }
 

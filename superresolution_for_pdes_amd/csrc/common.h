@@ -20,6 +20,8 @@
 namespace srpde {
 
 void set_error(const char* fmt, ...);
+// the main kernel a conv entry point launched, as rocprofv3 names it (srpde_last_kernel; bench.py's roofline)
+void note_kernel(const char* fmt, ...);
 
 constexpr int kErrArg = -1;
 constexpr int kErrShape = -2;

@@ -330,6 +330,7 @@ static bool c4_ok(const ConvParams& p) {
 }
 
 static int launch_fwd_c4(const ConvParams& p, hipStream_t st) {
+  note_kernel("conv_fwd_c4_kernel");
   hipLaunchKernelGGL(conv_fwd_c4_kernel, dim3(ceil_div(p.P, 256), p.Cout / 64), dim3(256), 0, st, p);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd(c4)");
   return 0;

@@ -1696,6 +1696,8 @@ static int launch_fwd_h3(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;   // pieces are whole channel chunks
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
+  note_kernel("conv_fwd_h3_kernel<%d, %d, %d, %d, %d, %s, %d, %s, %s>", BM, BN, WM, WN, SRB, TWO_LEVEL ? "true" : "false",
+              TPS, BNB ? "true" : "false", PRE ? "true" : "false");
   hipLaunchKernelGGL((conv_fwd_h3_kernel<BM, BN, WM, WN, SRB, TWO_LEVEL, TPS, BNB, PRE>), dim3(grid), dim3(NT), lds, st,
                      p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3");
@@ -1758,6 +1760,7 @@ static int launch_fwd_h3r(ConvParams p, H3Args h, hipStream_t st, void* ws, size
   if (p.ntail > 0 && p.tsplit > nch) p.tsplit = nch;
   if (p.tsplit < 2) { p.ntail = 0; p.tsplit = 1; }
   const int grid = T - p.ntail + p.ntail * p.tsplit;
+  note_kernel("conv_fwd_h3r_kernel<%d, %d, %d, %d, %s>", BN, TPS, H3R_NTK, H3R_NB, PRE ? "true" : "false");
   hipLaunchKernelGGL((conv_fwd_h3r_kernel<BN, TPS, H3R_NTK, H3R_NB, PRE>), dim3(grid), dim3(256), lds, st, p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h3r)");
   if (p.ntail > 0) return launch_tail_fixup<BM, BN, SRB>(p, st);
@@ -1770,10 +1773,13 @@ int launch_wgrad_h3(const WgradParams& p, const unsigned* amax_dy, const unsigne
   const int nb = ceil_div(p.Cout, p.Cout >= 128 ? 128 : (p.Cout >= 64 ? 64 : 32)) *
                  ceil_div(p.K, p.Cout >= 128 ? 128 : 256) * p.splits;
   if (p.Cout >= 128) {
+    note_kernel("conv_wgrad_h3_kernel<128, 128, 2, 2, 4>");
     hipLaunchKernelGGL((conv_wgrad_h3_kernel<128, 128, 2, 2, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (128 + 128), st, p, sc);
   } else if (p.Cout >= 64) {
+    note_kernel("conv_wgrad_h3_kernel<64, 256, 1, 4, 4>");
     hipLaunchKernelGGL((conv_wgrad_h3_kernel<64, 256, 1, 4, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (64 + 256), st, p, sc);
   } else {
+    note_kernel("conv_wgrad_h3_kernel<32, 256, 1, 4, 4>");
     hipLaunchKernelGGL((conv_wgrad_h3_kernel<32, 256, 1, 4, 4>), dim3(nb), dim3(256), (size_t)2 * 2 * BKH * 2 * (32 + 256), st, p, sc);
   }
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3");
@@ -1832,6 +1838,7 @@ static int launch_h3h_cfg(const WgradParams& p, const H3P& q, hipStream_t st) {
   const int cc_n = p.Cin / 32;
   const int nb = ceil_div(p.Cout, BM) * cc_n * p.splits;
   const size_t lds = (size_t)NST * 2 * PS * BM * 2 + (size_t)2 * (CAP + 1) * 64;
+  note_kernel("conv_wgrad_h3h_kernel<%d, %d, %d, %d>", BM, PS, NST, CAP);
   hipLaunchKernelGGL((conv_wgrad_h3h_kernel<BM, PS, NST, CAP>), dim3(nb), dim3(576), lds, st, p, q, cc_n);
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p(h3h)");
   return 0;
@@ -1846,6 +1853,7 @@ static int launch_h3p(const WgradParams& p, const H3P& q, hipStream_t st) {
   constexpr int PS = 32, NST = 3;
   const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
   const size_t lds = (size_t)NST * 2 * PS * 2 * (BM + BN) + 1024;
+  note_kernel("conv_wgrad_h3p_kernel<%d, %d, %d, %d, %d, %d, 3>", BM, BN, WM, WN, PS, NST);
   hipLaunchKernelGGL((conv_wgrad_h3p_kernel<BM, BN, WM, WN, PS, NST, 3>), dim3(nb), dim3(WM * WN * 64), lds, st, p, q);
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p");
   return 0;

@@ -652,6 +652,7 @@ static int launch_h4_cfg(ConvParams p, H3Args h, hipStream_t st, void* ws, size_
   // K-pieces of the split tail)
   const int nitems = T - p.ntail + p.ntail * p.tsplit;
   const int grid = G::PERSIST ? std::min(nitems, cus) : nitems;
+  note_kernel("conv_fwd_h4_kernel<%d, %d, %d, %d, %s, %s>", W, DIL, BN, SIGN, PRE ? "true" : "false", UP ? "true" : "false");
   hipLaunchKernelGGL((conv_fwd_h4_kernel<W, DIL, BN, SIGN, PRE, UP>), dim3(grid), dim3(512), G::template lds<PRE>(), st,
                      p, h);
   SRPDE_LAUNCH_CHECK("srpde_conv_fwd_h3(h4)");

@@ -523,6 +523,7 @@ int h5_stats_rows() { return kSRB; }
 
 template <int NCB, int MODE>
 static void launch_h5_variant(const ConvParams& p, const H3Args& h, int grid, hipStream_t st) {
+  note_kernel("conv_fwd_h5_kernel<%d, %d>", NCB, MODE);
   hipLaunchKernelGGL((conv_fwd_h5_kernel<NCB, MODE>), dim3(grid), dim3(512), kLDS, st, p, h);
 }
 

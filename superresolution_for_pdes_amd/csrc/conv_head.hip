@@ -166,6 +166,7 @@ int srpde_conv_head_eval(const float* z, int ldz, const unsigned* amax_z, const 
   const size_t lds = (size_t)(HEAD_BM + 2 * (w + 1)) * HEAD_SR + 128;
   SRPDE_CHECK_ARG(srpde_conv_head_eval_supported(w), "srpde_conv_head_eval: image rows too wide for the tile (w=%d > 63)",
                   w);
+  note_kernel("conv_head_eval_kernel");
   hipLaunchKernelGGL(conv_head_eval_kernel, dim3(ceil_div(a.P, HEAD_BM)), dim3(256), lds, stream, a);
   SRPDE_LAUNCH_CHECK("srpde_conv_head_eval");
   return 0;

@@ -45,6 +45,24 @@ def set_conv_math(mode: str):
     _CONV_MATH = mode
 
 
+# per-kernel accounting (bench.py's roofline): while LAUNCH_TAP is a list, every conv entry call appends
+# (kernel name as rocprofv3 prints it -- srpde_last_kernel --, algorithmic FLOP, start event, end event), the
+# events recorded on the stream the call launches on
+LAUNCH_TAP = None
+
+
+def _conv_call(name, flop, *args):
+    tap = LAUNCH_TAP
+    if tap is None:
+        return call(name, *args)
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    call(name, *args)
+    b.record(st)
+    tap.append((query("srpde_last_kernel").decode(), float(flop), a, b))
+
+
 def conv_math() -> str:
     return _CONV_MATH
 
@@ -216,7 +234,7 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
                                  "with the input channels / bn_bwd_partials)")
         a0 = amax_of(x0)
         a1 = amax_of(x1) if x1 is not None else None
-        call("srpde_conv_fwd_h3", p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
+        _conv_call("srpde_conv_fwd_h3", 2.0 * cout * (x0.shape[1] + c1) * ksize * ksize * n * h * w, p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
              wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
              *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), _p(x1_gate[0] if x1_gate else None),
@@ -232,7 +250,7 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
             and x1_gate is None), "planes_out / in_affine / bn_bwd / out_max / x1_gate need the h3 kernels"
     if stats is not None and getattr(stats, "_srpde_rows", None) != int(query("srpde_conv_stats_rows_per_block", cout)):
         raise ValueError("statistics buffer not laid out for this conv family (use conv_stats_buffer)")
-    call("srpde_conv_fwd", p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
+    _conv_call("srpde_conv_fwd", 2.0 * cout * (x0.shape[1] + c1) * ksize * ksize * n * h * w, p0, x0.shape[1], ld0, p1, c1, ld1, wpack.data_ptr(), _p(bias), py, ldy,
          n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), *_ep_args(ep_bn), ws.data_ptr(), ws.numel(),
          stream_ptr())
     if ep_bn is not None:
@@ -250,7 +268,7 @@ def conv_fwd_presplit(xp, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1,
         if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
             raise ValueError("statistics buffer not laid out for the h3 kernel")
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
-    call("srpde_conv_fwd_h3_presplit", xp.data_ptr(), c, xp._srpde_amax.data_ptr(), planes.data_ptr(), wexp.data_ptr(),
+    _conv_call("srpde_conv_fwd_h3_presplit", 2.0 * cout * c * ksize * ksize * n * h * w, xp.data_ptr(), c, xp._srpde_amax.data_ptr(), planes.data_ptr(), wexp.data_ptr(),
          _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), *_bn_bwd_args(bn_bwd),
          _p(out_max), ws.data_ptr(), ws.numel(), stream_ptr())
 
@@ -351,7 +369,7 @@ def conv_dgrad_bnb(da, y, mean, invstd, gamma, beta, m1, m2, dy_amax, wpack, dx,
         if buf is not None and getattr(buf, "_srpde_rows", None) != int(query("srpde_conv_h3_stats_rows")):
             raise ValueError("statistics buffer not laid out for the h3 kernel (bn_bwd_partials)")
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cin_dx)), dx.device)
-    call("srpde_conv_dgrad_h3_bnb", pda, ldda, dy_amax.data_ptr(), py, ldy, mean.data_ptr(), invstd.data_ptr(),
+    _conv_call("srpde_conv_dgrad_h3_bnb", 2.0 * cin_dx * cout_dy * 9 * n * h * w, pda, ldda, dy_amax.data_ptr(), py, ldy, mean.data_ptr(), invstd.data_ptr(),
          gamma.data_ptr(), beta.data_ptr(), m1.data_ptr(), m2.data_ptr(), BN_RELU if relu else 0, planes.data_ptr(),
          wexp.data_ptr(), pdx, lddx, n, h, w, cout_dy, cin_dx, dil, dysplit.data_ptr(), *_bn_bwd_args(bn_bwd),
          _p(dx_max), ws.data_ptr(), ws.numel(), stream_ptr())
@@ -430,11 +448,11 @@ def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dy.device)
     if _CONV_MATH == "h3" and x0.shape[1] % 32 == 0 and c1 % 32 == 0 and cout % 16 == 0 and ksize == 3:
         a1 = amax_of(x1) if x1 is not None else None
-        call("srpde_conv_wgrad_h3", pdy, lddy, amax_of(dy).data_ptr(), p0, x0.shape[1], ld0, amax_of(x0).data_ptr(),
+        _conv_call("srpde_conv_wgrad_h3", 2.0 * cout * cin_real * ksize * ksize * n * h * w, pdy, lddy, amax_of(dy).data_ptr(), p0, x0.shape[1], ld0, amax_of(x0).data_ptr(),
              p1, c1, ld1, _p(a1), dw.data_ptr(), cin_real, int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(),
              ws_bytes, stream_ptr())
         return
-    call("srpde_conv_wgrad", pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1, dw.data_ptr(), cin_real,
+    _conv_call("srpde_conv_wgrad", 2.0 * cout * cin_real * ksize * ksize * n * h * w, pdy, lddy, p0, x0.shape[1], ld0, p1, c1, ld1, dw.data_ptr(), cin_real,
          int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes, stream_ptr())
 
 
@@ -455,7 +473,7 @@ def conv_wgrad_h3p(dyp, xp, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     c0 = cin - c1
     ws_bytes = int(query("srpde_conv_wgrad_h3p_workspace_size", n, h, w, cout, cin, ksize))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dyp.device)
-    call("srpde_conv_wgrad_h3p", dyp.data_ptr(), dyp._srpde_amax.data_ptr(), xp.data_ptr(), c0, a0.data_ptr(), c1,
+    _conv_call("srpde_conv_wgrad_h3p", 2.0 * cout * dw.shape[1] * ksize * ksize * n * h * w, dyp.data_ptr(), dyp._srpde_amax.data_ptr(), xp.data_ptr(), c0, a0.data_ptr(), c1,
          _p(a1), dw.data_ptr(), dw.shape[1], int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes,
          stream_ptr())
 
@@ -776,7 +794,7 @@ def conv_head_eval(z, wpack, bias, mean, invstd, gamma, beta, wf, bf, xin, n, h,
     planes, wexp = wpack.h3
     out = empty(n * h * w, device=z.device)
     pz, ldz = _pl(z)
-    call("srpde_conv_head_eval", pz, ldz, amax_of(z).data_ptr(), planes.data_ptr(), wexp.data_ptr(), _p(bias),
+    _conv_call("srpde_conv_head_eval", 2.0 * 16 * 32 * 9 * n * h * w, pz, ldz, amax_of(z).data_ptr(), planes.data_ptr(), wexp.data_ptr(), _p(bias),
          mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), wf.data_ptr(), bf.data_ptr(),
          xin.data_ptr(), xin.shape[1], n, h, w, out.data_ptr(), stream_ptr())
     return out

@@ -88,7 +88,7 @@ def _conv_launch(conv, *args, **kw):
     a.record()
     H.conv_fwd(*args, **kw)
     b.record()
-    sink.append((a, b))
+    sink.append((a, b, H.query("srpde_last_kernel").decode()))
 
 
 class GatedInput:
