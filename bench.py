@@ -133,6 +133,9 @@ def parse():
                          "every 3rd row / 5th column; tests/golden/cascade640_fixture.npz with the cascade20 state)")
     ap.add_argument("--ddp", action="store_true",
                     help="use the process group + DataParallel path even at world size 1 (RCCL smoke check)")
+    ap.add_argument("--ddp-rccl", action="store_true",
+                    help="with --ddp at world size 1: keep the buckets' one-rank RCCL all-reduce (by default a "
+                         "one-rank group skips it), so the step carries RCCL's kernels and stream")
     return ap.parse_args()
 
 
@@ -546,6 +549,7 @@ def launch_ranks(args):
 def main():
     global _JSON_OUT
     args = parse()
+    args.ddp = args.ddp or args.ddp_rccl
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -616,7 +620,7 @@ def main():
     net = model
     if use_pg:
         from superresolution_for_pdes_amd.distributed import DataParallel
-        net = DataParallel(model)
+        net = DataParallel(model, reduce_single_rank=args.ddp_rccl)
     opt = FusedAdamW(model.parameters(), lr=2e-4, weight_decay=1e-4, max_grad_norm=1.0)
 
     B = args.batch

@@ -45,6 +45,17 @@ __device__ __forceinline__ void h5_dma16(int32x4 rsrc, unsigned voff, unsigned s
       : "memory");
 }
 
+// 16-B buffer store as inline asm: the loader waves count their vector-memory operations exactly in the tap
+// waits (a store to a buffer of 0 records is dropped but still counted).  The s_nop is the wait state a VALU
+// write of the store's data registers needs after a store of more than 8 bytes: the compiler's hazard pass
+// does not see an asm store, and without it the first data register was measured overwritten before the
+// store read it
+__device__ __forceinline__ void h5_st16(floatx4 v, unsigned voff, int32x4 rsrc, unsigned soff) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rsrc),
+               "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory");
+}
+
 namespace {
 constexpr int kW = 40;                       // image width (compile-time: the pad geometry)
 constexpr int kTR = 8;                       // image rows per tile
@@ -57,8 +68,8 @@ constexpr int kNPB = 5;                      // 16-pixel blocks per wave
 constexpr int kSRB = 80;                     // rows per BN-statistics partial (one wave's pixels)
 constexpr int kOffW = 2 * kSBUF;             // the weight ring: 3 slots of one tap [2 planes][64 rows][64 B]
 constexpr int kWSLOT = 8192;
-constexpr int kOffP = kOffW + 3 * kWSLOT;     // per output channel: wexp, bias, eval BN mean / invstd / gamma / beta
-constexpr int kOffA = kOffP + 6 * 64 * 4;     // the fused input BN's scale / shift per input channel (<= 192)
+constexpr int kOffP = kOffW + 3 * kWSLOT;     // per output channel: cs, bias, eval BN mean / invstd / gamma / beta, pm
+constexpr int kOffA = kOffP + 8 * 64 * 4;     // the fused input BN's scale / shift per input channel (<= 192)
 constexpr int kOffR = kOffA + 2 * 192 * 4;    // the max|y| reduction
 constexpr int kLDS = kOffR + 64;
 constexpr int kHaloPix = (kTR + 2) * kW;     // 400 halo pixels converted per chunk (4 units of 8 channels each)
@@ -66,11 +77,17 @@ constexpr int kHaloPix = (kTR + 2) * kW;     // 400 halo pixels converted per ch
 
 // timing-only diagnostics (results wrong when non-zero; an A/B library is built with
 // SRPDE_EXTRA_FLAGS=-DH5_DBG=<bits>): 1 = no convert in the taps, 2 = no MFMAs, 4 = no epilogue stores,
-// 8 = no weight loads in the taps, 16 = phase timestamps (every wave stores s_memtime before and after every tap
+// 8 = no weight loads in the taps, 32 = no pixel-fragment reads in the taps, 64 = halo loads out of bounds (zeros), 16 = phase timestamps (every wave stores s_memtime before and after every tap
 // barrier and around the epilogue of its SECOND tile into room past the output: y + P * ldy + 512 * blockIdx.x +
 // 64 * wave 64-bit words; tools/h5_phase_ts.py)
 #ifndef H5_DBG
 #define H5_DBG 0
+#endif
+#ifndef H5_CVLATE
+#define H5_CVLATE 0
+#endif
+#ifndef H5_XEARLY
+#define H5_XEARLY 0
 #endif
 
 template <int B, int E, typename F>
@@ -137,7 +154,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     float* prm = reinterpret_cast<float*>(lds + kOffP);
     if (tid < p.Cout) {
       const int c = tid;
-      prm[c] = __int_as_float(h.wexp[c]);
+      // the operand scales undone: acc * 2^-(ea + wexp) as (acc * pm) * cs, in two exact steps where
+      // 2^-(ea + wexp) is no normal float (conv_fwd_h4_kernel); pm = 1 or 2^-ea (a multiply by 1 is exact)
+      const int e = ea + h.wexp[c];
+      const bool two = e > 126 || e < -126;
+      prm[c] = exp2i(two ? -h.wexp[c] : -e);
+      prm[384 + c] = two ? exp2i(-ea) : 1.f;
       prm[64 + c] = p.bias != nullptr ? p.bias[c] : 0.f;
       if constexpr (EPBN) {
         prm[128 + c] = p.ep_mean[c];
@@ -214,7 +236,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
   const int32x4 rs1 = make_rsrc(p.c1 ? p.x1 : p.x0, (unsigned)((size_t)p.P * (p.c1 ? p.ldx1 : p.ldx0) * 4));
   const unsigned xplane = (unsigned)p.P * (unsigned)p.Cin;
   auto unit_pos = [&](int i, int ttile, int& iy, int& x, int& gp, bool& valid) {
-    const int pi = i * 64 + (tid >> 2);
+    int tq = tid >> 2;
+    asm volatile("" : "+v"(tq));   // recomputed at each use: hoisted out of the tile loop they were spilled
+    const int pi = i * 64 + tq;
     iy = pi / kW;
     x = pi - kW * iy;
     const int kk = ttile - (ttile / tps) * tps;
@@ -231,7 +255,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     bool valid;
     unit_pos(U, ttile, iy, x, gp, valid);
     const bool on = U < 6 || (tid >> 2) + 384 < kHaloPix;   // unit 6: tid < 64; a zero fill past it
-    const unsigned vo = (on && valid) ? (unsigned)((gp * ld + cb) * 4) : OOB;
+    const unsigned vo = (on && valid && !(H5_DBG & 64)) ? (unsigned)((gp * ld + cb) * 4) : OOB;
     stg[2 * SS] = h5_bload(second ? rs1 : rs0, (int)vo, 0, 0);
     stg[2 * SS + 1] = h5_bload(second ? rs1 : rs0, (int)(vo + 16u), 0, 0);
   };
@@ -290,6 +314,105 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     }
   };
 
+  // ---- epilogue of 16-channel block C of a finished tile, from acc (the tile's sums): scales, bias, (eval)
+  // BN + ReLU, 16-B stores, (train) BN statistics.  Deferred into taps 9 - NCB .. 8 of the next tile's first chunk
+  // pair -- acc is dead there until the fold at tap 9 -- so its VALU work issues between that tap's MFMAs.  It
+  // runs at those taps of EVERY chunk pair, branch-free: its stores go to buffers of 0 records (dropped, and
+  // max|y| not updated) except in the first pair of a tile that has a predecessor in this workgroup; the last
+  // tile's epilogue runs after the loop.  Stores are inline asm, which the loader waves count in their tap waits.
+  unsigned eyo[NCB], eso[NCB];   // byte offsets of the lane's outputs / BN partials within a tile
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int col0 = 16 * (cp * NCB + c) + 4 * lq;
+    eyo[c] = (unsigned)(((80 * q + l16) * p.ldy + col0) * 4);
+    eso[c] = l16 == 0 ? (unsigned)((q * p.Cout + col0) * 8) : OOB;
+  }
+  int32x4 eyr = make_rsrc(p.y, 0u), esr = make_rsrc(p.stats, 0u);   // the epilogue's tile (0 records: none)
+  unsigned eso_t = 0;                                                // + its BN partial rows
+  bool e_on = false;
+  auto epi_tile = [&](int tt, bool on) {
+    e_on = on;
+    eyr = make_rsrc(p.y + (size_t)tt * kM * p.ldy, on ? (unsigned)(kM * p.ldy * 4) : 0u);
+    if constexpr (TRAIN) {
+      esr = make_rsrc(p.stats, on ? (unsigned)(p.P / kSRB * p.Cout * 8) : 0u);
+      eso_t = (unsigned)(tt * (kM / kSRB) * p.Cout * 8);
+    }
+  };
+  float4 ecs, epm, ebi, emu, eis, ega, ebe;
+  auto epi_prm = [&](int C) {
+    const float* prm = reinterpret_cast<const float*>(lds + kOffP) + 16 * (cp * NCB + C) + 4 * lq;
+    ecs = *reinterpret_cast<const float4*>(prm);
+    ebi = *reinterpret_cast<const float4*>(prm + 64);
+    epm = *reinterpret_cast<const float4*>(prm + 384);
+    if constexpr (EPBN) {
+      emu = *reinterpret_cast<const float4*>(prm + 128);
+      eis = *reinterpret_cast<const float4*>(prm + 192);
+      ega = *reinterpret_cast<const float4*>(prm + 256);
+      ebe = *reinterpret_cast<const float4*>(prm + 320);
+    }
+  };
+  auto epi_blk = [&](auto c_tag, auto j_tag, float(&v)[4]) {
+    constexpr int C = decltype(c_tag)::value, J = decltype(j_tag)::value;
+    const float cs[4] = {ecs.x, ecs.y, ecs.z, ecs.w}, pm[4] = {epm.x, epm.y, epm.z, epm.w};
+    const float bi[4] = {ebi.x, ebi.y, ebi.z, ebi.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(acc[C][J][r] * pm[r], cs[r], bi[r]);
+    if constexpr (EPBN) {   // eval-mode BN + ReLU (ConvParams::ep_*)
+      const float mu[4] = {emu.x, emu.y, emu.z, emu.w}, is[4] = {eis.x, eis.y, eis.z, eis.w};
+      const float ga[4] = {ega.x, ega.y, ega.z, ega.w}, be[4] = {ebe.x, ebe.y, ebe.z, ebe.w};
+      float m = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ep_bn_relu(v[r], mu[r], is[r], ga[r], be[r]);
+        m = fmaxf(m, fabsf(v[r]));
+      }
+      amax_run = e_on ? fmaxf(amax_run, m) : amax_run;
+    }
+    floatx4 o = {v[0], v[1], v[2], v[3]};
+    const unsigned so = (unsigned)(J * 16 * p.ldy * 4);
+    if constexpr (ACC) {
+      const floatx4 prev = h5_bload(eyr, (int)(eyo[C] + so), 0, 0);
+      o = floatx4{prev[0] + o[0], prev[1] + o[1], prev[2] + o[2], prev[3] + o[3]};
+    }
+    if constexpr (!(H5_DBG & 4)) h5_st16(o, eyo[C], eyr, so);
+  };
+  auto epi_stats = [&](auto c_tag, const float(&v)[kNPB][4]) {   // (mean, M2) of the wave's 80 pixels
+    constexpr int C = decltype(c_tag)::value;
+    float mean[4], m2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < kNPB; ++j) s += v[j][r];
+      mean[r] = h5_row_sum(s) / (float)kSRB;
+      float m = 0.f;
+#pragma unroll
+      for (int j = 0; j < kNPB; ++j) {
+        const float d = v[j][r] - mean[r];
+        m = __builtin_fmaf(d, d, m);
+      }
+      m2[r] = h5_row_sum(m);
+    }
+    if constexpr (!(H5_DBG & 4)) {
+      h5_st16(floatx4{mean[0], m2[0], mean[1], m2[1]}, eso[C], esr, eso_t);
+      h5_st16(floatx4{mean[2], m2[2], mean[3], m2[3]}, eso[C] + 16u, esr, eso_t);
+    }
+  };
+  auto epi_full = [&](auto c_tag) {
+    constexpr int C = decltype(c_tag)::value;
+    epi_prm(C);
+    float v[kNPB][4];
+    h5_for<0, kNPB>([&](auto j_tag) { epi_blk(c_tag, j_tag, v[decltype(j_tag)::value]); });
+    if constexpr (TRAIN) epi_stats(c_tag, v);
+  };
+  // the deferred epilogue runs block C at tap kEpiT0 + C: the last taps of the first chunk, where the converters'
+  // staging registers are free again
+  constexpr int kEpiT0 = 9 - NCB;
+  // vector-memory operations a loader wave issues at tap T after that tap's weight DMA (the deferred epilogue)
+  constexpr auto epi_ns = [](int T) {
+    return (!ACC && !(H5_DBG & 4) && T >= kEpiT0 && T < 9) ? kNPB + (TRAIN ? 2 : 0) : 0;
+  };
+
   // one tap T (0 .. 17) of the chunk pair (cc, cc + 1) of tile t: chunk cc + T / 9 from halo buffer T / 9
   auto tap = [&](auto T_tag, int cc, int t, bool has_next) {
     constexpr int T = decltype(T_tag)::value;
@@ -298,7 +421,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     // one barrier per tap: after it the ring slot of tap T + 1 is complete (DMA'd at tap T - 2, waited for by
     // its loader just below) and the slot of tap T (read during tap T - 1) free
     stamp();
-    if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCB) : "memory");   // DMA of tap T + 1 landed
+    // DMA of tap T + 1 (issued at tap T - 2) landed: younger are the DMA of tap T + 2 and the epilogue stores
+    // of taps T - 2 and T - 1
+    if (loader) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCB + epi_ns(T - 2) + epi_ns(T - 1)) : "memory");
     asm volatile("s_barrier" ::: "memory");
     stamp();
     if constexpr (!(H5_DBG & 8)) {
@@ -317,27 +442,68 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     const bool cv_next_tile = ch + 1 >= nch;
     const bool cv_on = (!cv_next_tile || has_next) && !(H5_DBG & 1);
     const int cv_tile = cv_next_tile ? t + 1 : t, cv_ch = cv_next_tile ? 0 : ch + 1;
-    // schedule (one or two units converted per tap, loads two to three taps ahead): tap 0 loads units 0 .. 3;
-    // tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5, 6, 7 convert
-    // 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk is read.
-    if (!loader && cv_on) {
-      if constexpr (TT == 0) {
-        cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
-        cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
+    auto convert_step = [&]() {
+      if constexpr (!H5_CVLATE) {
+        // schedule (one or two units converted per tap, loads two to three taps ahead): tap 0 loads units
+        // 0 .. 3; tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5,
+        // 6, 7 convert 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk
+        // is read.
+        if (!loader && cv_on) {
+          if constexpr (TT == 0) {
+            cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
+            cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
+          }
+          if constexpr (TT == 2) {
+            cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
+            cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
+          }
+          if constexpr (TT == 3) cv_process(I2{}, cv_tile, cv_ch);
+          if constexpr (TT == 4) {
+            cv_process(I3{}, cv_tile, cv_ch);
+            cv_issue(I6{}, cv_tile, cv_ch);
+          }
+          if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
+          if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
+          if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
+        }
+      } else {
+        // at the END of the tap (after its MFMAs), loads three to four taps ahead: tap 8 loads units 0 .. 3
+        // of the chunk converted during the NEXT chunk (the chunk after next); tap 2 converts 0, 1 and loads
+        // 4, 5; tap 3 converts 2 and loads 6; taps 4 .. 7 convert 3 .. 6
+        if (!loader) {
+          if (cv_on) {
+            if constexpr (TT == 2) {
+              cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
+              cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
+            }
+            if constexpr (TT == 3) {
+              cv_process(I2{}, cv_tile, cv_ch);
+              cv_issue(I6{}, cv_tile, cv_ch);
+            }
+            if constexpr (TT == 4) cv_process(I3{}, cv_tile, cv_ch);
+            if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
+            if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
+            if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
+          }
+          if constexpr (TT == 8) {
+            int nt = t, nc = ch + 2;
+            if (nc >= nch) {
+              nc -= nch;
+              nt = t + 1;
+            }
+            if (nt < t_end && !(H5_DBG & 1)) {
+              cv_issue(I0{}, nt, nc); cv_issue(I1{}, nt, nc);
+              cv_issue(I2{}, nt, nc); cv_issue(I3{}, nt, nc);
+            }
+          }
+        }
       }
-      if constexpr (TT == 2) {
-        cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
-        cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
-      }
-      if constexpr (TT == 3) cv_process(I2{}, cv_tile, cv_ch);
-      if constexpr (TT == 4) {
-        cv_process(I3{}, cv_tile, cv_ch);
-        cv_issue(I6{}, cv_tile, cv_ch);
-      }
-      if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
-      if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
-      if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
-    }
+    };
+    if constexpr (!H5_CVLATE) convert_step();
+    constexpr bool EPI = !ACC && T >= kEpiT0 && T < 9;   // the deferred epilogue's block T - kEpiT0 at this tap
+    constexpr int EC = EPI ? T - kEpiT0 : 0;
+    [[maybe_unused]] float ev[kNPB][4];
+    if constexpr (EPI) epi_prm(EC);
     if constexpr (TT == 0) {   // fold the previous chunk's partial chain (two-level accumulation)
       if (B == 1 && cc == 0) {   // the tile's first chunk: 0 + part (no zeroing pass)
 #pragma unroll
@@ -358,6 +524,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
       constexpr int G = 5 * T + J, SX = G % 3;
       constexpr int G2 = (G + 2) % 90, T2 = G2 / 5, J2 = G2 % 5, B2 = T2 / 9, TT2 = T2 % 9;
       constexpr int TOFF2 = ((TT2 / 3) * kPW + TT2 % 3) * kSR;
+      auto xread = [&]() {
+        if constexpr (!(H5_DBG & 32)) {
+          const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
+          xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
+          xl[G2 % 3] = *reinterpret_cast<const half8*>(lds + a + 64);
+        }
+      };
+      if constexpr (H5_XEARLY) xread();
 #pragma unroll
       for (int c = 0; c < NCB && !(H5_DBG & 2); ++c) {
         floatx4 c0;
@@ -368,15 +542,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[SL][c], xh[SX], c0, 0, 0, 0);
         part[c][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[SL][c], xh[SX], c0, 0, 0, 0);
       }
-      {
-        const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
-        xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
-        xl[G2 % 3] = *reinterpret_cast<const half8*>(lds + a + 64);
+      if constexpr (!H5_XEARLY) xread();
+      if constexpr (EPI) {
+        epi_blk(std::integral_constant<int, EC>{}, j_tag, ev[J]);
+        if constexpr (TRAIN && J == kNPB - 1) epi_stats(std::integral_constant<int, EC>{}, ev);
       }
       // keep the block's order (its MFMAs, then one block's reads): the scheduler would otherwise hoist
       // reads into fresh registers and run out of them
       __builtin_amdgcn_sched_barrier(0);
     });
+    if constexpr (H5_CVLATE) convert_step();
   };
 
   // prologue: the first tile's chunk 0 into buffer 0, the ring's first taps
@@ -386,6 +561,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     cv_process(I0{}, t_beg, 0); cv_process(I1{}, t_beg, 0); cv_process(I2{}, t_beg, 0); cv_process(I3{}, t_beg, 0);
     cv_issue(I4{}, t_beg, 0); cv_issue(I5{}, t_beg, 0); cv_issue(I6{}, t_beg, 0);
     cv_process(I4{}, t_beg, 0); cv_process(I5{}, t_beg, 0); cv_process(I6{}, t_beg, 0);
+    if constexpr (H5_CVLATE) {   // the first load group of the convert during chunk 0 (chunk 1's data)
+      cv_issue(I0{}, t_beg, 1); cv_issue(I1{}, t_beg, 1); cv_issue(I2{}, t_beg, 1); cv_issue(I3{}, t_beg, 1);
+    }
   } else {   // the ring's taps 0, 1, 2
     wdma(0, 0, 0);
     wdma(0, 1, 1);
@@ -402,90 +580,28 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
   // (tap 0's DMA overwrites ring slot 0: this wave's reads of it are complete before the barrier)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  const float ia = exp2i(-ea);
   for (int t = t_beg; t < t_end; ++t) {
     const bool has_next = t + 1 < t_end;
     for (int cc = 0; cc < nch; cc += 2) {
+      if constexpr (!ACC) epi_tile(t - 1, cc == 0 && t > t_beg);   // the previous tile's epilogue, taps 9 - NCB .. 8
       h5_for<0, 18>([&](auto T_tag) { tap(T_tag, cc, t, has_next); });
     }
-
-    // ---- epilogue: scales, bias, (eval) BN + ReLU, 16-B stores, (train) BN statistics
-    stamp();
-    const int pix0 = t * kM + 80 * q;   // the wave's first pixel
+    // the last chunk's fold: acc = the tile's sums
 #pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      const int col0 = 16 * (cp * NCB + c) + 4 * lq;
-      float v[kNPB][4];
-      const float* prm = reinterpret_cast<const float*>(lds + kOffP) + col0;
-      const int4 we = *reinterpret_cast<const int4*>(prm);
-      const float4 bi = *reinterpret_cast<const float4*>(prm + 64);
-      const int wer[4] = {we.x, we.y, we.z, we.w};
-      const float bir[4] = {bi.x, bi.y, bi.z, bi.w};
+    for (int c = 0; c < NCB; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        // the operand scales undone: acc * 2^-(ea + wexp), in two exact steps where 2^-(ea + wexp) is no
-        // normal float (conv_fwd_h4_kernel); pm = 1 or 2^-ea (a multiply by 1 is exact: same bits)
-        const int e = ea + wer[r];
-        const bool two = e > 126 || e < -126;
-        const float cs = exp2i(two ? -wer[r] : -e), pm = two ? ia : 1.f;
-#pragma unroll
-        for (int j = 0; j < kNPB; ++j)
-          v[j][r] = __builtin_fmaf((acc[c][j][r] + part[c][j][r]) * pm, cs, bir[r]);   // the last chunk's fold
-      }
-      if constexpr (EPBN) {   // eval-mode BN + ReLU (ConvParams::ep_*)
-        const float4 mu = *reinterpret_cast<const float4*>(prm + 128);
-        const float4 is = *reinterpret_cast<const float4*>(prm + 192);
-        const float4 ga = *reinterpret_cast<const float4*>(prm + 256);
-        const float4 be = *reinterpret_cast<const float4*>(prm + 320);
-        const float mur[4] = {mu.x, mu.y, mu.z, mu.w}, isr[4] = {is.x, is.y, is.z, is.w};
-        const float gar[4] = {ga.x, ga.y, ga.z, ga.w}, ber[4] = {be.x, be.y, be.z, be.w};
-#pragma unroll
-        for (int j = 0; j < kNPB; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[j][r] = ep_bn_relu(v[j][r], mur[r], isr[r], gar[r], ber[r]);
-            amax_run = fmaxf(amax_run, fabsf(v[j][r]));
-          }
-      }
-#pragma unroll
-      for (int j = 0; j < kNPB; ++j) {
-        float4* dst = reinterpret_cast<float4*>(p.y + (size_t)(pix0 + 16 * j + l16) * p.ldy + col0);
-        float4 o = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
-        if constexpr (ACC) {
-          const float4 prev = *dst;
-          o = make_float4(prev.x + o.x, prev.y + o.y, prev.z + o.z, prev.w + o.w);
-        }
-        if ((H5_DBG & 4) && o.x != 123.f) continue;
-        *dst = o;
-      }
-      if constexpr (TRAIN) {   // (mean, M2) of the wave's 80 pixels per channel
-        float mean[4], m2[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s = 0.f;
-#pragma unroll
-          for (int j = 0; j < kNPB; ++j) s += v[j][r];
-          mean[r] = h5_row_sum(s) / (float)kSRB;
-          float m = 0.f;
-#pragma unroll
-          for (int j = 0; j < kNPB; ++j) {
-            const float d = v[j][r] - mean[r];
-            m = __builtin_fmaf(d, d, m);
-          }
-          m2[r] = h5_row_sum(m);
-        }
-        if (l16 == 0) {
-          float2* st = p.stats + (size_t)(pix0 / kSRB) * p.Cout + col0;
-          st[0] = make_float2(mean[0], m2[0]);
-          st[1] = make_float2(mean[1], m2[1]);
-          st[2] = make_float2(mean[2], m2[2]);
-          st[3] = make_float2(mean[3], m2[3]);
-        }
-      }
+      for (int j = 0; j < kNPB; ++j) acc[c][j] += part[c][j];
+    if constexpr (ACC) {   // (y += conv: not deferred, the loads of y would stall the taps)
+      epi_tile(t, true);
+      h5_for<0, NCB>([&](auto c_tag) { epi_full(c_tag); });
     }
     stamp();
     ++tile_no;
     nts = 0;
+  }
+  if constexpr (!ACC) {   // the last tile's epilogue
+    epi_tile(t_end - 1, true);
+    h5_for<0, NCB>([&](auto c_tag) { epi_full(c_tag); });
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last (unused) weight DMAs, before the workgroup ends
   if (EPBN && p.ep_amax != nullptr) {   // max|y| of the workgroup's tiles -> one atomicMax

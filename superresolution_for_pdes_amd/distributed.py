@@ -62,7 +62,8 @@ class GradReducer:
 
     # a one-rank group has nothing to reduce: the mean over one rank is the gradient itself.  RCCL still
     # runs its one-rank all-reduce as a scaled copy of every bucket (oneRankReduce, 31 MB in and out,
-    # 0.2 ms of kernels beside the backward: +1.4 % on the world-1 step, profiles/r04l_dp_world1.txt)
+    # 0.2 ms of kernels beside the backward: +1.4 % on the world-1 step, profiles/r04l_dp_world1.txt).
+    # DataParallel(reduce_single_rank=True) keeps it (the one-GPU rehearsal of the RCCL path).
     skip_single_rank = True
 
     def _collective(self, chunk):
@@ -118,12 +119,17 @@ class DataParallel(torch.nn.Module):
     reference; see module docstring).  ``forward`` broadcasts BN buffers from rank 0 and
     runs the wrapped model; its backward all-reduces gradients bucket by bucket."""
 
-    def __init__(self, module, process_group=None, bucket_bytes: int = 8 << 20, broadcast_buffers: bool = True):
+    def __init__(self, module, process_group=None, bucket_bytes: int = 8 << 20, broadcast_buffers: bool = True,
+                 reduce_single_rank: bool = False):
+        """``reduce_single_rank``: run the buckets' all-reduce even in a one-rank group (RCCL's one-rank
+        reduce, a scaled copy per bucket), so a one-GPU rehearsal carries RCCL's kernels and stream beside
+        the backward exactly as an N > 1 step does; the default skips it (nothing to reduce)."""
         super().__init__()
         self.module = module
         self.pg = process_group
         self.broadcast_buffers = broadcast_buffers
         module._grad_reducer = GradReducer(process_group, bucket_bytes)
+        module._grad_reducer.skip_single_rank = not reduce_single_rank
         self._sync_params()
 
     @torch.no_grad()

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -112,3 +113,27 @@ def test_no_runtime_diagnostic_switch(lib):
     shipped library never reads it from the environment (the name is not even in its strings)."""
     data = open(lib.LIB_PATH, "rb").read()
     assert b"SRPDE_CONV_DBG" not in data
+
+
+def test_spill_budget(lib):
+    """Verdict r4 #9: no kernel of the shipped library spills more than its committed budget
+    (tests/spill_budget.json, written by tools/spill_budget.py --write; a kernel not listed has budget 0).
+    Reads .private_segment_fixed_size and the SGPR / VGPR spill counts from the code-object notes."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import spill_budget as SB
+    finally:
+        sys.path.pop(0)
+    if not os.path.exists(os.path.join(SB.LLVM, "clang-offload-bundler")):
+        pytest.skip("ROCm LLVM tools not present")
+    ks = SB.kernel_spills(lib.LIB_PATH)
+    assert sum(1 for k in ks if "conv_fwd_h5_kernel" in k) >= 10   # the notes really were read
+    budget = json.load(open(SB.BUDGET))["kernels"]
+    over = []
+    for name, rec in ks.items():
+        b = budget.get(name, {})
+        for k in SB.KEYS:
+            if rec[k] > b.get(k, 0):
+                over.append((SB.demangle([name])[0], k, rec[k], b.get(k, 0)))
+    assert not over, over

