@@ -550,6 +550,12 @@ def main():
     global _JSON_OUT
     args = parse()
     args.ddp = args.ddp or args.ddp_rccl
+    if os.environ.get("SRPDE_DUMP_MAPS"):
+        # debug aid: this process's memory map at Python exit, to attribute the frames of a native crash in
+        # a C-level exit handler (the rocprofv3 --pmc teardown fault)
+        import atexit
+        import shutil
+        atexit.register(lambda: shutil.copyfile("/proc/self/maps", os.environ["SRPDE_DUMP_MAPS"]))
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
         sys.exit(launch_ranks(args))

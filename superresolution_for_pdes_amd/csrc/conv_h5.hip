@@ -10,19 +10,19 @@
 //    tap of every lane is ONE compile-time LDS offset from the lane's pixel: no per-tap address math,
 //    no out-of-image masks (the pad ring and, at a sample's top / bottom, the halo rows are zeros).
 //    160-byte rows keep the 16x16x32 fragment reads conflict-free at any row shift.
-//  * The weights never touch LDS: each wave loads the B fragments of its output channels for tap
-//    tau + 2 straight into registers (buffer loads, L1 / L2 resident), so there is no weight ring, no
-//    weight DMA and no per-tap barrier.
-//  * Two halo buffers: while the nine taps of chunk c run from one, every wave converts its share of
-//    chunk c + 1 (register-staged fp32 loads -> fused input BN / gate -> scaled split -> LDS) into the
-//    other, spread over the taps so the VALU work issues beside the partner wave's MFMAs.  One
-//    workgroup barrier per chunk.  The last chunk of a tile converts the first chunk of the
-//    workgroup's next tile (persistent workgroups walk contiguous tile ranges, so a tile's top halo
-//    rows were its predecessor's bottom rows: L2 hits on the same XCD).
+//  * Weights: a tap's [2 planes][Cout][32] fp16 tile goes through a 3-slot LDS ring, DMA'd (buffer_load ...
+//    lds) three taps ahead by the four "loader" waves, one workgroup barrier per tap; every wave reads its A
+//    fragments of the next tap into registers.
+//  * Two halo buffers: while the nine taps of chunk c run from one, the four "converter" waves convert chunk
+//    c + 1 (register-staged fp32 loads -> fused input BN / gate -> scaled split -> LDS) into the other,
+//    one or two units per tap.  A SIMD runs one wave of each role.  The last chunk of a tile converts the
+//    first chunk of the workgroup's next tile (persistent workgroups walk contiguous tile ranges, so a
+//    tile's top halo rows were its predecessor's bottom rows: L2 hits on the same XCD).
 //  * The MFMA operands are swapped (weights as A, pixels as B): a lane's accumulator holds four
 //    consecutive output channels of one pixel, so the epilogue stores 16-byte NHWC pieces straight
 //    from registers and the BN statistics of a wave's 80 pixels (two image rows) reduce in registers
-//    and across a 16-lane DPP row -- one (mean, M2) partial per 80 rows, no LDS.
+//    and across a 16-lane DPP row -- one (mean, M2) partial per 80 rows, no LDS.  The epilogue of a
+//    tile runs inside the next tile's taps 7 .. 8 (its accumulators are dead there), between MFMAs.
 // Layout per wave (8 waves, 2 per SIMD): output channels 32*(w & 1) .. + 32 (two 16-channel blocks;
 // one at Cout = 32), pixels 80*(w >> 1) .. + 80 (five 16-pixel blocks).
 #include <atomic>
@@ -83,12 +83,7 @@ constexpr int kHaloPix = (kTR + 2) * kW;     // 400 halo pixels converted per ch
 #ifndef H5_DBG
 #define H5_DBG 0
 #endif
-#ifndef H5_CVLATE
-#define H5_CVLATE 0
-#endif
-#ifndef H5_XEARLY
-#define H5_XEARLY 0
-#endif
+
 
 template <int B, int E, typename F>
 __device__ __forceinline__ void h5_for(F&& f) {
@@ -442,64 +437,28 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     const bool cv_next_tile = ch + 1 >= nch;
     const bool cv_on = (!cv_next_tile || has_next) && !(H5_DBG & 1);
     const int cv_tile = cv_next_tile ? t + 1 : t, cv_ch = cv_next_tile ? 0 : ch + 1;
-    auto convert_step = [&]() {
-      if constexpr (!H5_CVLATE) {
-        // schedule (one or two units converted per tap, loads two to three taps ahead): tap 0 loads units
-        // 0 .. 3; tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5,
-        // 6, 7 convert 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk
-        // is read.
-        if (!loader && cv_on) {
-          if constexpr (TT == 0) {
-            cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
-            cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
-          }
-          if constexpr (TT == 2) {
-            cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
-            cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
-          }
-          if constexpr (TT == 3) cv_process(I2{}, cv_tile, cv_ch);
-          if constexpr (TT == 4) {
-            cv_process(I3{}, cv_tile, cv_ch);
-            cv_issue(I6{}, cv_tile, cv_ch);
-          }
-          if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
-          if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
-          if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
-        }
-      } else {
-        // at the END of the tap (after its MFMAs), loads three to four taps ahead: tap 8 loads units 0 .. 3
-        // of the chunk converted during the NEXT chunk (the chunk after next); tap 2 converts 0, 1 and loads
-        // 4, 5; tap 3 converts 2 and loads 6; taps 4 .. 7 convert 3 .. 6
-        if (!loader) {
-          if (cv_on) {
-            if constexpr (TT == 2) {
-              cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
-              cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
-            }
-            if constexpr (TT == 3) {
-              cv_process(I2{}, cv_tile, cv_ch);
-              cv_issue(I6{}, cv_tile, cv_ch);
-            }
-            if constexpr (TT == 4) cv_process(I3{}, cv_tile, cv_ch);
-            if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
-            if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
-            if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
-          }
-          if constexpr (TT == 8) {
-            int nt = t, nc = ch + 2;
-            if (nc >= nch) {
-              nc -= nch;
-              nt = t + 1;
-            }
-            if (nt < t_end && !(H5_DBG & 1)) {
-              cv_issue(I0{}, nt, nc); cv_issue(I1{}, nt, nc);
-              cv_issue(I2{}, nt, nc); cv_issue(I3{}, nt, nc);
-            }
-          }
-        }
+    // schedule (one or two units converted per tap, loads two to three taps ahead): tap 0 loads units
+    // 0 .. 3; tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5,
+    // 6, 7 convert 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk
+    // is read.
+    if (!loader && cv_on) {
+      if constexpr (TT == 0) {
+        cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
+        cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
       }
-    };
-    if constexpr (!H5_CVLATE) convert_step();
+      if constexpr (TT == 2) {
+        cv_process(I0{}, cv_tile, cv_ch); cv_process(I1{}, cv_tile, cv_ch);
+        cv_issue(I4{}, cv_tile, cv_ch); cv_issue(I5{}, cv_tile, cv_ch);
+      }
+      if constexpr (TT == 3) cv_process(I2{}, cv_tile, cv_ch);
+      if constexpr (TT == 4) {
+        cv_process(I3{}, cv_tile, cv_ch);
+        cv_issue(I6{}, cv_tile, cv_ch);
+      }
+      if constexpr (TT == 5) cv_process(I4{}, cv_tile, cv_ch);
+      if constexpr (TT == 6) cv_process(I5{}, cv_tile, cv_ch);
+      if constexpr (TT == 7) cv_process(I6{}, cv_tile, cv_ch);
+    }
     constexpr bool EPI = !ACC && T >= kEpiT0 && T < 9;   // the deferred epilogue's block T - kEpiT0 at this tap
     constexpr int EC = EPI ? T - kEpiT0 : 0;
     [[maybe_unused]] float ev[kNPB][4];
@@ -524,14 +483,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
       constexpr int G = 5 * T + J, SX = G % 3;
       constexpr int G2 = (G + 2) % 90, T2 = G2 / 5, J2 = G2 % 5, B2 = T2 / 9, TT2 = T2 % 9;
       constexpr int TOFF2 = ((TT2 / 3) * kPW + TT2 % 3) * kSR;
-      auto xread = [&]() {
-        if constexpr (!(H5_DBG & 32)) {
-          const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
-          xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
-          xl[G2 % 3] = *reinterpret_cast<const half8*>(lds + a + 64);
-        }
-      };
-      if constexpr (H5_XEARLY) xread();
 #pragma unroll
       for (int c = 0; c < NCB && !(H5_DBG & 2); ++c) {
         floatx4 c0;
@@ -542,7 +493,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[SL][c], xh[SX], c0, 0, 0, 0);
         part[c][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[SL][c], xh[SX], c0, 0, 0, 0);
       }
-      if constexpr (!H5_XEARLY) xread();
+      if constexpr (!(H5_DBG & 32)) {
+        const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
+        xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
+        xl[G2 % 3] = *reinterpret_cast<const half8*>(lds + a + 64);
+      }
       if constexpr (EPI) {
         epi_blk(std::integral_constant<int, EC>{}, j_tag, ev[J]);
         if constexpr (TRAIN && J == kNPB - 1) epi_stats(std::integral_constant<int, EC>{}, ev);
@@ -551,7 +506,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
       // reads into fresh registers and run out of them
       __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (H5_CVLATE) convert_step();
   };
 
   // prologue: the first tile's chunk 0 into buffer 0, the ring's first taps
@@ -561,9 +515,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     cv_process(I0{}, t_beg, 0); cv_process(I1{}, t_beg, 0); cv_process(I2{}, t_beg, 0); cv_process(I3{}, t_beg, 0);
     cv_issue(I4{}, t_beg, 0); cv_issue(I5{}, t_beg, 0); cv_issue(I6{}, t_beg, 0);
     cv_process(I4{}, t_beg, 0); cv_process(I5{}, t_beg, 0); cv_process(I6{}, t_beg, 0);
-    if constexpr (H5_CVLATE) {   // the first load group of the convert during chunk 0 (chunk 1's data)
-      cv_issue(I0{}, t_beg, 1); cv_issue(I1{}, t_beg, 1); cv_issue(I2{}, t_beg, 1); cv_issue(I3{}, t_beg, 1);
-    }
   } else {   // the ring's taps 0, 1, 2
     wdma(0, 0, 0);
     wdma(0, 1, 1);

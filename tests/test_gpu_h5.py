@@ -1,4 +1,4 @@
-"""The h5 convolution forward (conv_h5.hip: W = 40, tiles of 8 image rows, weights in registers) against the
+"""The h5 convolution forward (conv_h5.hip: W = 40, tiles of 8 image rows, weight taps through an LDS ring) against the
 h4 / h3r kernels it replaces for the U-Net's 40x40 layers (src/models.py:16,18,57: enc1.conv2, dec1.conv1,
 dec1.conv2, out_conv1).  Same fragments, products, accumulation order and epilogue expressions, so the conv
 outputs must be EQUAL bit for bit: plain, eval-mode epilogue (BN + ReLU, max|y| word), training (stored input

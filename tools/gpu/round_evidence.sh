@@ -23,5 +23,5 @@ python tools/traffic_json.py gpurun_out/pmc_$T bridge.3 gpurun_out/traffic_$T.js
 timeout -k 10 500 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { echo "bench failed"; tail -20 gpurun_out/bench_$T.err; exit 1; }
 cat gpurun_out/bench_$T.json
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o bench -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-live-traffic > $R/gpurun_out/prof_$T.log 2>&1 || { echo "prof failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o bench -- python $R/bench.py --no-cpu-baseline --no-live-traffic > $R/gpurun_out/prof_$T.log 2>&1 || { echo "prof failed"; exit 1; }
 echo "round evidence done"
