@@ -280,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     char* dst = lds + buf * kSBUF + (iy * kPW + x + 1) * kSR + c8 * 16;
     *reinterpret_cast<half8*>(dst) = hv;
     *reinterpret_cast<half8*>(dst + 64) = lv;
-    if (TRAIN && iy >= 1 && iy <= kTR) {   // the tile's own pixels: the stored input split
+    if (TRAIN && h.xsplit != nullptr && iy >= 1 && iy <= kTR) {   // the tile's own pixels: the stored input split
       _Float16* o = h.xsplit + (size_t)gp * p.Cin + tch * 32 + c8 * 8;
       *reinterpret_cast<half8*>(o) = hv;
       *reinterpret_cast<half8*>(o + xplane) = lv;
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     e_on = on;
     eyr = make_rsrc(p.y + (size_t)tt * kM * p.ldy, on ? (unsigned)(kM * p.ldy * 4) : 0u);
     if constexpr (TRAIN) {
-      esr = make_rsrc(p.stats, on ? (unsigned)(p.P / kSRB * p.Cout * 8) : 0u);
+      esr = make_rsrc(p.stats, on && p.stats != nullptr ? (unsigned)(p.P / kSRB * p.Cout * 8) : 0u);
       eso_t = (unsigned)(tt * (kM / kSRB) * p.Cout * 8);
     }
   };
