@@ -193,11 +193,36 @@ __global__ __launch_bounds__(256) void bn_relu_fwd_kernel(const float* __restric
 
 // Generic per-channel column reduction layout used by the backward passes:
 // block b owns rows [b*rows_per_blk, ...), threads tile (row, channel-quad).
+// rows a thread keeps in flight in the row loops below (bn_rows): one outstanding row per thread left
+// these HBM-bound kernels latency-bound at 2-3 TB/s.  The per-thread order of the rows (and of the sums
+// over them) is unchanged.
+constexpr int BN_U = 4;
+
 __device__ __forceinline__ void thread_rc(int C, int* c4, int* r0, int* rstride) {
   const int C4 = C >> 2;
   *c4 = threadIdx.x % C4;
   *r0 = threadIdx.x / C4;
   *rstride = blockDim.x / C4;
+}
+
+// rows p0, p0 + rs, ... < pe of (y, da) at channel quad c, handed in order to row(p, y quad, da quad): BN_U
+// rows loaded before the first is used, the last partial group one row at a time
+template <typename F>
+__device__ __forceinline__ void bn_rows(long long p0, long long pe, int rs, const float* __restrict__ y, int ldy,
+                                        const float* __restrict__ da, int ldda, int c, F&& row) {
+  for (; p0 + (BN_U - 1) * rs < pe; p0 += BN_U * rs) {
+    float4 vv[BN_U], dd[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      vv[u] = *reinterpret_cast<const float4*>(y + (p0 + u * rs) * ldy + c);
+      dd[u] = *reinterpret_cast<const float4*>(da + (p0 + u * rs) * ldda + c);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // (the scheduler would sink each load to its row)
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) row(p0 + u * rs, vv[u], dd[u]);
+  }
+  for (; p0 < pe; p0 += rs)
+    row(p0, *reinterpret_cast<const float4*>(y + p0 * ldy + c), *reinterpret_cast<const float4*>(da + p0 * ldda + c));
 }
 
 // partial sums of dz and dz*xhat per (block, channel); dz = da * [bn_out > 0]
@@ -224,9 +249,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     const float4 b = *reinterpret_cast<const float4*>(beta + c);
     const long long pb = (long long)blockIdx.x * rows_per_blk;
     const long long pe = min(P, pb + rows_per_blk);
-    for (long long p = pb + r0; p < pe; p += rs) {
-      const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
-      const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+    auto row = [&](long long, const float4& v, const float4& d) {
       dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
       float xh, dz;
 #define BN_ACC(X)                                              \
@@ -236,7 +259,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   s2.X += dz * xh;
       BN_ACC(x) BN_ACC(y) BN_ACC(z) BN_ACC(w)
 #undef BN_ACC
-    }
+    };
+    bn_rows(pb + r0, pe, rs, y, ldy, da, ldda, c, row);
   }
   red4[threadIdx.x] = s1;
   red4[256 + threadIdx.x] = s2;
@@ -321,9 +345,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     k.x = g.x * is.x; k.y = g.y * is.y; k.z = g.z * is.z; k.w = g.w * is.w;
     const long long pb = (long long)blockIdx.x * rows_per_blk;
     const long long pe = min(P, pb + rows_per_blk);
-    for (long long p = pb + r0; p < pe; p += rs) {
-      const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
-      const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+    auto row = [&](long long p, const float4& v, const float4& d) {
       float4 o;
       float xh, dz;
 #define BN_APPLY(X)                                            \
@@ -335,7 +357,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 #undef BN_APPLY
       *reinterpret_cast<float4*>(dy + p * lddy + c) = o;
       mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
-    }
+    };
+    bn_rows(pb + r0, pe, rs, y, ldy, da, ldda, c, row);
   }
   if (amax) block_amax(mx, amax);
   if (bias_part == nullptr) return;
@@ -395,9 +418,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __
   const float4 m2 = *reinterpret_cast<const float4*>(m2v + c);
   const float4 k = make_float4(g.x * is.x, g.y * is.y, g.z * is.z, g.w * is.w);
   const float s = exp2i(h3_exp(*dy_amax));
-  for (long long p = pb + r0; p < pe; p += rs) {
-    const float4 v = *reinterpret_cast<const float4*>(y + p * ldy + c);
-    const float4 d = *reinterpret_cast<const float4*>(da + p * ldda + c);
+  auto row = [&](long long p, const float4& v, const float4& d) {
     float o[4];
     float xh, dz;
 #define BN_APPLY_S(I, X)                                       \
@@ -416,7 +437,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_split_kernel(const float* __
     }
     *reinterpret_cast<half4*>(planes + (size_t)p * Cp + c) = hi;
     *reinterpret_cast<half4*>(planes + plane + (size_t)p * Cp + c) = lo;
-  }
+  };
+  bn_rows(pb + r0, pe, rs, y, ldy, da, ldda, c, row);
 }
 
 // The BN (+ReLU) backward's per-channel apply coefficients for a consumer that computes dy on the
