@@ -923,15 +923,26 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_v2_kernel(WgradParams p) {
 }
 
 // first level of a two-level slab sum (few elements, many slabs: enc1.conv1's 2304 weights over
-// ~2048 slabs): slab g*G <- sum of slabs [g*G, g*G + G) in order, one thread per (element, group)
-__global__ void slab_group_sum_kernel(float* __restrict__ part, int splits, int G, long long total) {
+// ~2048 slabs): slab g*G <- sum of slabs [g*G, g*G + G) in order, one thread per (element, group).
+// A whole group's G loads are issued before the in-order sum (one load in flight per thread made it
+// latency-bound: ~250 us per call for ~19 MB)
+template <int G>
+__global__ void slab_group_sum_kernel(float* __restrict__ part, int splits, long long total) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long ngroups = (splits + G - 1) / G;
   if (i >= total * ngroups) return;
   const long long g = i / total, e = i - g * total;
   const int q0 = (int)(g * G), q1 = min(splits, q0 + G);
   float s = 0.f;
-  for (int q = q0; q < q1; ++q) s += part[(size_t)q * total + e];
+  if (q1 - q0 == G) {
+    float v[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) v[u] = part[(size_t)(q0 + u) * total + e];
+#pragma unroll
+    for (int u = 0; u < G; ++u) s += v[u];
+  } else {
+    for (int q = q0; q < q1; ++q) s += part[(size_t)q * total + e];
+  }
   part[(size_t)q0 * total + e] = s;
 }
 
@@ -948,8 +959,18 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __res
   const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const long long e = (long long)blockIdx.x * 64 + el;
   float s = 0.f;
-  if (e < total)
-    for (int q = grp; q < splits; q += 4) s += part[(size_t)q * stride * cout * K + e];
+  if (e < total) {
+    const size_t qs = (size_t)stride * cout * K;
+    int q = grp;
+    for (; q + 28 < splits; q += 32) {   // eight of this thread's slabs loaded before their in-order sum
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(q + 4 * u) * qs + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; q < splits; q += 4) s += part[(size_t)q * qs + e];
+  }
   red[grp][el] = s;
   __syncthreads();
   if (grp == 0 && e < total) {
@@ -972,8 +993,8 @@ int wgrad_reduce(const float* part, float* dw, int splits, int cout, int cin, in
   if (total < 65536 && splits >= 128) {   // too few elements to keep the chip busy: sum groups of 32 first
     constexpr int G = 32;
     const long long work = total * ((splits + G - 1) / G);
-    hipLaunchKernelGGL(slab_group_sum_kernel, dim3((int)((work + 255) / 256)), dim3(256), 0, stream,
-                       const_cast<float*>(part), splits, G, total);
+    hipLaunchKernelGGL(slab_group_sum_kernel<G>, dim3((int)((work + 255) / 256)), dim3(256), 0, stream,
+                       const_cast<float*>(part), splits, total);
     SRPDE_LAUNCH_CHECK("srpde_conv_wgrad(reduce groups)");
     stride = G;
     splits = (splits + G - 1) / G;

@@ -1082,6 +1082,22 @@ __device__ __forceinline__ half8 tr_read(const lds_char* p0, const lds_char* p1)
 template <int RB>
 __device__ __forceinline__ int wx_swz(int row) { return (wx_off<RB>(row, 0) - row * RB) >> 4; }
 
+template <int B, int E, typename F>
+__device__ __forceinline__ void h3_for(F&& f) {   // f(integral_constant<B>), ..., f(integral_constant<E - 1>)
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    h3_for<B + 1, E>(f);
+  }
+}
+
+// timing-only diagnostics of the weight gradient (A/B builds, results wrong when non-zero): 1 = no stage wait /
+// barrier, 2 = no DMA in the stage loop (with the DMA, bridge.3's weight gradient took 1.39 ms, without it
+// 1.07 ms; issued right after the stage barrier, a stage's 48 DMA wave-instructions held up its first
+// MFMAs: spread over the stage's MFMA groups 1.26 ms, tools/gpu/wgrad_variants.sh)
+#ifndef H3P_DBG
+#define H3P_DBG 0
+#endif
+
 template <int BM, int BN, int WM, int WN, int PS, int NST, int HP>
 __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradParams p, H3P q) {
   constexpr int NW = WM * WN;
@@ -1157,13 +1173,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
     b_y[j] = rem / p.W;
     b_x[j] = rem - b_y[j] * p.W;
   }
-  // issue stage `s` into ring slot s % NST (always DA + DB ops per wave; past the chunk: zero fill)
-  auto issue = [&](int s, int slot) {
+  // issue stage `s` into ring slot s % NST (always DA + DB ops per wave; past the chunk: zero fill); ops
+  // [OLO, OHI) of the wave's A-then-B list (issue_part), all of them (issue)
+  auto issue_part = [&](int s, int slot, auto olo_tag, auto ohi_tag) {
+    constexpr int OLO = decltype(olo_tag)::value, OHI = decltype(ohi_tag)::value;
     char* st = lds + slot * STAGE;
     const int pbase = pbeg + s * PS;
     const bool full = pbase + PS <= pend;                // wave-uniform: no row of the stage is past the chunk
 #pragma unroll
     for (int j = 0; j < DA; ++j) {
+      if (j < OLO || j >= OHI) continue;
       const int w = wave + j * NW;
       const int pl = w / (NA / 2), idx = w - pl * (NA / 2);
       const bool in = full || pbase + a_row[j] < pend;
@@ -1172,6 +1191,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
     }
 #pragma unroll
     for (int j = 0; j < DB; ++j) {
+      if (DA + j < OLO || DA + j >= OHI) continue;
       const int w = wave + j * NW;
       const int pl = w / (NB / 2), idx = w - pl * (NB / 2);
       const bool ok = b_ok[j] && (full || pbase + b_row[j] < pend) && (unsigned)(b_y[j] + b_dy[j]) < (unsigned)p.H &&
@@ -1183,6 +1203,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
       if (y >= p.H) y -= p.H;
       b_x[j] = x; b_y[j] = y;
     }
+  };
+  auto issue = [&](int s, int slot) {
+    issue_part(s, slot, std::integral_constant<int, 0>{}, std::integral_constant<int, DPW>{});
   };
 
   const int ea = h3_exp(*q.ady);
@@ -1211,9 +1234,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
   auto stage = [&](int s, auto fresh_tag, auto slot_tag) {
     constexpr bool FRESH = decltype(fresh_tag)::value;
     constexpr int SLOT = decltype(slot_tag)::value;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DPW) : "memory");
-    __syncthreads();
-    issue(s + NST - 1, (SLOT + NST - 1) % NST);
+    if constexpr (!(H3P_DBG & 1)) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DPW) : "memory");
+      __syncthreads();
+    }
     const lds_char* sb = (const lds_char*)(uintptr_t)lds_addr_of(lds) + SLOT * STAGE;
     const lds_char* va[TI][2];   // this stage's per-lane fragment addresses (+ immediates below)
     const lds_char* vb[TJ][2];
@@ -1233,6 +1257,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
       for (int j = 0; j < TJ; ++j) {
         const half8 bh = tr_read(vb[j][0] + kk * 16 * RBB, vb[j][1] + kk * 16 * RBB);
         const half8 bl = tr_read(vb[j][0] + IMG_B + kk * 16 * RBB, vb[j][1] + IMG_B + kk * 16 * RBB);
+        if constexpr (!(H3P_DBG & 2)) {   // stage s + 2's DMA ops, spread over this stage's MFMA groups
+          constexpr int NG = (PS / 16) * TJ, PER = (DPW + NG - 1) / NG;
+          h3_for<0, PS / 16>([&](auto kk_tag) {
+            h3_for<0, TJ>([&](auto j_tag) {
+              constexpr int G = decltype(kk_tag)::value * TJ + decltype(j_tag)::value;
+              if (kk == decltype(kk_tag)::value && j == decltype(j_tag)::value && G * PER < DPW)
+                issue_part(s + NST - 1, (SLOT + NST - 1) % NST, std::integral_constant<int, G * PER>{},
+                           std::integral_constant<int, (G + 1) * PER < DPW ? (G + 1) * PER : DPW>{});
+            });
+          });
+        }
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           floatx16 c0;
@@ -1406,7 +1441,7 @@ __global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H
     if (wave < NHI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * (DLO + 1)) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DLO) : "memory");
     __syncthreads();
-    issue(s + NST - 1, (SLOT + NST - 1) % NST);
+
     const lds_char* sa = (const lds_char*)(uintptr_t)lds_addr_of(abuf) + SLOT * 2 * IMG_A;
     const int p0 = pbeg + s * PS;
     // fragments of kk + 1 are read while kk's MFMAs run (register double buffer)
@@ -1450,6 +1485,7 @@ __global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H
         c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][i], bl[cur], c0v, 0, 0, 0);
         part[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][i], bh[cur], c0v, 0, 0, 0);
       }
+      if (kk == 0) issue(s + NST - 1, (SLOT + NST - 1) % NST);   // stage s + 2's DMA after the first MFMAs
     }
     // the lane's pixels of the next stage
 #pragma unroll

@@ -903,12 +903,23 @@ __global__ __launch_bounds__(256) void weighted_colsum_kernel(const float* __res
   const long long pb = (long long)blockIdx.x * rows_per_blk;
   const long long pe = min(P, pb + rows_per_blk);
   if ((int)threadIdx.x < active) {
-    for (long long p = pb + r0; p < pe; p += rs) {
-      const float4 a = *reinterpret_cast<const float4*>(v + p * ldv + c4 * 4);
-      const float w = s[p];
+    auto row = [&](const float4& a, float w) {
       acc.x += a.x * w; acc.y += a.y * w; acc.z += a.z * w; acc.w += a.w * w;
       if (c4 == 0) sacc += w;
+    };
+    long long p = pb + r0;
+    for (; p + 3 * rs < pe; p += 4 * rs) {   // four rows' loads before their in-order sums
+      float4 a[4];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = *reinterpret_cast<const float4*>(v + (p + u * rs) * ldv + c4 * 4);
+        w[u] = s[p + u * rs];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row(a[u], w[u]);
     }
+    for (; p < pe; p += rs) row(*reinterpret_cast<const float4*>(v + p * ldv + c4 * 4), s[p]);
   }
   red4[threadIdx.x] = acc;
   red4[256 + threadIdx.x] = make_float4(sacc, 0.f, 0.f, 0.f);
@@ -940,7 +951,18 @@ __global__ __launch_bounds__(1024) void outer_sum_kernel(const float* __restrict
   const int j = blockIdx.y * 64 + jl;
   double s = 0.0;
   if (j < lb) {
-    for (int k = grp; k < n; k += 16) {
+    int k = grp;
+    for (; k + 7 * 16 < n; k += 8 * 16) {   // eight samples' loads before their in-order products
+      float av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        av[u] = a ? a[(long long)(k + 16 * u) * la + i] : 1.f;
+        bv[u] = b ? b[(long long)(k + 16 * u) * lb + j] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)av[u] * (double)bv[u];
+    }
+    for (; k < n; k += 16) {
       const double av = a ? (double)a[(long long)k * la + i] : 1.0;
       const double bv = b ? (double)b[(long long)k * lb + j] : 1.0;
       s += av * bv;
