@@ -120,7 +120,12 @@ bool h4_up_supported(int w, int dil, int cout);   // the upsampled-input forward
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes);
 bool h4_on();
 
-// h5 (conv_h5.hip): the W = 40 forward into 64 / 32 channels (8-row tiles, weights in registers)
+// the 16-output forward of out_conv2 in training (conv_head.hip): c0 == 32, c1 == 0, cout == 16, w <= 63
+// (with the h5 kernels: srpde_conv_h5_set(0) routes it back to h3r)
+bool n16_supported(int c0, int c1, int cout, int w, int dil);
+int launch_fwd_n16(const ConvParams& p, const H3Args& h, hipStream_t st);
+// h5 (conv_h5.hip): the W = 40 forward into 64 / 32 channels (8-row tiles, weight taps through an LDS ring)
+bool h5_on();
 bool h5_supported(int c0, int c1, int cout, int h, int w, int dil);
 int h5_set(int on);
 int h5_stats_rows();

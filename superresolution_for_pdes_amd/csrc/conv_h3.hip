@@ -2074,6 +2074,10 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                   "bn_part, cout %% 4 == 0");
   p.ep_mean = ep_mean; p.ep_invstd = ep_invstd; p.ep_gamma = ep_gamma; p.ep_beta = ep_beta;
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
+  // out_conv2's shape in training (32 -> 16, no epilogue BN): the 16-output kernel, 128-row statistics
+  if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr && ep_mean == nullptr && !accumulate &&
+      n16_supported(c0, c1, cout, w, dil) && ldx0 % 4 == 0 && aligned16(x0))
+    return launch_fwd_n16(p, a, stream);
   // h5 takes the forward of the shapes srpde_conv_h3_stats_rows_for reports 80-row statistics for
   if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr &&
       h5_supported(c0, c1, cout, h, w, dil)) {

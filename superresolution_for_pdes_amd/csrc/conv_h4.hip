@@ -312,7 +312,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
       t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
       t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
     }
-#pragma unroll
+    // (UP: not unrolled -- unrolled, the interpolating convert spilled 48-50 VGPRs; eval forward -1 %)
+#pragma unroll (UP ? 1 : (AROWS * 4 + 511) / 512)
     for (int k = 0; k < (AROWS * 4 + 511) / 512; ++k) {
       const int sg = tid + 512 * k;
       if (sg >= AROWS * 4) break;

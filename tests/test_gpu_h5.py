@@ -129,3 +129,45 @@ def test_conv_h5_accumulate_into_strided_output():
     finally:
         H.set_h5(prev)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("n,h", [(5, 40), (3, 16), (1, 7)])
+def test_conv_n16_equals_h3r(n, h):
+    """out_conv2's training forward (32 -> 16, conv_head.hip conv_fwd_n16_kernel) against the 32-column h3r
+    tile it replaces: y and the stored input split bit for bit (same products, same order), the 128-row BN
+    partials against fp64 statistics of the same y; with and without the fused input BN + ReLU; ragged
+    last block (n * h * 40 % 128 != 0)."""
+    from superresolution_for_pdes_amd import hipops as H
+    if H.conv_math() != "h3":
+        pytest.skip("h3 kernels off")
+    w_, cin, cout = 40, 32, 16
+    g = torch.Generator(device=DEV).manual_seed(23 + n)
+    P = n * h * w_
+    x = torch.randn(P, cin, device=DEV, generator=g)
+    x._srpde_amax = H.amax_of(x)
+    wt = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, _ = H.pack_conv_weights(wt, cin, True, False)
+    aff = (torch.rand(cin, device=DEV, generator=g) + 0.5, torch.randn(cin, device=DEV, generator=g) * 0.2)
+    for in_aff in (None, aff):
+        outs = []
+        prev = H.set_h5(True)
+        try:
+            for on in (False, True):
+                H.set_h5(on)
+                y = torch.empty(P, cout, device=DEV)
+                stats, nblk, rows = H.conv_stats_buffer(n, h, w_, cout, DEV, cin, 0, 1)
+                xp = H.split_planes_buffer(P, cin, DEV)
+                H.conv_fwd(x, None, wf, b, y, n, h, w_, cout, 3, 1, 1, False, stats, xp, in_affine=in_aff)
+                torch.cuda.synchronize()
+                outs.append((y, xp, stats, rows))
+        finally:
+            H.set_h5(prev)
+        assert torch.equal(outs[0][0], outs[1][0]), "y"
+        assert torch.equal(outs[0][1], outs[1][1]), "xsplit"
+        y, _, stats, rows = outs[1]
+        assert rows == 128
+        ref = _block_stats64(y, rows)
+        got = stats.double().view(ref.shape)
+        assert torch.allclose(got[:, :, 0], ref[:, :, 0], rtol=1e-5, atol=1e-6)
+        assert torch.allclose(got[:, :, 1], ref[:, :, 1], rtol=1e-4, atol=1e-4)
