@@ -97,6 +97,16 @@ __device__ __forceinline__ void gate8(float4& v0, float4& v1, const H3Args& h, i
   v1.x = (v1.x * a1.x) * s; v1.y = (v1.y * a1.y) * s; v1.z = (v1.z * a1.z) * s; v1.w = (v1.w * a1.w) * s;
 }
 
+// gate8 with the pixel's sample index n known (no division by H W; h5 has it from the tile index)
+__device__ __forceinline__ void gate8n(float4& v0, float4& v1, const H3Args& h, int n, int pix, int c1, int cc1) {
+  if (pix < 0) return;
+  const float4 a0 = *reinterpret_cast<const float4*>(h.x1_ca + (size_t)n * c1 + cc1);
+  const float4 a1 = *reinterpret_cast<const float4*>(h.x1_ca + (size_t)n * c1 + cc1 + 4);
+  const float s = h.x1_sa[pix];
+  v0.x = (v0.x * a0.x) * s; v0.y = (v0.y * a0.y) * s; v0.z = (v0.z * a0.z) * s; v0.w = (v0.w * a0.w) * s;
+  v1.x = (v1.x * a1.x) * s; v1.y = (v1.y * a1.y) * s; v1.z = (v1.z * a1.z) * s; v1.w = (v1.w * a1.w) * s;
+}
+
 // the K-split tail's fixup: one block per statistics sub-block of each tail tile (twice the blocks of a
 // whole-tile fixup for the same work: the tail has few tiles; 32.15 -> 32.12 ms per step) unless the
 // per-tile max|out| slot is wanted

@@ -2085,6 +2085,11 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
     SRPDE_CHECK_ARG(stats == nullptr, "srpde_conv_fwd_h3: the h5 shape (w=40, cout=%d) needs a 16-byte aligned y "
                     "with ldy %% 4 == 0 when it writes statistics", cout);
   }
+  // the eval decoder's dec1.conv1 (upsampled x0, gated x1, BN + ReLU epilogue) at W = 40: h5's UP variant
+  if (x0_up != nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr && ep_mean != nullptr &&
+      stats == nullptr && x1_ca != nullptr && !accumulate && h5_supported(c0, c1, cout, h, w, dil) && ldy % 4 == 0 &&
+      aligned16(y) && (c1 == 0 || ldx1 % 4 == 0))
+    return launch_fwd_h5(p, a, stream);
   SRPDE_CHECK_ARG(x0_up == nullptr || stats == nullptr || !h5_supported(c0, c1, cout, h, w, dil),
                   "srpde_conv_fwd_h3: an upsampled x0 with statistics at an h5 shape (w=40, cout=%d): the statistics "
                   "blocks would not be the srpde_conv_h3_stats_rows_for ones", cout);

@@ -111,12 +111,14 @@ constexpr int H5_GATE = 2;    // attention-gated second input (H3Args::x1_ca / x
 constexpr int H5_TRAIN = 4;   // BN statistics partials + the stored input split (ConvParams::stats, H3Args::xsplit)
 constexpr int H5_EPBN = 8;    // eval-mode BN + ReLU epilogue + max|y| (ConvParams::ep_*)
 constexpr int H5_ACC = 16;    // y += conv (ConvParams::accumulate)
+constexpr int H5_UP = 32;     // x0 is the bilinear x2 upsample of H3Args::up_src, interpolated in the convert
 
 // NCB: 16-channel output blocks per wave (2: Cout 64, 1: Cout 32); MODE: H5_* bits
 template <int NCB, int MODE>
 __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Args h) {
   constexpr bool AFF = (MODE & H5_AFF) != 0, GATE = (MODE & H5_GATE) != 0;
   constexpr bool TRAIN = (MODE & H5_TRAIN) != 0, EPBN = (MODE & H5_EPBN) != 0, ACC = (MODE & H5_ACC) != 0;
+  constexpr bool UP = (MODE & H5_UP) != 0;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     unit_pos(U, ttile, iy, x, gp, valid);
     float4 v0 = make_float4(stg[2 * SS][0], stg[2 * SS][1], stg[2 * SS][2], stg[2 * SS][3]);
     float4 v1 = make_float4(stg[2 * SS + 1][0], stg[2 * SS + 1][1], stg[2 * SS + 1][2], stg[2 * SS + 1][3]);
-    if (GATE && second) gate8(v0, v1, h, valid ? gp : -1, p.P, HW, p.c1, tch * 32 - p.c0 + c8 * 8);
+    if (GATE && second) gate8n(v0, v1, h, ttile / tps, valid ? gp : -1, p.c1, tch * 32 - p.c0 + c8 * 8);
     if constexpr (AFF) {   // fused BN + ReLU of the producer; rows outside the sample stay 0
       const float* aff = reinterpret_cast<const float*>(lds + kOffA) + tch * 32 + c8 * 8;
       const float4 s0 = *reinterpret_cast<const float4*>(aff), s1 = *reinterpret_cast<const float4*>(aff + 4);
@@ -285,6 +287,62 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
       *reinterpret_cast<half8*>(o) = hv;
       *reinterpret_cast<half8*>(o + xplane) = lv;
     }
+  };
+  // UP (the decoder's upsampled input, eval): unit U of a chunk of x0 interpolates its halo pixel from the
+  // four low-res pixels of up_src, upsample_gate_fwd_px_kernel's / conv_fwd_h4's expression; its 8 loads fill
+  // the whole staging array (one unit in flight: loaded at one tap, converted at the next)
+  const int32x4 rsu = make_rsrc(UP ? h.up_src : p.x0, UP ? (unsigned)((size_t)p.N * h.up_h * h.up_w * h.up_ld * 4) : 0u);
+  auto up_src = [&](int U, int ttile, Lerp& ly, Lerp& lx, int& b0, bool& valid) {
+    int iy, x, gp;
+    unit_pos(U, ttile, iy, x, gp, valid);
+    const int nn = ttile / tps, oy = (ttile - nn * tps) * kTR + iy - 1;
+    ly = lerp_index(valid ? oy : 0, h.up_h, p.H);
+    lx = lerp_index(x, h.up_w, kW);
+    b0 = nn * h.up_h * h.up_w;
+  };
+  auto cv_issue_up = [&](auto u_tag, int ttile, int tch) {
+    constexpr int U = decltype(u_tag)::value;
+    Lerp ly, lx;
+    int b0;
+    bool valid;
+    up_src(U, ttile, ly, lx, b0, valid);
+    const bool on = (U < 6 || (tid >> 2) + 384 < kHaloPix) && valid;
+    const int cb = tch * 32 + c8 * 8;
+    const int src[4] = {b0 + ly.i0 * h.up_w + lx.i0, b0 + ly.i0 * h.up_w + lx.i1, b0 + ly.i1 * h.up_w + lx.i0,
+                        b0 + ly.i1 * h.up_w + lx.i1};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned vo = on ? (unsigned)((src[k] * h.up_ld + cb) * 4) : OOB;
+      stg[2 * k] = h5_bload(rsu, (int)vo, 0, 0);
+      stg[2 * k + 1] = h5_bload(rsu, (int)(vo + 16u), 0, 0);
+    }
+  };
+  auto cv_process_up = [&](auto u_tag, int ttile, int tch) {
+    constexpr int U = decltype(u_tag)::value;
+    if (U == 6 && (tid >> 2) + 384 >= kHaloPix) return;   // (uniform per wave: unit 6 is wave 0's)
+    Lerp ly, lx;
+    int b0;
+    bool valid;
+    up_src(U, ttile, ly, lx, b0, valid);
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int hf = q >> 2, c = q & 3;
+      const float a = stg[hf][c], b = stg[2 + hf][c], d = stg[4 + hf][c], f = stg[6 + hf][c];
+      // ly.l0 (lx.l0 a + lx.l1 b) + ly.l1 (lx.l0 d + lx.l1 f), contracted as the compiler contracts it in
+      // upsample_gate_fwd_px_kernel and conv_fwd_h4 (each sum: fma of its first product onto the second)
+      const float t0 = __builtin_fmaf(lx.l0, a, lx.l1 * b), t1 = __builtin_fmaf(lx.l0, d, lx.l1 * f);
+      o[q] = __builtin_fmaf(ly.l0, t0, ly.l1 * t1);
+    }
+    const float4 v0 = make_float4(o[0], o[1], o[2], o[3]), v1 = make_float4(o[4], o[5], o[6], o[7]);
+    int iy, x, gp;
+    bool vv;
+    unit_pos(U, ttile, iy, x, gp, vv);
+    half8 hv, lv;
+    split2h(v0, v1, sa, hv, lv);
+    char* dst = lds + (tch & 1) * kSBUF + (iy * kPW + x + 1) * kSR + c8 * 16;
+    *reinterpret_cast<half8*>(dst) = hv;
+    *reinterpret_cast<half8*>(dst + 64) = lv;
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -441,7 +499,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
     // 0 .. 3; tap 2 converts 0, 1 and loads 4, 5; tap 3 converts 2; tap 4 converts 3 and loads 6; taps 5,
     // 6, 7 convert 4, 5, 6.  Every LDS write lands before the barrier of tap 8, after which the next chunk
     // is read.
-    if (!loader && cv_on) {
+    const bool cv_up = UP && cv_ch * 32 < p.c0;   // a chunk of the upsampled input: one unit per tap
+    if (!loader && cv_on && cv_up) {
+      if constexpr (UP) {
+        if constexpr (TT >= 1 && TT <= 7) cv_process_up(std::integral_constant<int, TT - 1>{}, cv_tile, cv_ch);
+        if constexpr (TT <= 6) cv_issue_up(std::integral_constant<int, TT>{}, cv_tile, cv_ch);
+      }
+    } else if (!loader && cv_on) {
       if constexpr (TT == 0) {
         cv_issue(I0{}, cv_tile, cv_ch); cv_issue(I1{}, cv_tile, cv_ch);
         cv_issue(I2{}, cv_tile, cv_ch); cv_issue(I3{}, cv_tile, cv_ch);
@@ -510,7 +574,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
 
   // prologue: the first tile's chunk 0 into buffer 0, the ring's first taps
   __syncthreads();   // (the staged parameters, before the first convert reads them)
-  if (!loader) {
+  if (!loader && UP) {   // (chunk 0 of an UP launch is always a chunk of the upsampled input)
+    h5_for<0, 7>([&](auto u_tag) {
+      cv_issue_up(u_tag, t_beg, 0);
+      cv_process_up(u_tag, t_beg, 0);
+    });
+  } else if (!loader) {
     cv_issue(I0{}, t_beg, 0); cv_issue(I1{}, t_beg, 0); cv_issue(I2{}, t_beg, 0); cv_issue(I3{}, t_beg, 0);
     cv_process(I0{}, t_beg, 0); cv_process(I1{}, t_beg, 0); cv_process(I2{}, t_beg, 0); cv_process(I3{}, t_beg, 0);
     cv_issue(I4{}, t_beg, 0); cv_issue(I5{}, t_beg, 0); cv_issue(I6{}, t_beg, 0);
@@ -579,7 +648,7 @@ int h5_set(int on) {
   return prev;
 }
 
-// the shapes h5 takes (forward, no upsampled input): W = 40, H a multiple of 8, Cout 64 or 32, input
+// the shapes h5 takes (forward; an upsampled input: h5_up_supported): W = 40, H a multiple of 8, Cout 64 or 32, input
 // channels a multiple of 64 (chunk pairs), the first input a multiple of 32
 bool h5_supported(int c0, int c1, int cout, int h, int w, int dil) {
   return h5_on() && w == kW && h > 0 && h % kTR == 0 && dil == 1 && (cout == 64 || cout == 32) && c0 % 32 == 0 &&
@@ -598,6 +667,14 @@ template <int NCB>
 static int launch_h5_ncb(const ConvParams& p, const H3Args& h, int grid, hipStream_t st) {
   const bool aff = h.in_scale != nullptr, gate = h.x1_ca != nullptr, epbn = p.ep_mean != nullptr;
   const bool train = p.stats != nullptr || h.xsplit != nullptr;
+  if (h.up_src != nullptr) {   // the eval decoder's dec1.conv1: upsampled x0, gated x1, BN + ReLU epilogue
+    if (!(gate && epbn && !aff && !train && !p.accumulate)) {
+      set_error("srpde_conv_fwd_h3(h5): an upsampled x0 only with a gated x1 and the eval BN epilogue");
+      return kErrArg;
+    }
+    launch_h5_variant<NCB, H5_UP | H5_GATE | H5_EPBN>(p, h, grid, st);
+    return 0;
+  }
   if (p.accumulate) {   // (not in the U-Net's forward: the plain conv only)
     if (aff || gate || train || epbn) {
       set_error("srpde_conv_fwd_h3(h5): accumulate only without in_scale / gate / statistics / ep");

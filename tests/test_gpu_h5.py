@@ -171,3 +171,50 @@ def test_conv_n16_equals_h3r(n, h):
         got = stats.double().view(ref.shape)
         assert torch.allclose(got[:, :, 0], ref[:, :, 0], rtol=1e-5, atol=1e-6)
         assert torch.allclose(got[:, :, 1], ref[:, :, 1], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [3, 300])
+def test_conv_h5_upsampled_input_equals_h4(n):
+    """The eval decoder's dec1.conv1 on h5 (x0 = the bilinear x2 upsample of d, interpolated in h5's convert,
+    one unit per tap; x1 gated; BN + ReLU epilogue) against the materialised upsample through h5 (output and
+    max word bit for bit) and against h4's upsampled-input kernel."""
+    from superresolution_for_pdes_amd import hipops as H
+    if H.conv_math() != "h3":
+        pytest.skip("h3 kernels off")
+    g = torch.Generator(device=DEV).manual_seed(31)
+    hw, hl, c0, c1, cout = 40, 20, 128, 64, 64
+    d = torch.randn(n * hl * hl, c0, device=DEV, generator=g)
+    e = torch.randn(n * hw * hw, c1, device=DEV, generator=g)
+    ca = torch.sigmoid(torch.randn(n, c1, device=DEV, generator=g))
+    w = torch.randn(cout, c0 + c1, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    wf, _ = H.pack_conv_weights(w, c0 + c1, True, False)
+    wg = torch.randn(1, c0, 1, 1, device=DEV, generator=g) * 0.1
+    bg = torch.randn(1, device=DEV, generator=g)
+    emean, einv = torch.randn(cout, device=DEV, generator=g) * 0.1, torch.rand(cout, device=DEV, generator=g) + 0.5
+    ega, ebe = torch.randn(cout, device=DEV, generator=g), torch.randn(cout, device=DEV, generator=g) * 0.1
+    d._srpde_amax = H.amax_of(d)
+    e._srpde_amax = H.amax_of(e)
+    u, sa = H.upsample_gate_fwd(d, n, hl, hl, hw, hw, wg, bg)
+    P = n * hw * hw
+    outs = []
+    prev = H.set_h5(True)
+    try:
+        for on, x0 in ((True, H.UpsampledInput(d, n, hl, hl)), (False, H.UpsampledInput(d, n, hl, hl)), (True, u)):
+            H.set_h5(on)
+            ye = torch.empty(P, cout, device=DEV)
+            eam = torch.zeros(1, dtype=torch.int32, device=DEV)
+            H.conv_fwd(x0, e, wf, b, ye, n, hw, hw, cout, 3, 1, 1, False, None, ep_bn=(emean, einv, ega, ebe, eam),
+                       x1_gate=(ca, sa))
+            torch.cuda.synchronize()
+            outs.append((ye, eam))
+    finally:
+        H.set_h5(prev)
+    # the materialised upsample through h5: bit for bit
+    assert torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1])
+    # h4's upsampled-input kernel: bit for bit where it runs whole tiles; with more tiles than CUs its last
+    # tiles are K-split (summed by conv_tail_fixup in another order), so there fp32 rounding apart
+    if n * hw * hw <= 256 * 256:
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    else:
+        torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
