@@ -176,13 +176,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
 
   // the lane's B fragment (pixel 16 j + l16 of the wave's 80, 8 channels at 16 lq) of tap (ky, kx) is
   // at halo-image row (r + ky) * 42 + x + kx, r / x the pixel's tile row / column
-  unsigned ab0[kNPB], ab1[kNPB];
+  unsigned ab0[kNPB];   // (+ kSBUF for buffer 1, added at each read: kept as registers they were spilled)
 #pragma unroll
   for (int j = 0; j < kNPB; ++j) {
     const int tp = 80 * q + 16 * j + l16;
     const int r = tp / kW, x = tp - kW * r;
     ab0[j] = (unsigned)((r * kPW + x) * kSR + lq * 16);
-    ab1[j] = ab0[j] + kSBUF;
   }
 
   // Roles: waves 4 .. 7 DMA the weights into the LDS ring, waves 0 .. 3 load and convert the halo tiles.  The
@@ -558,7 +557,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
         part[c][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[SL][c], xh[SX], c0, 0, 0, 0);
       }
       if constexpr (!(H5_DBG & 32)) {
-        const unsigned a = (B2 ? ab1[J2] : ab0[J2]) + TOFF2;
+        unsigned a = ab0[J2];
+        if constexpr (B2 != 0) {
+          asm volatile("" : "+v"(a));   // (not hoisted into a second register array)
+          a += kSBUF;
+        }
+        a += TOFF2;
         xh[G2 % 3] = *reinterpret_cast<const half8*>(lds + a);
         xl[G2 % 3] = *reinterpret_cast<const half8*>(lds + a + 64);
       }
