@@ -45,8 +45,9 @@ typedef struct ihipStream_t* hipStream_t;
  *   7  srpde_conv_fwd_h3: x0_up, up_ld, up_h, up_w before the workspace; srpde_upsample_gate_sa;
  *      srpde_conv_head_eval
  *   8  srpde_conv_h3_stats_rows_for, srpde_conv_h5_set (the h5 forward writes 80-row statistics),
- *      srpde_conv_head_eval_supported, srpde_last_kernel */
-#define SRPDE_ABI_VERSION 8
+ *      srpde_conv_head_eval_supported, srpde_last_kernel
+ *   9  srpde_conv_wgrad_h3x, srpde_conv_wgrad_h3x_supported */
+#define SRPDE_ABI_VERSION 9
 
 const char* srpde_last_error(void);
 /* Name of the main kernel the last conv entry point (srpde_conv_fwd*, srpde_conv_dgrad_h3_bnb, srpde_conv_wgrad*,
@@ -197,6 +198,18 @@ size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int ci
 int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* xp, int c0, const unsigned* amax0,
                          int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
                          int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* srpde_conv_wgrad_h3p for the 40 x 40 layers (cout <= 64, c0 and c1 multiples of 32: shapes for which
+ * srpde_conv_wgrad_h3x_supported returns 1) with the input read from its fp32 rows instead of a stored split,
+ * so the forward need not write xsplit_out: in_scale / in_shift and x1_ca / x1_sa (nullable, in pairs) repeat
+ * the forward call's input transform and amax0 / amax1 are that call's words -- the operand is bit for bit
+ * the split the forward would have stored, and dw equals srpde_conv_wgrad_h3p's on it.  Workspace:
+ * srpde_conv_wgrad_h3p_workspace_size. */
+int srpde_conv_wgrad_h3x_supported(int c0, int c1, int cout, int w, int dil);
+int srpde_conv_wgrad_h3x(const void* dyp, const unsigned* amax_dy, const float* x0, int ldx0, int c0,
+                         const unsigned* amax0, const float* in_scale, const float* in_shift, const float* x1, int ldx1,
+                         int c1, const unsigned* amax1, const float* x1_ca, const float* x1_sa, float* dw, int cin_real,
+                         int accumulate, int n, int h, int w, int cout, int ksize, int dil, void* workspace,
+                         size_t ws_bytes, hipStream_t stream);
 
 /* ---- BatchNorm2d + ReLU -------------------------------------------------------------
  * replaces aten::native_batch_norm / native_batch_norm_backward and relu /

@@ -1057,6 +1057,13 @@ struct H3P {
   const unsigned* ady;     // max|dY| word (the dgrad split's scale)
   const unsigned* ax0;     // max|x0|, max|x1| words (the forward split's scale)
   const unsigned* ax1;
+  // h3h with the fp32 input (srpde_conv_wgrad_h3x): the forward's input transform, repeated where the
+  // input rows are staged -- the producing BatchNorm + ReLU of x0 (in_scale / in_shift) and the
+  // AttentionGate of x1 (x1_ca [N][c1], x1_sa [P]); null: none
+  const float* in_scale;
+  const float* in_shift;
+  const float* x1_ca;
+  const float* x1_sa;
 };
 
 // byte offsets (relative to an image base) of the two transposed 4-row reads that give lane
@@ -1069,6 +1076,9 @@ __device__ __forceinline__ int2 tr_offsets(int col0, int lane) {
 }
 // the fragment at LDS byte pointers p0 / p1 (a tr_offsets pair added to an image base; compile-time
 // parts of the base fold into the instructions' offset fields)
+// compiler-visible raw buffer loads (the compiler counts them in its own waits; offsets past the buffer read 0)
+__device__ floatx4 h3x_bload4(int32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ float h3x_bload1(int32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
 typedef __attribute__((address_space(3))) char lds_char;
 __device__ __forceinline__ half8 tr_read(const lds_char* p0, const lds_char* p1) {
   typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -1321,20 +1331,30 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv_wgrad_h3p_kernel(WgradPa
 // off(t) = dy * W + dx.  Input rows a tap must not see (it leaves the image: padding, row and image
 // wrap) are read from a zero row instead, per lane: each lane addresses one pixel row of the
 // transposed read.  Nine waves, one per tap, each a BM x 32 tile.  ~0.11 pieces per MFMA.
-template <int BM, int PS, int NST, int CAP>
-__global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H3P q, int cc_n) {
+//
+// XF (srpde_conv_wgrad_h3x): the input rows come from the fp32 activations instead of a stored split,
+// so the training forward writes no split planes (4 B per input element).  Two more waves (loaders)
+// stage them: each stage's rows are loaded into registers two stages ahead, put through the forward's
+// input transform (fused BN + ReLU of x0, attention gate of x1) and split with the forward's scale, and
+// written into the ring one stage ahead, before that stage's barrier -- the ring then holds exactly the
+// bits the forward's stored split held.  The loaders issue no LDS-DMA, so the compiler's own waits
+// count their loads; the MFMA waves DMA only the dY pieces.
+template <int BM, int PS, int NST, int CAP, int XF>
+__global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H3P q, int cc_n) {
   constexpr int NW = 9, TI = BM / 32;
   constexpr int RA = BM * 2;                   // A image row bytes (one plane)
   constexpr int IMG_A = PS * RA;               // one plane of one stage
   constexpr int NA = 2 * IMG_A / 1024;         // A pieces per stage
   constexpr int NBP = PS / 16;                 // B pieces per plane per stage (16 rows x 64 B)
-  constexpr int NB = 2 * NBP;
+  constexpr int NB = XF ? 0 : 2 * NBP;
   constexpr int TOT = NA + NB;                 // pieces per stage
   constexpr int DLO = TOT / NW, NHI = TOT % NW;   // waves < NHI issue DLO + 1 pieces per stage
   constexpr int RING = (CAP + 1) * 64;         // one plane of the input ring + its zero row
   static_assert(IMG_A % 1024 == 0 && PS % 16 == 0 && (NST == 3 || NST == 4), "stage geometry");
   static_assert((CAP & (CAP - 1)) == 0 && CAP >= 64, "ring rows: a power of two");
   static_assert((NST - 2) * (DLO + 1) <= 63, "vmcnt range");
+  static_assert(!XF || PS == 64, "XF: two loader waves stage 64 rows x 8 channel quads");
+  static_assert(XF >= 0 && XF <= 2, "XF: 0 stored split, 1 fp32 input, 2 fp32 input with the gate's loads");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char* lds = reinterpret_cast<char*>(smem);
   char* const abuf = lds;                              // [NST][2][PS][RA]
@@ -1392,8 +1412,115 @@ __global__ __launch_bounds__(576, 1) void conv_wgrad_h3h_kernel(WgradParams p, H
       }
     }
   };
+  if constexpr (XF) {
+    if (wave >= NW) {   // the loader waves: 64 rows x 8 channel quads per stage, 4 rows per lane
+      typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+      const int lt = tid - NW * 64, qd = lt & 7, rw = lt >> 3;
+      const bool second = c0 >= p.c0;
+      const float* __restrict__ xs = second ? p.x1 : p.x0;
+      const int ld = second ? p.ldx1 : p.ldx0;
+      const int cb = (second ? c0 - p.c0 : c0) + 4 * qd;
+      const bool aff = !second && q.in_scale != nullptr;
+      const bool gate = XF == 2 && second && q.x1_ca != nullptr;
+      float4 as = make_float4(1.f, 1.f, 1.f, 1.f), at = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (aff) {
+        as = *reinterpret_cast<const float4*>(q.in_scale + cb);
+        at = *reinterpret_cast<const float4*>(q.in_shift + cb);
+      }
+      unsigned xw = *q.ax0;
+      if (p.c1) xw = max(xw, *q.ax1);
+      const float sc = exp2i(h3_exp(xw));
+      const int HW = p.H * p.W;
+      // buffer loads: a row outside the tensor reads zeros at an out-of-range offset instead of branching, so
+      // every stage issues the same loads and the compiler's waits count them exactly (a branch around a load
+      // made them all vmcnt(0)); the gate's loads read zeros from an empty buffer where there is no gate
+      const int32x4 rsx = make_rsrc(xs, (unsigned)((size_t)p.P * ld * 4));
+      const int32x4 rsg = make_rsrc(q.x1_ca, gate ? (unsigned)((size_t)p.N * p.c1 * 4) : 0u);
+      const int32x4 rss = make_rsrc(q.x1_sa, gate ? (unsigned)((size_t)p.P * 4) : 0u);
+      struct Rows { floatx4 v[4], g[4]; float s[4]; };
+      auto load = [&](int R, Rows& b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = R + rw + 16 * j;
+          const bool in = r >= 0 && r < p.P;
+          b.v[j] = h3x_bload4(rsx, in ? (int)(((unsigned)r * ld + cb) * 4u) : (int)OOB, 0, 0);
+          if constexpr (XF == 2) {   // the gate-capable variant (dec1.conv1)
+            b.g[j] = h3x_bload4(rsg, in ? (int)(((unsigned)(r / HW) * p.c1 + cb) * 4u) : (int)OOB, 0, 0);
+            b.s[j] = h3x_bload1(rss, in ? r * 4 : (int)OOB, 0, 0);
+          }
+        }
+      };
+      // the forward's transform (conv_h5.hip cv_process / gate8n) and split (split2h) of rows < rend
+      auto put = [&](int R, const Rows& b, int rend) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = R + rw + 16 * j;
+          if (r >= rend) continue;
+          float v[4] = {b.v[j][0], b.v[j][1], b.v[j][2], b.v[j][3]};
+          if (r >= 0 && r < p.P) {
+            if (aff) {
+              v[0] = fmaxf(v[0] * as.x + at.x, 0.f); v[1] = fmaxf(v[1] * as.y + at.y, 0.f);
+              v[2] = fmaxf(v[2] * as.z + at.z, 0.f); v[3] = fmaxf(v[3] * as.w + at.w, 0.f);
+            }
+            if (gate) {
+              const float s = b.s[j];
+              v[0] = (v[0] * b.g[j][0]) * s; v[1] = (v[1] * b.g[j][1]) * s;
+              v[2] = (v[2] * b.g[j][2]) * s; v[3] = (v[3] * b.g[j][3]) * s;
+            }
+          }
+          half4 hi, lo;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float xv = v[k] * sc;
+            const _Float16 hv = (_Float16)xv;
+            hi[k] = hv;
+            lo[k] = (_Float16)(xv - (float)hv);
+          }
+          char* d = bring + (r & (CAP - 1)) * 64 + qd * 8;
+          *reinterpret_cast<half4*>(d) = hi;
+          *reinterpret_cast<half4*>(d + RING) = lo;
+        }
+      };
+      Rows b0, b1, b2;
+      // the rows every stage assumes resident and stage 0's: three groups in flight at once where they fit
+      if (rbase + PS - rlo <= 3 * 64) {
+        load(rlo, b0);
+        load(rlo + 64, b1);
+        load(rlo + 128, b2);
+        put(rlo, b0, rbase + PS);
+        put(rlo + 64, b1, rbase + PS);
+        put(rlo + 128, b2, rbase + PS);
+      } else {
+        for (int R = rlo; R < rbase; R += 64) {
+          load(R, b0);
+          put(R, b0, rbase);
+        }
+        load(rbase, b0);
+        put(rbase, b0, 0x7fffffff);
+      }
+      load(rbase + PS, b1);
+      load(rbase + 2 * PS, b2);
+      // stage s (after its barrier): stage s + 3's loads into the set stage s's rows left, then stage
+      // s + 1's rows (loaded two stages ago) into the ring.  Unconditional: past the chunk they load rows
+      // nobody reads (or zeros) into ring rows ahead of every stage's reach
+      auto step = [&](int s, Rows& tgt, const Rows& src) {
+        __syncthreads();
+        load(rbase + (s + 3) * PS, tgt);
+        put(rbase + (s + 1) * PS, src, 0x7fffffff);
+      };
+      int s = 0;
+      for (; s + 3 <= nsteps; s += 3) {
+        step(s, b0, b1);
+        step(s + 1, b1, b2);
+        step(s + 2, b2, b0);
+      }
+      if (s < nsteps) step(s, b0, b1);
+      if (s + 1 < nsteps) step(s + 1, b1, b2);
+      return;
+    }
+  }
   // prologue: the input rows [rlo, rbase) every later stage assumes resident
-  {
+  if constexpr (!XF) {
     const int ng = (rbase - rlo) >> 4;
     for (int v = wave; v < 2 * ng; v += NW) bpiece(rlo + 16 * (v >> 1), v & 1);
   }
@@ -1869,19 +1996,20 @@ static bool h3h_ok(int cout, int K, int cin, int w, int dil) {
   return h3p_use288(cout, K) && K == 9 * cin && cin % 32 == 0 && 2 * (w + 1) * dil + 15 + 3 * H3H_PS <= H3H_CAP;
 }
 
-template <int BM, int PS, int NST, int CAP>
+template <int BM, int PS, int NST, int CAP, int XF>
 static int launch_h3h_cfg(const WgradParams& p, const H3P& q, hipStream_t st) {
   const int cc_n = p.Cin / 32;
   const int nb = ceil_div(p.Cout, BM) * cc_n * p.splits;
   const size_t lds = (size_t)NST * 2 * PS * BM * 2 + (size_t)2 * (CAP + 1) * 64;
-  note_kernel("conv_wgrad_h3h_kernel<%d, %d, %d, %d>", BM, PS, NST, CAP);
-  hipLaunchKernelGGL((conv_wgrad_h3h_kernel<BM, PS, NST, CAP>), dim3(nb), dim3(576), lds, st, p, q, cc_n);
-  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p(h3h)");
+  note_kernel("conv_wgrad_h3h_kernel<%d, %d, %d, %d, %d>", BM, PS, NST, CAP, XF);
+  hipLaunchKernelGGL((conv_wgrad_h3h_kernel<BM, PS, NST, CAP, XF>), dim3(nb), dim3(XF ? 704 : 576), lds, st, p, q,
+                     cc_n);
+  SRPDE_LAUNCH_CHECK(XF ? "srpde_conv_wgrad_h3x" : "srpde_conv_wgrad_h3p(h3h)");
   return 0;
 }
-template <int BM>
+template <int BM, int XF = 0>
 static int launch_h3h(const WgradParams& p, const H3P& q, hipStream_t st) {
-  return launch_h3h_cfg<BM, H3H_PS, 3, H3H_CAP>(p, q, st);
+  return launch_h3h_cfg<BM, H3H_PS, 3, H3H_CAP, XF>(p, q, st);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1938,6 +2066,52 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   else if (h3h_ok(cout, p.K, p.Cin, w, dil)) rc = cout >= 64 ? launch_h3h<64>(p, q, stream) : launch_h3h<32>(p, q, stream);
   else if (cout >= 64) rc = h3p_use288(cout, p.K) ? launch_h3p<64, 288, 1, 9>(p, q, stream) : launch_h3p<64, 256, 1, 8>(p, q, stream);
   else rc = h3p_use288(cout, p.K) ? launch_h3p<32, 288, 1, 9>(p, q, stream) : launch_h3p<32, 256, 1, 8>(p, q, stream);
+  if (rc) return rc;
+  return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
+}
+
+int srpde_conv_wgrad_h3x_supported(int c0, int c1, int cout, int w, int dil) {
+  const int cin = c0 + c1;
+  return cout > 0 && cout <= 64 && cout % 16 == 0 && c0 > 0 && c0 % 32 == 0 && c1 % 32 == 0 && dil > 0 &&
+         h3h_ok(cout, 9 * cin, cin, w, dil);
+}
+
+int srpde_conv_wgrad_h3x(const void* dyp, const unsigned* amax_dy, const float* x0, int ldx0, int c0,
+                         const unsigned* amax0, const float* in_scale, const float* in_shift, const float* x1, int ldx1,
+                         int c1, const unsigned* amax1, const float* x1_ca, const float* x1_sa, float* dw, int cin_real,
+                         int accumulate, int n, int h, int w, int cout, int ksize, int dil, void* workspace,
+                         size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dyp && amax_dy && x0 && amax0 && dw && workspace && (c1 == 0 || (x1 && amax1)),
+                  "srpde_conv_wgrad_h3x: null pointer");
+  SRPDE_CHECK_ARG(ksize == 3 && srpde_conv_wgrad_h3x_supported(c0, c1, cout, w, dil) && cin_real <= c0 + c1,
+                  "srpde_conv_wgrad_h3x: shape not supported (cout=%d c0=%d c1=%d w=%d dil=%d)", cout, c0, c1, w, dil);
+  SRPDE_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr) && (x1_ca == nullptr) == (x1_sa == nullptr) &&
+                      (x1_ca == nullptr || c1 > 0),
+                  "srpde_conv_wgrad_h3x: in_scale / in_shift and x1_ca / x1_sa go together (a gate needs x1)");
+  SRPDE_CHECK_ARG(aligned16(dyp) && aligned16(x0) && ldx0 % 4 == 0 && ldx0 >= c0 &&
+                      (c1 == 0 || (aligned16(x1) && ldx1 % 4 == 0 && ldx1 >= c1)) &&
+                      (in_scale == nullptr || (aligned16(in_scale) && aligned16(in_shift))) &&
+                      (x1_ca == nullptr || aligned16(x1_ca)),
+                  "srpde_conv_wgrad_h3x: 16-byte aligned operands, row strides multiples of 4");
+  WgradParams p;
+  p.dy = nullptr; p.lddy = (cout + 31) / 32 * 32; p.x0 = x0; p.c0 = c0; p.ldx0 = ldx0; p.x1 = x1; p.c1 = c1;
+  p.ldx1 = ldx1;
+  p.N = n; p.H = h; p.W = w; p.Cout = cout; p.ksize = ksize; p.dil = dil;
+  p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
+  SRPDE_CHECK_ARG(2LL * p.P * p.lddy * 2 < (1LL << 31) && (long long)p.P * std::max(ldx0, ldx1) < (1LL << 31),
+                  "srpde_conv_wgrad_h3x: tensor too large");
+  h3p_split(p.P, cout, p.K, &p.chunk, &p.splits);
+  const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
+  if (ws_bytes < need) {
+    set_error("srpde_conv_wgrad_h3x: workspace %zu < %zu bytes", ws_bytes, need);
+    return kErrWorkspace;
+  }
+  p.part = static_cast<float*>(workspace);
+  const H3P q{static_cast<const _Float16*>(dyp), nullptr, amax_dy, amax0, c1 ? amax1 : amax0, in_scale, in_shift,
+              x1_ca, x1_sa};
+  int rc;
+  if (x1_ca != nullptr) rc = cout > 32 ? launch_h3h<64, 2>(p, q, stream) : launch_h3h<32, 2>(p, q, stream);
+  else rc = cout > 32 ? launch_h3h<64, 1>(p, q, stream) : launch_h3h<32, 1>(p, q, stream);
   if (rc) return rc;
   return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
 }

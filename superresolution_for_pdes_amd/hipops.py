@@ -461,10 +461,40 @@ def split_planes_buffer(P, c, device):
     return torch.empty(2, P, c, dtype=torch.float16, device=device)
 
 
+class XSource:
+    """The input of a forward whose split the weight gradient forms itself (srpde_conv_wgrad_h3x) instead
+    of reading stored planes: what that forward read -- x0, x1, its fused input BN (``in_affine``), the
+    attention gate of x1 (``x1_gate``) -- and its max|.| words.  Stands where the stored split ``xp``
+    would (conv_wgrad_h3p takes either)."""
+
+    def __init__(self, x0, x1, in_affine, x1_gate):
+        self.x0, self.x1, self.in_affine, self.x1_gate = x0, x1, in_affine, x1_gate
+        self.a0 = amax_of(x0)
+        self.a1 = amax_of(x1) if x1 is not None else None
+        for t, a in ((x0, self.a0), (x1, self.a1)):   # the forward then reads the same words
+            if t is not None and getattr(t, "_srpde_amax", None) is None:
+                t._srpde_amax = a
+
+    def tensors(self):
+        """everything the launch reads (kept alive on the weight-gradient stream)"""
+        out = [self.x0, self.x1, self.a0, self.a1]
+        for t in (self.in_affine or ()) + (self.x1_gate or ()):
+            out.append(t)
+        return [t for t in out if t is not None]
+
+
+def wgrad_x_capable(c0, c1, cout, w, dil):
+    """srpde_conv_wgrad_h3x takes this layer (the 40 x 40 layers' h3h weight gradient)"""
+    return bool(query("srpde_conv_wgrad_h3x_supported", c0, c1, cout, w, dil))
+
+
 def conv_wgrad_h3p(dyp, xp, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     """Weight gradient from the stored splits: ``dyp`` from the dgrad conv_fwd(planes_out=...) or
     bn_bwd_apply_split (its channels padded to 32: out_conv2's 16), ``xp`` from the forward
-    conv_fwd(planes_out=...), each carrying its max|.| word(s); ``dw`` [Cout, Cin, k, k]."""
+    conv_fwd(planes_out=...), each carrying its max|.| word(s); ``dw`` [Cout, Cin, k, k].
+    ``xp`` may be an XSource: the kernel splits the fp32 input rows itself (srpde_conv_wgrad_h3x)."""
+    if isinstance(xp, XSource):
+        return _conv_wgrad_h3x(dyp, xp, dw, n, h, w, ksize, dil, accumulate)
     cout, cin = dw.shape[0], xp.shape[2]
     assert dyp.shape[2] == cpad32(cout), "dy planes must hold cout rounded up to 32 channels"
     ax = xp._srpde_amax
@@ -476,6 +506,23 @@ def conv_wgrad_h3p(dyp, xp, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     _conv_call("srpde_conv_wgrad_h3p", 2.0 * cout * dw.shape[1] * ksize * ksize * n * h * w, dyp.data_ptr(), dyp._srpde_amax.data_ptr(), xp.data_ptr(), c0, a0.data_ptr(), c1,
          _p(a1), dw.data_ptr(), dw.shape[1], int(accumulate), n, h, w, cout, ksize, dil, ws.data_ptr(), ws_bytes,
          stream_ptr())
+
+
+def _conv_wgrad_h3x(dyp, xs, dw, n, h, w, ksize, dil, accumulate):
+    cout = dw.shape[0]
+    assert dyp.shape[2] == cpad32(cout), "dy planes must hold cout rounded up to 32 channels"
+    x0, x1 = xs.x0, xs.x1
+    c0, c1 = x0.shape[1], (x1.shape[1] if x1 is not None else 0)
+    p0, ld0 = _pl(x0)
+    p1, ld1 = _pl(x1) if x1 is not None else (0, 0)
+    aff, gate = xs.in_affine, xs.x1_gate
+    ws_bytes = int(query("srpde_conv_wgrad_h3p_workspace_size", n, h, w, cout, c0 + c1, ksize))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dyp.device)
+    _conv_call("srpde_conv_wgrad_h3x", 2.0 * cout * dw.shape[1] * ksize * ksize * n * h * w, dyp.data_ptr(),
+               dyp._srpde_amax.data_ptr(), p0, ld0, c0, xs.a0.data_ptr(), _p(aff[0] if aff else None),
+               _p(aff[1] if aff else None), p1, ld1, c1, _p(xs.a1), _p(gate[0] if gate else None),
+               _p(gate[1] if gate else None), dw.data_ptr(), dw.shape[1], int(accumulate), n, h, w, cout, ksize, dil,
+               ws.data_ptr(), ws_bytes, stream_ptr())
 
 
 # ---------------------------------- batch norm -------------------------------------

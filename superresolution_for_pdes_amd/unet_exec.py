@@ -273,10 +273,14 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     if training:
         stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev, x0.shape[1], c1, dil)
         if _splits_both_ways(x0.shape[1], c1, cout, w, dil):
-            xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
+            if _WGRAD_X and x0.is_cuda and H.wgrad_x_capable(x0.shape[1], c1, cout, w, dil):
+                # the weight gradient splits the fp32 input itself (srpde_conv_wgrad_h3x): nothing stored
+                xp = H.XSource(x0, x1, in_affine, x1_gate)
+            else:
+                xp = H.split_planes_buffer(P, cin, dev)   # the input's split, kept for the weight gradient
         assert in_affine is None or xp is not None, "a fused input needs the stored split for its wgrad"
-        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats, xp, in_affine,
-                     x1_gate=x1_gate)
+        _conv_launch(conv, x0, x1, wf, conv.bias, y, n, h, w, cout, 3, dil, 1, False, stats,
+                     None if isinstance(xp, H.XSource) else xp, in_affine, x1_gate=x1_gate)
         mom = bn.momentum if bn.momentum is not None else 0.0
         _buffers_ready(dev)
         _RS_EPOCH[0] += 1   # the finalize below rewrites the running statistics torch's version counters miss
@@ -488,6 +492,11 @@ def _priority_stream(dev):
     return st
 
 
+def _xkeep(xp):
+    """what an XSource's weight-gradient launch reads (stream-kept like its other operands)"""
+    return tuple(xp.tensors()) if isinstance(xp, H.XSource) else ()
+
+
 def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumulate=False, part=None,
              below=None, wq=None):
     """dgrad first: its h3 kernel stores dy's split, which the weight gradient then reads together
@@ -527,7 +536,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         H.conv_dgrad_bnb(da, y, mean, invstd, bn.weight, bn.bias, m1, m2, dyw, wd, dx, n, h, w, cout, cin, dil, dyp,
                          bn_bwd=bn_bwd, dx_max=dx_max)
         _tap_dgrad(conv, dyp, dx, dx_max, out_part)
-        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw) + _xkeep(xp)
         if wq is None:
             fn()
         else:
@@ -554,7 +563,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         H.conv_fwd_presplit(dyp, wd, None, dx, n, h, w, cin, 3, dil, -1, dx_accumulate, None, bn_bwd=bn_bwd,
                             out_max=dx_max)
         _tap_dgrad(conv, dyp, dx, dx_max, out_part)
-        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, grads[conv.weight], n, h, w, 3, dil)), (dyp, dyw) + _xkeep(xp)
         if wq is None:
             fn()
         else:
@@ -583,7 +592,7 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         _tap_dgrad(conv, dyp, dx, dx_max, out_part)
     dw = grads[conv.weight]
     if xp is not None and dyp is not None:
-        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax)
+        fn, keep = (lambda: H.conv_wgrad_h3p(dyp, xp, dw, n, h, w, 3, dil)), (dyp, dyp._srpde_amax) + _xkeep(xp)
     else:
         assert x0 is not None, "fused-input layer without stored splits"
         if isinstance(x1, GatedInput):
@@ -611,6 +620,10 @@ _BNB_MAX_CIN, _BNB_MIN_COUT = 64, 64
 # the BN backward apply writes dy as its h3 split for a presplit dgrad (SRPDE_PRESPLIT_BWD=0: fp32 dy,
 # split inside the dgrad)
 _PRESPLIT_BWD = os.environ.get("SRPDE_PRESPLIT_BWD", "1") != "0"
+
+# the 40 x 40 layers' weight gradients split their fp32 input rows themselves (srpde_conv_wgrad_h3x), so
+# their training forwards store no input split (SRPDE_WGRAD_X=0: the forward stores it, h3h reads it)
+_WGRAD_X = os.environ.get("SRPDE_WGRAD_X", "1") != "0"
 
 # the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
 _FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"

@@ -326,7 +326,7 @@ def test_fused_bn_apply_matches_separate_pass():
 
 
 SWITCHES = ("_FUSE_D1", "_FIN_AFFINE", "_FUSE_SA", "_FUSE_ATT_CH", "_FUSE_POOL", "_H3W_SIDE", "_FUSE_BN_BWD",
-            "_FUSE_BN_APPLY", "_WGRAD_STREAM", "_PRESPLIT_BWD", "_FUSE_ATT_APPLY")
+            "_FUSE_BN_APPLY", "_WGRAD_STREAM", "_PRESPLIT_BWD", "_FUSE_ATT_APPLY", "_WGRAD_X")
 
 
 @pytest.mark.parametrize("off", [SWITCHES] + [(s,) for s in SWITCHES])
