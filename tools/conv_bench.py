@@ -75,18 +75,24 @@ def main():
         # (bn_bwd_apply_split's output, 32-channel padded for out_conv2) and the wgrad reads both
         cp = H.cpad32(cout)
         h3p = H.conv_math() == "h3" and H.h3_capable(c0, c1, cout, hw, dil) and H.h3_capable(cp, 0, cin, hw, dil)
+        # the 40 x 40 layers as training runs them: no stored input split, the weight gradient splits the
+        # fp32 rows itself (srpde_conv_wgrad_h3x; unet_exec._WGRAD_X)
+        wx = h3p and H.wgrad_x_capable(c0, c1, cout, hw, dil)
         xp = H.split_planes_buffer(P, cin, dev) if h3p else None
         dyp = H.split_planes_buffer(P, cp, dev) if h3p else None
+        xfwd = None if wx else xp
         if h3p:
             dyin = dy if cp == cout else torch.cat([dy, torch.zeros(P, cp - cout, device=dev)], 1)
             dyin._srpde_amax = dy._srpde_amax
             H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp)
             H.conv_fwd(dyin, None, wd, None, dx, n, hw, hw, cin, 3, dil, -1, False, None, dyp)
             seq.extend([(name, "setup"), (name, "setup")])
+            if wx:
+                xp = H.XSource(x0, x1, None, None)
         for kind in args.only.split(","):
             tag = (name, kind)
             if kind == "fwd":
-                ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xp),
+                ms = timeit(lambda: H.conv_fwd(x0, x1, wf, b, y, n, hw, hw, cout, 3, dil, 1, False, stats, xfwd),
                             args.iters, seq, tag)
             elif kind == "dgrad" and h3p:
                 ms = timeit(lambda: H.conv_fwd_presplit(dyp, wd, None, dx, n, hw, hw, cin, 3, dil, -1), args.iters,
@@ -100,17 +106,17 @@ def main():
                 ms = timeit(lambda: H.conv_wgrad(dy, x0, x1, dw, n, hw, hw, 3, dil), args.iters, seq, tag)
             tf = flops / ms / 1e9
             # algorithmic HBM bytes of one call (fp32 4 B/elem; stored h3 splits 2x2 B/elem):
-            # fwd x + w + y (+ the input split it stores); dgrad dy + w + dx (+ dy's split);
-            # wgrad: both stored splits (else both fp32 operands) + dw
+            # fwd x + w + y (+ the input split it stores, not at the 40 x 40 layers); dgrad dy + w + dx
+            # (+ dy's split); wgrad: both operands (stored splits or fp32: 4 B/elem either way) + dw
             wb = 4 * cout * cin * 9
             if kind == "fwd":
-                ab = 4 * P * cin + wb + 4 * P * cout + (4 * P * cin if h3p else 0)
+                ab = 4 * P * cin + wb + 4 * P * cout + (4 * P * cin if h3p and not wx else 0)
             elif kind == "dgrad":   # h3: dy arrives as its stored split (4 B/elem), nothing else stored
                 ab = 4 * P * cout + wb + 4 * P * cin
             else:
                 ab = 4 * P * (cin + cout) + wb
             rows.append({"layer": name, "pass": kind, "ms": round(ms, 4), "tflops": round(tf, 1), "flop": flops,
-                         "algorithmic_bytes": ab, "h3p": h3p})
+                         "algorithmic_bytes": ab, "h3p": h3p, "wgrad_x": wx})
             t = tot.setdefault(kind, [0.0, 0.0])
             t[0] += flops
             t[1] += ms
