@@ -1104,6 +1104,9 @@ __device__ __forceinline__ void h3_for(F&& f) {   // f(integral_constant<B>), ..
 // barrier, 2 = no DMA in the stage loop (with the DMA, bridge.3's weight gradient took 1.39 ms, without it
 // 1.07 ms; issued right after the stage barrier, a stage's 48 DMA wave-instructions held up its first
 // MFMAs: spread over the stage's MFMA groups 1.26 ms, tools/gpu/wgrad_variants.sh)
+#ifndef H3H_DBG
+#define H3H_DBG 0
+#endif
 #ifndef H3P_DBG
 #define H3P_DBG 0
 #endif
@@ -1592,6 +1595,12 @@ __global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(Wgrad
         al[i] = tr_read(sa + IMG_A + oa[i].x + kk * 16 * RA, sa + IMG_A + oa[i].y + kk * 16 * RA);
       }
     };
+    // H3H_DBG & 1 (timing diagnostic, wrong results): the last tap's wave does no fragment reads or MFMAs,
+    // leaving eight MFMA waves, two per SIMD
+    if ((H3H_DBG & 1) && wave == NW - 1) {
+      issue(s + NST - 1, (SLOT + NST - 1) % NST);
+      return;
+    }
     half8 bh[2], bl[2], ah[2][TI], al[2][TI];
     bfrag(0, bh[0], bl[0]);
     afrag(0, ah[0], al[0]);
