@@ -1595,12 +1595,9 @@ __global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(Wgrad
         al[i] = tr_read(sa + IMG_A + oa[i].x + kk * 16 * RA, sa + IMG_A + oa[i].y + kk * 16 * RA);
       }
     };
-    // H3H_DBG & 1 (timing diagnostic, wrong results): the last tap's wave does no fragment reads or MFMAs,
-    // leaving eight MFMA waves, two per SIMD
-    if ((H3H_DBG & 1) && wave == NW - 1) {
-      issue(s + NST - 1, (SLOT + NST - 1) % NST);
-      return;
-    }
+    // H3H_DBG & 1 (timing diagnostic, wrong results): the last tap's wave issues no MFMAs, leaving eight
+    // MFMA waves, two per SIMD
+    const bool mskip = (H3H_DBG & 1) && wave == NW - 1;
     half8 bh[2], bl[2], ah[2][TI], al[2][TI];
     bfrag(0, bh[0], bl[0]);
     afrag(0, ah[0], al[0]);
@@ -1612,7 +1609,7 @@ __global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(Wgrad
         afrag(kk + 1, ah[cur ^ 1], al[cur ^ 1]);
       }
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
+      for (int i = 0; i < TI && !mskip; ++i) {
         floatx16 c0v;
         if (FRESH && kk == 0)
           c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cur][i], bh[cur], floatx16{}, 0, 0, 0);   // small terms first
