@@ -65,6 +65,24 @@ def test_argument_errors_are_reported(lib):
         lib.call("srpde_bn_relu_fwd", 0, 4, 0, 0, 0, 0, 0, 4, 16, 4, 1, 0, 0)
 
 
+def test_wgrad_h3x_shape_query_and_argument_checks(lib):
+    """srpde_conv_wgrad_h3x (ABI 9): the shapes it takes are the 40 x 40 layers' (Cout <= 64, both inputs
+    in whole 32-channel chunks, a ring that holds a stage's reach); bad arguments fail before any launch."""
+    q = lib.query
+    for c0, c1, cout in ((64, 0, 64), (128, 64, 64), (64, 0, 32), (32, 0, 16)):   # enc1.conv2 .. out_conv2
+        assert q("srpde_conv_wgrad_h3x_supported", c0, c1, cout, 40, 1) == 1
+    assert q("srpde_conv_wgrad_h3x_supported", 128, 0, 128, 20, 1) == 0   # Cout 128: h3p's tiles
+    assert q("srpde_conv_wgrad_h3x_supported", 48, 16, 64, 40, 1) == 0    # a chunk would straddle x0 / x1
+    assert q("srpde_conv_wgrad_h3x_supported", 64, 0, 64, 200, 1) == 0    # the ring cannot hold the reach
+    assert q("srpde_conv_wgrad_h3x_supported", 64, 0, 24, 40, 1) == 0     # Cout not a multiple of 16
+    cd = lib.lib()
+    rc = cd.srpde_conv_wgrad_h3x(0, 0, 0, 64, 64, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 0, 2, 40, 40, 64, 3, 1, 0, 0, 0)
+    assert rc < 0 and "null" in lib.last_error()
+    with pytest.raises(RuntimeError, match="srpde_conv_wgrad_h3x"):   # gate without x1
+        lib.call("srpde_conv_wgrad_h3x", 16, 16, 16, 64, 64, 16, 0, 0, 0, 0, 0, 0, 16, 16, 16, 64, 0, 2, 40, 40, 64,
+                 3, 1, 16, 1 << 20, 0)
+
+
 def test_product_path_never_imports_oracle():
     pkg = os.path.join(ROOT, "superresolution_for_pdes_amd")
     for dirpath, _, files in os.walk(pkg):
