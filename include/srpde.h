@@ -46,7 +46,8 @@ typedef struct ihipStream_t* hipStream_t;
  *      srpde_conv_head_eval
  *   8  srpde_conv_h3_stats_rows_for, srpde_conv_h5_set (the h5 forward writes 80-row statistics),
  *      srpde_conv_head_eval_supported, srpde_last_kernel
- *   9  srpde_conv_wgrad_h3x, srpde_conv_wgrad_h3x_supported */
+ *   9  srpde_conv_wgrad_h3x, srpde_conv_wgrad_h3x_supported, srpde_bn_train_finalize_ws,
+ *      srpde_bn_finalize_workspace_size */
 #define SRPDE_ABI_VERSION 9
 
 const char* srpde_last_error(void);
@@ -225,6 +226,17 @@ int srpde_bn_train_finalize_affine(const float* stats, int nblk, int rows_per_bl
                                    float momentum, float eps, float* mean_out, float* invstd_out, const float* gamma,
                                    const float* beta, float* scale, float* shift, unsigned* amax_bound,
                                    hipStream_t stream);
+/* Either of the two above in two coalesced passes through a workspace of srpde_bn_finalize_workspace_size(nblk, C)
+ * bytes (row slices of 16-channel groups, then one thread per channel over the slices): a 40 x 40 layer's
+ * 20,480 partials per channel take a few microseconds instead of ~36.  gamma / beta / scale / shift /
+ * amax_bound nullable (scale and shift together: the _affine outputs).  The fp64 sums run per slice, then over
+ * the slices, so mean / invstd can differ from srpde_bn_train_finalize's in the last bit of the fp64 sums. */
+size_t srpde_bn_finalize_workspace_size(int nblk, int C);
+int srpde_bn_train_finalize_ws(const float* stats, int nblk, int rows_per_blk, long long P, int C, float* running_mean,
+                               float* running_var, long long* num_batches_tracked, float momentum, float eps,
+                               float* mean_out, float* invstd_out, const float* gamma, const float* beta, float* scale,
+                               float* shift, unsigned* amax_bound, void* workspace, size_t ws_bytes,
+                               hipStream_t stream);
 int srpde_bn_eval_prepare(const float* running_mean, const float* running_var, int C, float eps, float* mean_out,
                           float* invstd_out, hipStream_t stream);
 /* amax (nullable): *amax = max(*amax, max|out|) as float bits -- the operand-scale word of the

@@ -36,6 +36,44 @@ __device__ __forceinline__ Chan chan_merge(Chan a, Chan b) {
 // num_batches_tracked (block 0), which used to be a launch of its own.
 // 1024 threads, four partials in flight per thread: the kernel is latency-bound (one block per
 // channel reads nblk strided float2), e.g. 12,800 partials per channel at the 40x40 layers.
+// channel c's batch statistics from the fp64 sums over its nfull equal-count row blocks (shift = block 0's
+// mean; s1 = sum (mean_b - shift), s2 = sum (mean_b - shift)^2, sm = sum M2_b) and the ragged last block: mean /
+// invstd, running statistics, num_batches_tracked (c == 0) and, with scale_out, the fused consumer's affine
+__device__ __forceinline__ void fin_channel(int c, const float2* __restrict__ stats, int nblk, int nfull,
+                                            int rows_per_blk, long long P, int C, double shift, double s1, double s2,
+                                            double sm, float* running_mean, float* running_var, float momentum,
+                                            float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                            long long* num_batches_tracked, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, float* __restrict__ scale_out,
+                                            float* __restrict__ shift_out, unsigned* amax, float sqrt_pm1) {
+  Chan acc{0.0, 0.0, 0.0};
+  if (nfull > 0) {
+    const double k = (double)nfull, n0 = (double)rows_per_blk;
+    const double m2 = sm + n0 * fmax(s2 - s1 * s1 / k, 0.0);
+    acc = Chan{k * n0, shift + s1 / k, m2};
+  }
+  for (int b = nfull; b < nblk; ++b) {   // the ragged last block, if any
+    const float2 v = stats[(size_t)b * C + c];
+    const long long rem = P - (long long)b * rows_per_blk;
+    const double cnt = (double)(rem < rows_per_blk ? rem : rows_per_blk);
+    acc = chan_merge(acc, Chan{cnt, (double)v.x, (double)v.y});
+  }
+  const double n = acc.n, mean = acc.mean, m2 = acc.m2;
+  const double var_b = m2 / n;
+  const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)(1.0 / sqrt(var_b + (double)eps));
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+  if (running_var) running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)var_u;
+  if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
+  if (scale_out) {   // bn_affine_kernel's outputs for this channel, from the same float mean / invstd
+    const float sc = gamma[c] * invstd_out[c];
+    scale_out[c] = sc;
+    shift_out[c] = beta[c] - mean_out[c] * sc;
+    if (amax) atomicMax(amax, __float_as_uint(fabsf(gamma[c]) * sqrt_pm1 + fabsf(beta[c])));
+  }
+}
+
 constexpr int FIN_T = 1024;
 __global__ __launch_bounds__(FIN_T) void bn_train_finalize_kernel(
     const float2* __restrict__ stats, int nblk, int rows_per_blk, long long P, int C,
@@ -80,34 +118,94 @@ __global__ __launch_bounds__(FIN_T) void bn_train_finalize_kernel(
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    Chan acc{0.0, 0.0, 0.0};
-    if (nfull > 0) {
-      const double k = (double)nfull, n0 = (double)rows_per_blk;
-      const double m2 = sm[0] + n0 * fmax(s2[0] - s1[0] * s1[0] / k, 0.0);
-      acc = Chan{k * n0, shift + s1[0] / k, m2};
+  if (threadIdx.x == 0)
+    fin_channel(c, stats, nblk, nfull, rows_per_blk, P, C, shift, s1[0], s2[0], sm[0], running_mean, running_var,
+                momentum, eps, mean_out, invstd_out, num_batches_tracked, gamma, beta, scale_out, shift_out, amax,
+                sqrt_pm1);
+}
+
+// The same statistics in two coalesced passes (srpde_bn_train_finalize_ws): one block per channel reads one float2 of
+// each 128-B line, so a 40 x 40 layer's 20,480 partials per channel are 20,480 line requests on each of only C CUs
+// (36 us at C = 64).  Pass 1: (16-channel group, row slice) blocks, a wave reading 4 rows x 16 channels = four whole
+// lines per instruction, fp64 sums per channel and slice into ws [S][C][3]; pass 2: one wave per channel loads
+// the S slices at once and sums them in order, then finishes as fin_channel.  Same expressions; the sums are ordered per slice, then over slices.
+constexpr int FIN_SPLIT_MAX = 64;
+__global__ __launch_bounds__(256) void bn_stats_split_kernel(const float2* __restrict__ stats, int nfull, int rows,
+                                                             int C, double* __restrict__ ws) {
+  __shared__ double red[3][16][17];
+  const int cl = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl, sl = blockIdx.y;
+  const int b0 = sl * rows, b1 = min(nfull, b0 + rows);
+  double a1 = 0.0, a2 = 0.0, am = 0.0;
+  if (c < C && nfull > 0) {
+    const double shift = (double)stats[c].x;
+    int b = b0 + ph;
+    for (; b + 48 < b1; b += 64) {
+      float2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = stats[(size_t)(b + 16 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double d = (double)v[u].x - shift;
+        a1 += d;
+        a2 = fma(d, d, a2);
+        am += (double)v[u].y;
+      }
     }
-    for (int b = nfull; b < nblk; ++b) {   // the ragged last block, if any
+    for (; b < b1; b += 16) {
       const float2 v = stats[(size_t)b * C + c];
-      const long long rem = P - (long long)b * rows_per_blk;
-      const double cnt = (double)(rem < rows_per_blk ? rem : rows_per_blk);
-      acc = chan_merge(acc, Chan{cnt, (double)v.x, (double)v.y});
-    }
-    const double n = acc.n, mean = acc.mean, m2 = acc.m2;
-    const double var_b = m2 / n;
-    const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
-    mean_out[c] = (float)mean;
-    invstd_out[c] = (float)(1.0 / sqrt(var_b + (double)eps));
-    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    if (running_var) running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)var_u;
-    if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
-    if (scale_out) {   // bn_affine_kernel's outputs for this channel, from the same float mean / invstd
-      const float sc = gamma[c] * invstd_out[c];
-      scale_out[c] = sc;
-      shift_out[c] = beta[c] - mean_out[c] * sc;
-      if (amax) atomicMax(amax, __float_as_uint(fabsf(gamma[c]) * sqrt_pm1 + fabsf(beta[c])));
+      const double d = (double)v.x - shift;
+      a1 += d;
+      a2 = fma(d, d, a2);
+      am += (double)v.y;
     }
   }
+  red[0][ph][cl] = a1; red[1][ph][cl] = a2; red[2][ph][cl] = am;
+  __syncthreads();
+  if (ph < 3 && c < C) {   // three threads per channel: one sum each, phases in order
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[ph][k][cl];
+    ws[((size_t)sl * C + c) * 3 + ph] = t;
+  }
+}
+
+__global__ __launch_bounds__(64) void bn_finalize_split_kernel(const float2* __restrict__ stats, const double* __restrict__ ws,
+                                                               int nsl, int nblk, int rows_per_blk, long long P, int C,
+                                                               float* running_mean, float* running_var, float momentum,
+                                                               float eps, float* __restrict__ mean_out,
+                                                               float* __restrict__ invstd_out,
+                                                               long long* num_batches_tracked,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float* __restrict__ scale_out,
+                                                               float* __restrict__ shift_out, unsigned* amax, float sqrt_pm1) {
+  // one wave per channel: every slice's sums loaded at once (lane k: slice k), then summed in slice order
+  __shared__ double part[3][FIN_SPLIT_MAX];
+  const int c = blockIdx.x, k = threadIdx.x;
+  if (k < nsl) {
+    const double* w = ws + ((size_t)k * C + c) * 3;
+    part[0][k] = w[0]; part[1][k] = w[1]; part[2][k] = w[2];
+  }
+  __syncthreads();
+  if (k != 0) return;
+  const long long nfull_ll = P / rows_per_blk;
+  const int nfull = (int)(nfull_ll < nblk ? nfull_ll : nblk);
+  double s1 = 0.0, s2 = 0.0, sm = 0.0;
+  for (int j = 0; j < nsl; ++j) {
+    s1 += part[0][j]; s2 += part[1][j]; sm += part[2][j];
+  }
+  fin_channel(c, stats, nblk, nfull, rows_per_blk, P, C, nfull > 0 ? (double)stats[c].x : 0.0, s1, s2, sm,
+              running_mean, running_var, momentum, eps, mean_out, invstd_out, num_batches_tracked, gamma, beta,
+              scale_out, shift_out, amax, sqrt_pm1);
+}
+
+// row slices of pass 1: ~4 blocks per CU-sized wave of work, at least 64 rows (4 per phase) per slice
+static int fin_slices(int nfull, int C) {
+  const int groups = (C + 15) / 16;
+  int sl = (1024 / groups + 3) / 4;
+  sl = std::max(1, std::min(sl, FIN_SPLIT_MAX));
+  sl = std::min(sl, std::max(1, nfull / 64));
+  return sl;
 }
 
 __global__ void bn_eval_prepare_kernel(const float* rm, const float* rv, int C, float eps, float* mean_out,
@@ -711,6 +809,40 @@ int srpde_bn_train_finalize_affine(const float* stats, int nblk, int rows_per_bl
                      momentum, eps, mean_out, invstd_out, num_batches_tracked, gamma, beta, scale, shift, amax_bound,
                      (float)sqrt((double)(P - 1)));
   SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize_affine");
+  return 0;
+}
+
+size_t srpde_bn_finalize_workspace_size(int nblk, int C) {
+  (void)nblk;   // (the slice count is capped; the partial count only sets the slice length)
+  return (size_t)FIN_SPLIT_MAX * (C > 0 ? C : 0) * 3 * sizeof(double);
+}
+
+int srpde_bn_train_finalize_ws(const float* stats, int nblk, int rows_per_blk, long long P, int C, float* running_mean,
+                               float* running_var, long long* num_batches_tracked, float momentum, float eps,
+                               float* mean_out, float* invstd_out, const float* gamma, const float* beta, float* scale,
+                               float* shift, unsigned* amax_bound, void* workspace, size_t ws_bytes,
+                               hipStream_t stream) {
+  SRPDE_CHECK_ARG(stats && mean_out && invstd_out && workspace && C > 0 && nblk > 0 && P > 0 && rows_per_blk > 0,
+                  "srpde_bn_train_finalize_ws: bad args");
+  SRPDE_CHECK_ARG((scale == nullptr) == (shift == nullptr) && (scale == nullptr || (gamma && beta)),
+                  "srpde_bn_train_finalize_ws: scale / shift need gamma / beta");
+  if (ws_bytes < srpde_bn_finalize_workspace_size(nblk, C)) {
+    set_error("srpde_bn_train_finalize_ws: workspace %zu < %zu bytes", ws_bytes, srpde_bn_finalize_workspace_size(nblk, C));
+    return kErrWorkspace;
+  }
+  const long long nfull_ll = P / rows_per_blk;
+  const int nfull = (int)(nfull_ll < nblk ? nfull_ll : nblk);
+  const int nsl = fin_slices(nfull, C);
+  const int rows = nfull > 0 ? ceil_div(nfull, nsl) : 0;
+  double* ws = static_cast<double*>(workspace);
+  hipLaunchKernelGGL(bn_stats_split_kernel, dim3(ceil_div(C, 16), nsl), dim3(256), 0, stream,
+                     reinterpret_cast<const float2*>(stats), nfull, rows, C, ws);
+  SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize_ws(slices)");
+  hipLaunchKernelGGL(bn_finalize_split_kernel, dim3(C), dim3(64), 0, stream,
+                     reinterpret_cast<const float2*>(stats), ws, nsl, nblk, rows_per_blk, P, C, running_mean,
+                     running_var, momentum, eps, mean_out, invstd_out, num_batches_tracked, gamma, beta, scale, shift,
+                     scale ? amax_bound : nullptr, (float)sqrt((double)(P - 1)));
+  SRPDE_LAUNCH_CHECK("srpde_bn_train_finalize_ws");
   return 0;
 }
 

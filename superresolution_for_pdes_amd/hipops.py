@@ -526,10 +526,25 @@ def _conv_wgrad_h3x(dyp, xs, dw, n, h, w, ksize, dil, accumulate):
 
 
 # ---------------------------------- batch norm -------------------------------------
+# the two-pass finalize (srpde_bn_train_finalize_ws; SRPDE_FIN_SPLIT=0: the one-block-per-channel kernel)
+_FIN_SPLIT = os.environ.get("SRPDE_FIN_SPLIT", "1") != "0"
+
+
+def _fin_ws(nblk, C, device):
+    n = int(query("srpde_bn_finalize_workspace_size", nblk, C))
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=device), n
+
+
 def bn_train_finalize(stats, nblk, rows_per_blk, P, running_mean, running_var, nbt, momentum, eps):
     C = stats.shape[1]
     mean = empty(C, device=stats.device)
     invstd = empty(C, device=stats.device)
+    if _FIN_SPLIT:
+        ws, n = _fin_ws(nblk, C, stats.device)
+        call("srpde_bn_train_finalize_ws", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
+             _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), 0, 0, 0, 0, 0,
+             ws.data_ptr(), n, stream_ptr())
+        return mean, invstd
     call("srpde_bn_train_finalize", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
          _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), stream_ptr())
     return mean, invstd
@@ -541,6 +556,13 @@ def bn_train_finalize_affine(stats, nblk, rows_per_blk, P, running_mean, running
     C = stats.shape[1]
     dev = stats.device
     mean, invstd, scale, shift = (empty(C, device=dev) for _ in range(4))
+    if _FIN_SPLIT:
+        ws, n = _fin_ws(nblk, C, dev)
+        call("srpde_bn_train_finalize_ws", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
+             _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(),
+             gamma.data_ptr(), beta.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(amax), ws.data_ptr(), n,
+             stream_ptr())
+        return mean, invstd, (scale, shift)
     call("srpde_bn_train_finalize_affine", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
          _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
          beta.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(amax), stream_ptr())

@@ -676,3 +676,44 @@ def test_bn_bwd_apply_split_matches_fp32_apply(P, C):
     deq = (planes[0, :, :C].double() + planes[1, :, :C].double()) / s
     err = float((deq - dy.double()).abs().max())
     assert err <= 2.0 ** -22 * (2.0 ** 15 / s) + 1e-30, (err, bound)
+
+
+@pytest.mark.parametrize("nblk,rpb,P,C", [
+    (20480, 80, 1638400, 64),     # a 40x40 layer's h5 partials (80-row blocks)
+    (20480, 80, 1638400, 16),     # out_bn2
+    (3200, 128, 409600, 128),     # a 20x20 layer
+    (800, 128, 102400, 512),      # a 10x10 layer
+    (13, 7, 87, 48),              # ragged last block, C not a multiple of 16, fewer rows than one slice
+    (1, 5, 3, 4),                 # one ragged block only (nfull = 0)
+])
+def test_bn_finalize_two_pass_matches_one_block_per_channel(nblk, rpb, P, C):
+    """srpde_bn_train_finalize_ws (row slices of 16-channel groups, then the slices in order) against the
+    one-block-per-channel kernel on the same (mean, M2) partials: mean / invstd / running statistics to
+    fp32 rounding (the fp64 sums differ in order only), affine outputs and the max|a| bound word equal."""
+    from superresolution_for_pdes_amd import hipops as H
+    g = torch.Generator().manual_seed(nblk + C)
+    st = torch.empty(nblk, C, 2)
+    st[:, :, 0] = torch.randn(nblk, C, generator=g) * 0.3 + torch.linspace(-2, 2, C)
+    st[:, :, 1] = torch.rand(nblk, C, generator=g) * rpb
+    st = st.to(DEV)
+    gam = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    bet = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    res = []
+    saved = H._FIN_SPLIT
+    try:
+        for split in (False, True):
+            H._FIN_SPLIT = split
+            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+            nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+            amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+            m, i, (sc, sh) = H.bn_train_finalize_affine(st, nblk, rpb, P, rm, rv, nbt, 0.1, 1e-5, gam, bet, amax=amax)
+            m2, i2 = H.bn_train_finalize(st, nblk, rpb, P, None, None, None, 0.1, 1e-5)
+            torch.cuda.synchronize()
+            res.append((m, i, sc, sh, rm, rv, int(nbt), int(amax), m2, i2))
+    finally:
+        H._FIN_SPLIT = saved
+    a, b = res
+    for k in (0, 1, 2, 3, 4, 5, 8, 9):
+        assert torch.allclose(a[k], b[k], rtol=2e-7, atol=1e-7), (k, float((a[k] - b[k]).abs().max()))
+    assert a[6] == b[6] == 1 and a[7] == b[7]
+    assert torch.equal(b[0], b[8]) and torch.equal(b[1], b[9])   # the affine variant's mean / invstd are the plain one's
