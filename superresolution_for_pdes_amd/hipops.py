@@ -526,8 +526,11 @@ def _conv_wgrad_h3x(dyp, xs, dw, n, h, w, ksize, dil, accumulate):
 
 
 # ---------------------------------- batch norm -------------------------------------
-# the two-pass finalize (srpde_bn_train_finalize_ws; SRPDE_FIN_SPLIT=0: the one-block-per-channel kernel)
+# the two-pass finalize (srpde_bn_train_finalize_ws; SRPDE_FIN_SPLIT=0: the one-block-per-channel kernel) from
+# this many partials per channel: the 40 x 40 layers' 20,480 (36 -> 12 us); at 800-3,200 (20 x 20, 10 x 10) the
+# one-pass kernel's 8.5-11.7 us is no slower than the two launches' ~12 (profiles/r05f_bn_finalize_ab.txt)
 _FIN_SPLIT = os.environ.get("SRPDE_FIN_SPLIT", "1") != "0"
+_FIN_SPLIT_MIN_BLOCKS = 8192
 
 
 def _fin_ws(nblk, C, device):
@@ -539,7 +542,7 @@ def bn_train_finalize(stats, nblk, rows_per_blk, P, running_mean, running_var, n
     C = stats.shape[1]
     mean = empty(C, device=stats.device)
     invstd = empty(C, device=stats.device)
-    if _FIN_SPLIT:
+    if _FIN_SPLIT and nblk >= _FIN_SPLIT_MIN_BLOCKS:
         ws, n = _fin_ws(nblk, C, stats.device)
         call("srpde_bn_train_finalize_ws", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
              _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(), 0, 0, 0, 0, 0,
@@ -556,7 +559,7 @@ def bn_train_finalize_affine(stats, nblk, rows_per_blk, P, running_mean, running
     C = stats.shape[1]
     dev = stats.device
     mean, invstd, scale, shift = (empty(C, device=dev) for _ in range(4))
-    if _FIN_SPLIT:
+    if _FIN_SPLIT and nblk >= _FIN_SPLIT_MIN_BLOCKS:
         ws, n = _fin_ws(nblk, C, dev)
         call("srpde_bn_train_finalize_ws", stats.data_ptr(), nblk, rows_per_blk, P, C, _p(running_mean),
              _p(running_var), _p(nbt), float(momentum), float(eps), mean.data_ptr(), invstd.data_ptr(),

@@ -699,8 +699,9 @@ def test_bn_finalize_two_pass_matches_one_block_per_channel(nblk, rpb, P, C):
     gam = (torch.rand(C, generator=g) + 0.5).to(DEV)
     bet = (torch.randn(C, generator=g) * 0.2).to(DEV)
     res = []
-    saved = H._FIN_SPLIT
+    saved = H._FIN_SPLIT, H._FIN_SPLIT_MIN_BLOCKS
     try:
+        H._FIN_SPLIT_MIN_BLOCKS = 1   # the two-pass kernels at every size here
         for split in (False, True):
             H._FIN_SPLIT = split
             rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
@@ -711,7 +712,7 @@ def test_bn_finalize_two_pass_matches_one_block_per_channel(nblk, rpb, P, C):
             torch.cuda.synchronize()
             res.append((m, i, sc, sh, rm, rv, int(nbt), int(amax), m2, i2))
     finally:
-        H._FIN_SPLIT = saved
+        H._FIN_SPLIT, H._FIN_SPLIT_MIN_BLOCKS = saved
     a, b = res
     for k in (0, 1, 2, 3, 4, 5, 8, 9):
         assert torch.allclose(a[k], b[k], rtol=2e-7, atol=1e-7), (k, float((a[k] - b[k]).abs().max()))
