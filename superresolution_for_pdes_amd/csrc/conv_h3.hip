@@ -1656,6 +1656,230 @@ __global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(Wgrad
     }
 }
 
+// ------------- weight gradient h3g: h3h's input-row ring for 128 output channels per tile -------------
+// The deep layers (Cout 128-512 at W = 10 / 20) ran h3p's 256 x 128 / 128 x 256 tiles: one tap per column
+// tile, so every tap DMA'd its own shifted copy of the input rows (~0.25 LDS-DMA pieces per MFMA, each ~60
+// issue cycles among the MFMAs) and both operands were re-read once per column tile.  Here a tile is 128 output
+// channels x one 32-channel input chunk x all nine taps: the input chunk is staged ONCE as h3h's ring of pixel
+// rows, and the nine taps read it at row shifts.  Twelve MFMA waves: wave (mi, ty) owns the 32-row m block mi
+// and the three taps of kernel row ty (dx = -dil, 0, +dil), i.e. three 32 x 32 accumulators; per 16-pixel step
+// it reads one A fragment pair (dY hi / lo) and three B pairs and issues nine MFMA chains of three products.
+// 40 DMA pieces per 64-pixel stage for 432 MFMAs (0.09 per MFMA).  Same products, same per-stage partial
+// chains folded into the accumulator every three stages, same slab layout as h3h: the slabs equal h3p's up to
+// the order of the three-stage partial sums.  Out-of-image taps read a zero row per lane (the tap's shift is
+// folded into the address, so the lane's address is the shifted row or the zero row).
+template <int PS, int NST, int CAP, int W, int DIL>
+__global__ __launch_bounds__(768, 1) void conv_wgrad_h3g_kernel(WgradParams p, H3P q, int cc_n) {
+  constexpr int BM = 128, NW = 12;
+  constexpr int RA = BM * 2;                   // A image row bytes (one plane)
+  constexpr int IMG_A = PS * RA;               // one plane of one stage
+  constexpr int NA = 2 * IMG_A / 1024;         // A pieces per stage
+  constexpr int NBP = PS / 16;                 // B pieces per plane per stage (16 rows x 64 B)
+  constexpr int TOT = NA + 2 * NBP;            // pieces per stage (+ the mirror copy of ring rows 0 .. 15)
+  constexpr int DLO = TOT / NW, NHI = TOT % NW;   // waves < NHI issue DLO + 1 pieces per stage
+  constexpr int NJ = DLO + (NHI ? 1 : 0);
+  // ring plane: CAP rows, then rows CAP .. CAP + 15 mirroring rows 0 .. 15 (a lane's row index base + lrow,
+  // lrow <= 11, never wraps), then the zero row
+  constexpr int RING = (CAP + 17) * 64;
+  constexpr int ZROW = CAP + 16;
+  constexpr int HALO = (W + 1) * DIL;
+  static_assert(IMG_A % 1024 == 0 && PS % 16 == 0 && NST == 3, "stage geometry");
+  static_assert((CAP & (CAP - 1)) == 0 && 2 * HALO + 15 + 3 * PS <= CAP, "ring rows: a power of two holding a stage's reach");
+  static_assert((NST - 2) * (DLO + 1) <= 62, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* lds = reinterpret_cast<char*>(smem);
+  char* const abuf = lds;                              // [NST][2][PS][RA]
+  char* const bring = abuf + NST * 2 * IMG_A;          // [2][CAP + 17][64]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nbm = (p.Cout + BM - 1) / BM;
+  const int ntile = nbm * cc_n;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int mt = tile / cc_n, cc = tile - mt * cc_n;
+  const int m0 = mt * BM, c0 = cc * 32;
+  const int pbeg = split * p.chunk, pend = min(p.P, pbeg + p.chunk);
+  const int nsteps = (pend - pbeg + PS - 1) / PS;
+  const int rbase = (pbeg + HALO + 15) & ~15;          // first row the stages DMA (16-aligned)
+  const int rlo = (pbeg - HALO) & ~15;                 // first row of the prologue (may be < 0)
+
+  if (threadIdx.x < 8)
+    reinterpret_cast<float4*>(bring + ZROW * 64 + (threadIdx.x >> 2) * RING)[threadIdx.x & 3] =
+        make_float4(0.f, 0.f, 0.f, 0.f);
+
+  const int32x4 rsa = make_rsrc(q.dyp, (unsigned)((size_t)2 * p.P * p.lddy * 2));
+  const int32x4 rsb = make_rsrc(q.xp, (unsigned)((size_t)2 * p.P * p.Cin * 2));
+  const unsigned aplane = (unsigned)((size_t)p.P * p.lddy * 2), bplane = (unsigned)((size_t)p.P * p.Cin * 2);
+  const unsigned bring_a = lds_addr_of(bring);
+
+  // B piece of rows [r, r + 16) of plane pl (r 16-aligned): lane -> row r + lane / 4, 16-B chunk lane % 4; the
+  // piece landing in ring rows 0 .. 15 goes to the mirror rows as well (one more DMA: the stage waits assume
+  // the minimum count per wave, so an extra op only makes them stricter)
+  auto bpiece = [&](int r, int pl) {
+    const int row = r + (lane >> 2);
+    const unsigned off = (row >= 0 && row < p.P)
+                             ? pl * bplane + (unsigned)(((size_t)row * p.Cin + c0 + 8 * (lane & 3)) * 2)
+                             : OOB;
+    const int slot = r & (CAP - 1);
+    dma16(rsb, off, bring_a + pl * RING + slot * 64);
+    if (slot == 0) dma16(rsb, off, bring_a + pl * RING + CAP * 64);
+  };
+  // this wave's pieces: piece u = wave + j * NW of every stage; u < NA: A (dY rows), else B (input rows).  The
+  // per-lane source offsets advance by one stage of rows per issue (stages are issued in order)
+  // (the lane's row / column of an A piece: m beyond Cout and rows past the chunk read zeros)
+  auto a_geom = [&](int u, int& row, int& m) {
+    const int idx = u - (u / (NA / 2)) * (NA / 2);
+    const int byte = idx * 1024 + lane * 16;
+    row = byte / RA;
+    const int sl = (byte - row * RA) >> 4;
+    m = m0 + 8 * (sl ^ wx_swz<RA>(row));
+  };
+  unsigned a_off[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int u = min(wave + j * NW, NA - 1);
+    int row, m;
+    a_geom(u, row, m);
+    a_off[j] = m < p.Cout ? (u / (NA / 2)) * aplane + (unsigned)(((size_t)(pbeg + row) * p.lddy + m) * 2) : OOB;
+  }
+  const unsigned astep = (unsigned)(PS * p.lddy * 2);
+  auto issue = [&](int s, int slot) {
+    const int p0 = pbeg + s * PS;
+    const bool full = p0 + PS <= pend;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int u = wave + j * NW;
+      if (j == DLO && wave >= NHI) break;
+      if (u < NA) {
+        const int pl = u / (NA / 2), idx = u - pl * (NA / 2);
+        bool ok = a_off[j] < OOB;
+        if (!full) {
+          int row, m;
+          a_geom(u, row, m);
+          ok = ok && p0 + row < pend;
+        }
+        dma16(rsa, ok ? a_off[j] : OOB, lds_addr_of(abuf + (slot * 2 + pl) * IMG_A + idx * 1024));
+      } else {
+        const int v = u - NA, pl = v / NBP, g = v - pl * NBP;
+        bpiece(rbase + s * PS + 16 * g, pl);
+      }
+      if (a_off[j] < OOB) a_off[j] += astep;
+    }
+  };
+  // prologue: the input rows [rlo, rbase) every later stage assumes resident
+  {
+    const int ng = (rbase - rlo) >> 4;
+    for (int v = wave; v < 2 * ng; v += NW) bpiece(rlo + 16 * (v >> 1), v & 1);
+  }
+
+  const int ea = h3_exp(*q.ady);
+  unsigned xb = *q.ax0;
+  if (p.c1) xb = max(xb, *q.ax1);
+  const int eb = h3_exp(xb);
+
+  const int mi = wave & 3, ty = wave >> 2;
+  floatx16 acc[3], part[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  const int2 oa = tr_offsets<RA>(32 * mi, lane);
+  // the lane's pixel rows of a 16-pixel step: 8h + 4j + qq (j = 0, 1: the two transposed 4-row reads)
+  const int dyo = (ty - 1) * DIL;
+  const int colb = 2 * ((lane & 16) + 4 * (lane & 3));
+  const int lrow = 8 * (lane >> 5) + ((lane & 15) >> 2);
+  const int HWp = p.H * W;
+  const unsigned lane_b = bring_a + (unsigned)(lrow * 64 + colb);   // + the row index base * 64
+  const unsigned zaddr = bring_a + (unsigned)(ZROW * 64 + colb);
+  int rs0 = pbeg % HWp;   // pixel-in-image of the stage's first pixel (uniform), advanced by PS per stage
+  static_assert(PS + 16 * (PS / 16) <= 2 * 100, "one wrap per add (H * W >= 100)");
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(s, s);
+  // B row addresses of the lane for the wave's three taps at step (kk, j) of the stage at pixel p0: uniform
+  // parts in scalars (the pixel-in-image of p0 + 16 kk + 4 j, the ring index of its shifted rows), per lane the
+  // row offset lrow, its wrap into the next image row / image, and the tap masks
+  auto baddr = [&](int P0, int R0, unsigned (&ba)[3]) {
+    if (R0 >= HWp) R0 -= HWp;                            // uniform: the pixel-in-image of P0
+    int r = R0 + lrow;
+    r = (int)min((unsigned)r, (unsigned)(r - HWp));      // wrap into the next image
+    const int y = r / W, x = r - y * W;
+    const bool yok = (unsigned)(y + dyo) < (unsigned)p.H;
+    const int ib = __builtin_amdgcn_readfirstlane((P0 + dyo * W - DIL) & (CAP - 1));   // tap 0's row index base
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const bool ok = yok && (t == 1 || (t == 0 ? x >= DIL : x < W - DIL));
+      const unsigned a = lane_b + (unsigned)(((ib + t * DIL) & (CAP - 1)) * 64);
+      ba[t] = ok ? a : zaddr;
+    }
+  };
+  auto stage = [&](int s, auto fresh_tag, auto slot_tag) {
+    constexpr bool FRESH = decltype(fresh_tag)::value;
+    constexpr int SLOT = decltype(slot_tag)::value;
+    if (wave < NHI) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * (DLO + 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * DLO) : "memory");
+    __syncthreads();
+
+    const lds_char* sa = (const lds_char*)(uintptr_t)lds_addr_of(abuf) + SLOT * 2 * IMG_A;
+    const int p0 = pbeg + s * PS;
+    unsigned ba0[3], ba1[3];
+    baddr(p0, rs0, ba0);
+    baddr(p0 + 4, rs0 + 4, ba1);
+#pragma unroll
+    for (int kk = 0; kk < NBP; ++kk) {
+      const half8 ah = tr_read(sa + oa.x + kk * 16 * RA, sa + oa.y + kk * 16 * RA);
+      const half8 al = tr_read(sa + IMG_A + oa.x + kk * 16 * RA, sa + IMG_A + oa.y + kk * 16 * RA);
+      half8 bh[3], bl[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        bh[t] = tr_read((const lds_char*)(uintptr_t)ba0[t], (const lds_char*)(uintptr_t)ba1[t]);
+        bl[t] = tr_read((const lds_char*)(uintptr_t)ba0[t] + RING, (const lds_char*)(uintptr_t)ba1[t] + RING);
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        floatx16 c0v;
+        if (FRESH && kk == 0)
+          c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[t], floatx16{}, 0, 0, 0);   // small terms first
+        else
+          c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[t], part[t], 0, 0, 0);
+        c0v = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[t], c0v, 0, 0, 0);
+        part[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[t], c0v, 0, 0, 0);
+      }
+      if (kk + 1 < NBP) {   // the next step's addresses (VALU beside this step's MFMAs)
+        baddr(p0 + 16 * (kk + 1), rs0 + 16 * (kk + 1), ba0);
+        baddr(p0 + 16 * (kk + 1) + 4, rs0 + 16 * (kk + 1) + 4, ba1);
+      }
+      if (kk == 0) issue(s + NST - 1, (SLOT + NST - 1) % NST);   // stage s + 2's DMA after the first MFMAs
+    }
+    rs0 += PS;
+    if (rs0 >= HWp) rs0 -= HWp;
+  };
+  for (int s = 0; s < nsteps; s += NST) {
+    stage(s, std::true_type{}, std::integral_constant<int, 0>{});
+    if (s + 1 < nsteps) stage(s + 1, std::false_type{}, std::integral_constant<int, 1>{});
+    if (s + 2 < nsteps) stage(s + 2, std::false_type{}, std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int t = 0; t < 3; ++t) acc[t] += part[t];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // spare DMAs land before the workgroup retires
+
+  // slab [split][Cout][K], k = tap * Cin + c; scales undone (exact powers of two)
+  const float ua = exp2i(-ea), ub = exp2i(-eb);
+  float* out = p.part + (size_t)split * p.Cout * p.K;
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int n = (3 * ty + t) * p.Cin + c0 + lr;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (m < p.Cout) out[(size_t)m * p.K + n] = (acc[t][r] * ua) * ub;
+    }
+  }
+}
+
 // fp32 packed weights [rows][K] -> fp16 hi / lo planes [2][rows][K] with a power-of-two scale
 // per row (one wave per row)
 __global__ __launch_bounds__(256) void split_weights_h3_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
@@ -1973,9 +2197,27 @@ static void h3p_tiles(int cout, int K, int* bm, int* bn) {
   else { *bm = 32; *bn = h3p_use288(cout, K) ? 288 : 256; }
 }
 
-void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
+// h3g (the input-row ring for 128-channel m tiles, Cout a multiple of 128) takes W = 10 / 20 (the ring holds a
+// stage's reach up to a halo of 24 rows: W = 10 at dilation 1 and 2, W = 20 at dilation 1; a W = 20 dilation-2
+// layer falls back to h3p with the same split plan, whose chunks are multiples of both kernels' stages)
+constexpr int H3G_PS = 64, H3G_CAP = 256;
+static bool h3g_shape(int cout, int K, int cin, int w) {
+#ifdef SRPDE_NO_H3G
+  (void)cout; (void)K; (void)cin; (void)w;
+  return false;
+#else
+  return cout % 128 == 0 && K == 9 * cin && cin % 32 == 0 && (w == 10 || w == 20);
+#endif
+}
+static bool h3g_ok(int cout, int K, int cin, int w, int dil) {
+  return h3g_shape(cout, K, cin, w) && (dil == 1 || (dil == 2 && w == 10));
+}
+
+void h3p_split(int P, int cout, int K, int w, int* chunk, int* splits) {
   int bm, bn;
   h3p_tiles(cout, K, &bm, &bn);
+  const bool g = h3g_shape(cout, K, K / 9, w);
+  if (g) { bm = 128; bn = 288; }
   const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
   // one workgroup per CU (LDS): ~2 rounds of 256 CUs, chunks a multiple of the 32-pixel stage.
   // The weight gradients run on a side stream next to the dgrad chain; half the workgroups of the
@@ -1984,7 +2226,7 @@ void h3p_split(int P, int cout, int K, int* chunk, int* splits) {
   constexpr long long target = 512;
   const long long want = std::max(1LL, target / tiles);
   long long c = (P + want - 1) / want;
-  c = (c + 31) / 32 * 32;
+  c = g ? (c + 63) / 64 * 64 : (c + 31) / 32 * 32;
   if (c < 256) c = 256;
   *chunk = (int)c;
   *splits = ceil_div(P, c);
@@ -2018,6 +2260,18 @@ static int launch_h3h(const WgradParams& p, const H3P& q, hipStream_t st) {
   return launch_h3h_cfg<BM, H3H_PS, 3, H3H_CAP, XF>(p, q, st);
 }
 
+template <int W, int DIL>
+static int launch_h3g(const WgradParams& p, const H3P& q, hipStream_t st) {
+  constexpr int PS = H3G_PS, NST = 3, CAP = H3G_CAP;
+  const int cc_n = p.Cin / 32;
+  const int nb = ceil_div(p.Cout, 128) * cc_n * p.splits;
+  const size_t lds = (size_t)NST * 2 * PS * 128 * 2 + (size_t)2 * (CAP + 17) * 64;
+  note_kernel("conv_wgrad_h3g_kernel<%d, %d, %d, %d, %d>", PS, NST, CAP, W, DIL);
+  hipLaunchKernelGGL((conv_wgrad_h3g_kernel<PS, NST, CAP, W, DIL>), dim3(nb), dim3(768), lds, st, p, q, cc_n);
+  SRPDE_LAUNCH_CHECK("srpde_conv_wgrad_h3p(h3g)");
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN>
 static int launch_h3p(const WgradParams& p, const H3P& q, hipStream_t st) {
   constexpr int PS = 32, NST = 3;
@@ -2037,7 +2291,7 @@ extern "C" {
 
 size_t srpde_conv_wgrad_h3p_workspace_size(int n, int h, int w, int cout, int cin, int ksize) {
   int chunk, splits;
-  h3p_split(n * h * w, cout, ksize * ksize * cin, &chunk, &splits);
+  h3p_split(n * h * w, cout, ksize * ksize * cin, w, &chunk, &splits);
   return (size_t)splits * cout * ksize * ksize * cin * sizeof(float);
 }
 
@@ -2058,7 +2312,7 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
   // the dy planes' row stride is cout rounded up to 32 (p.lddy): the bound is on that width
   SRPDE_CHECK_ARG(2LL * p.P * std::max(p.lddy, p.Cin) * 2 < (1LL << 31), "srpde_conv_wgrad_h3p: tensor too large");
-  h3p_split(p.P, cout, p.K, &p.chunk, &p.splits);
+  h3p_split(p.P, cout, p.K, w, &p.chunk, &p.splits);
   const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
   if (ws_bytes < need) {
     set_error("srpde_conv_wgrad_h3p: workspace %zu < %zu bytes", ws_bytes, need);
@@ -2067,13 +2321,19 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   p.part = static_cast<float*>(workspace);
   const H3P q{static_cast<const _Float16*>(dyp), static_cast<const _Float16*>(xp), amax_dy, amax0, c1 ? amax1 : amax0};
   int rc;
-  if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
+  if (h3g_ok(cout, p.K, p.Cin, w, dil))
+    rc = w == 20 ? launch_h3g<20, 1>(p, q, stream) : dil == 2 ? launch_h3g<10, 2>(p, q, stream) : launch_h3g<10, 1>(p, q, stream);
+  else if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
   else if (cout >= 128) rc = launch_h3p<128, 256, 2, 4>(p, q, stream);
   else if (h3h_ok(cout, p.K, p.Cin, w, dil)) rc = cout >= 64 ? launch_h3h<64>(p, q, stream) : launch_h3h<32>(p, q, stream);
   else if (cout >= 64) rc = h3p_use288(cout, p.K) ? launch_h3p<64, 288, 1, 9>(p, q, stream) : launch_h3p<64, 256, 1, 8>(p, q, stream);
   else rc = h3p_use288(cout, p.K) ? launch_h3p<32, 288, 1, 9>(p, q, stream) : launch_h3p<32, 256, 1, 8>(p, q, stream);
   if (rc) return rc;
   return wgrad_reduce(p.part, dw, p.splits, cout, p.Cin, cin_real, ksize * ksize, accumulate, stream);
+}
+
+int srpde_conv_wgrad_h3g_supported(int cout, int cin, int w, int dil) {
+  return cout > 0 && cin > 0 && h3g_ok(cout, 9 * cin, cin, w, dil) ? 1 : 0;
 }
 
 int srpde_conv_wgrad_h3x_supported(int c0, int c1, int cout, int w, int dil) {
@@ -2106,7 +2366,7 @@ int srpde_conv_wgrad_h3x(const void* dyp, const unsigned* amax_dy, const float* 
   p.P = n * h * w; p.Cin = c0 + c1; p.K = ksize * ksize * p.Cin;
   SRPDE_CHECK_ARG(2LL * p.P * p.lddy * 2 < (1LL << 31) && (long long)p.P * std::max(ldx0, ldx1) < (1LL << 31),
                   "srpde_conv_wgrad_h3x: tensor too large");
-  h3p_split(p.P, cout, p.K, &p.chunk, &p.splits);
+  h3p_split(p.P, cout, p.K, w, &p.chunk, &p.splits);
   const size_t need = (size_t)p.splits * cout * p.K * sizeof(float);
   if (ws_bytes < need) {
     set_error("srpde_conv_wgrad_h3x: workspace %zu < %zu bytes", ws_bytes, need);

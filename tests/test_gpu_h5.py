@@ -85,7 +85,17 @@ def test_conv_h5_equals_h4(n, h, c0, c1, cout):
             eam = torch.zeros(1, dtype=torch.int32, device=DEV)
             H.conv_fwd(x0, x1, wf, b, ye, n, h, w_, cout, 3, 1, 1, False, None,
                        ep_bn=(emean, einv, ega, ebe, eam), x1_gate=gate)
+            # the training paths in isolation: statistics without a stored split (the default at W = 40, whose
+            # weight gradient splits the input itself -- round 5's null-pointer fault) and a split without statistics
+            ys = torch.empty(P, cout, device=DEV)
+            stats_s, _, _ = H.conv_stats_buffer(n, h, w_, cout, DEV, c0, c1, 1)
+            H.conv_fwd(x0, x1, wf, b, ys, n, h, w_, cout, 3, 1, 1, False, stats_s, None, in_affine=aff, x1_gate=gate)
+            yx = torch.empty(P, cout, device=DEV)
+            xpx = H.split_planes_buffer(P, cin, DEV)
+            H.conv_fwd(x0, x1, wf, b, yx, n, h, w_, cout, 3, 1, 1, False, None, xpx, in_affine=aff, x1_gate=gate)
             torch.cuda.synchronize()
+            assert torch.equal(ys, y) and torch.equal(stats_s, stats), "statistics without a stored split"
+            assert torch.equal(yx, y) and torch.equal(xpx, xp), "stored split without statistics"
             outs.append((yp, y, xp, ye, eam, stats, rows))
     finally:
         H.set_h5(prev)

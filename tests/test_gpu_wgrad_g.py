@@ -1,0 +1,91 @@
+"""conv_wgrad_h3g_kernel: the deep layers' weight gradient (src/models.py:42-49 bridge, :80-87 enc2/enc3/dec3/dec2
+through aten::convolution_backward's weight gradient) as one 128-channel m tile x one 32-channel input chunk x all
+nine taps, the input chunk staged once as a ring of pixel rows.  It takes the stored splits the forward and dgrad
+kernels write (srpde_conv_wgrad_h3p with Cout % 128 == 0 at W = 10 / 20).  Held to fp64 with the fp32 bar of the
+other split kernels (< 1e-6 relative L2 and within 3x the fp32-MFMA kernel's error), at the model's shapes with
+several split-K chunks, a ragged last chunk and a chunk that ends inside a three-stage group; and it must be
+deterministic (two calls, same bits)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rows(x):
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c).contiguous()
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("n,c0,c1,cout,h,dil", [
+    (37, 512, 0, 512, 10, 2),    # bridge.3: dilation 2, several chunks, ragged
+    (23, 256, 0, 512, 10, 2),    # bridge.0
+    (29, 512, 256, 256, 10, 1),  # dec3.conv1: virtual concat
+    (19, 128, 0, 256, 10, 1),    # enc3.conv1
+    (11, 256, 128, 128, 20, 1),  # dec2.conv1 (W = 20)
+    (9, 64, 0, 128, 20, 1),      # enc2.conv1: two input chunks
+    (1, 256, 0, 256, 10, 1),     # one sample: one short chunk
+])
+def test_wgrad_h3g_matches_fp64(n, c0, c1, cout, h, dil):
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("h3")
+    cin = c0 + c1
+    assert bool(H.query("srpde_conv_wgrad_h3g_supported", cout, cin, h, dil))
+    g = torch.Generator().manual_seed(n * 13 + cin + cout)
+    x = torch.randn(n, cin, h, h, generator=g, dtype=torch.float64)
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) * (2.0 / (9 * cin)) ** 0.5
+    dy = torch.randn(n, cout, h, h, generator=g, dtype=torch.float64) * 1e-3
+    dw64 = torch.nn.grad.conv2d_weight(x, wt.shape, dy, padding=dil, dilation=dil)
+    xr = _rows(x.float()).to(DEV)
+    x0, x1 = (xr[:, :c0], xr[:, c0:]) if c1 else (xr, None)
+    dyr = _rows(dy.float()).to(DEV)
+    P = n * h * h
+    wf, wd = H.pack_conv_weights(wt.float().to(DEV), cin, want_dgrad=True)
+    xp, dyp = H.split_planes_buffer(P, cin, DEV), H.split_planes_buffer(P, cout, DEV)
+    y = H.empty(P, cout, device=DEV)
+    H.conv_fwd(x0, x1, wf, None, y, n, h, h, cout, 3, dil, 1, False, None, xp)
+    dx = H.empty(P, cin, device=DEV)
+    H.conv_fwd(dyr, None, wd, None, dx, n, h, h, cin, 3, dil, -1, False, None, dyp)
+    dw = torch.empty(cout, cin, 3, 3, device=DEV)
+    H.conv_wgrad_h3p(dyp, xp, dw, n, h, h, 3, dil)
+    assert H.query("srpde_last_kernel").decode().startswith("conv_wgrad_h3g_kernel")
+    dw2 = torch.empty(cout, cin, 3, 3, device=DEV)
+    H.conv_wgrad_h3p(dyp, xp, dw2, n, h, h, 3, dil)
+    H.set_conv_math("f32")
+    dwf = torch.empty(cout, cin, 3, 3, device=DEV)
+    H.conv_wgrad(dyr, x0, x1, dwf, n, h, h, 3, dil)
+    H.set_conv_math("h3")
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw2), "not deterministic"
+    e_g, e_f32 = _rel(dw, dw64), _rel(dwf, dw64)
+    print(f"wgrad h3g {e_g:.3e} f32 {e_f32:.3e}")
+    assert e_g < 1e-6 and e_g < 3.0 * e_f32 + 1e-7, (e_g, e_f32)
+
+
+def test_wgrad_h3g_accumulate():
+    """accumulate=1 adds the gradient into dw (the bridge's two-call pattern is not used, but the ABI has it)."""
+    from superresolution_for_pdes_amd import hipops as H
+    H.set_conv_math("h3")
+    n, c, cout, h = 4, 128, 128, 20
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n * h * h, c, generator=g).to(DEV)
+    dy = torch.randn(n * h * h, cout, generator=g).to(DEV) * 1e-2
+    wt = torch.randn(cout, c, 3, 3, generator=g).to(DEV) * 0.05
+    wf, wd = H.pack_conv_weights(wt, c, want_dgrad=True)
+    xp, dyp = H.split_planes_buffer(n * h * h, c, DEV), H.split_planes_buffer(n * h * h, cout, DEV)
+    x._srpde_amax = H.amax_of(x)
+    dy._srpde_amax = H.amax_of(dy)
+    H.conv_fwd(x, None, wf, None, H.empty(n * h * h, cout, device=DEV), n, h, h, cout, 3, 1, 1, False, None, xp)
+    H.conv_fwd(dy, None, wd, None, H.empty(n * h * h, c, device=DEV), n, h, h, c, 3, 1, -1, False, None, dyp)
+    a = torch.empty(cout, c, 3, 3, device=DEV)
+    H.conv_wgrad_h3p(dyp, xp, a, n, h, h)
+    base = torch.randn(cout, c, 3, 3, generator=g).to(DEV)
+    b = base.clone()
+    H.conv_wgrad_h3p(dyp, xp, b, n, h, h, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(b, base + a)
