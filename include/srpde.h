@@ -200,8 +200,8 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
                          int c1, const unsigned* amax1, float* dw, int cin_real, int accumulate, int n, int h, int w,
                          int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* 1 when srpde_conv_wgrad_h3p runs this shape on the input-row-ring kernel for 128-channel m tiles
- * (conv_wgrad_h3g_kernel: cout % 128 == 0, cin % 32 == 0, w = 10 at dilation 1 or 2, w = 20 at dilation 1 --
- * the deep layers, bridge / enc2-3 / dec2-3, models.py:42-49, 80-87); else the h3p / h3h tiles. */
+ * (conv_wgrad_h3g_kernel: cout 128, cin 32 .. 128 in steps of 32, w = 20, dilation 1 -- enc2.conv1 / conv2 and
+ * dec2.conv2, models.py:80-81, 92); else the h3p / h3h tiles. */
 int srpde_conv_wgrad_h3g_supported(int cout, int cin, int w, int dil);
 /* srpde_conv_wgrad_h3p for the 40 x 40 layers (cout <= 64, c0 and c1 multiples of 32: shapes for which
  * srpde_conv_wgrad_h3x_supported returns 1) with the input read from its fp32 rows instead of a stored split,

@@ -1664,7 +1664,10 @@ __global__ __launch_bounds__(XF ? 704 : 576, 1) void conv_wgrad_h3h_kernel(Wgrad
 // rows, and the nine taps read it at row shifts.  Twelve MFMA waves: wave (mi, ty) owns the 32-row m block mi
 // and the three taps of kernel row ty (dx = -dil, 0, +dil), i.e. three 32 x 32 accumulators; per 16-pixel step
 // it reads one A fragment pair (dY hi / lo) and three B pairs and issues nine MFMA chains of three products.
-// 40 DMA pieces per 64-pixel stage for 432 MFMAs (0.09 per MFMA).  Same products, same per-stage partial
+// 40 DMA pieces per 64-pixel stage for 432 MFMAs (0.09 per MFMA, h3p 0.25).  Measured (profiles/r06_h3g_ab.txt,
+// r06_pmc_h3g.txt): the DMA saving is paid back in issue -- the per-lane tap masks and ring addresses of three taps
+// cost 7-8 VALU per MFMA at 164 VGPRs, three waves per SIMD -- so the W = 10 layers stay on h3p (+5-10 % here) and
+// h3g takes only the W = 20 shapes whose K leaves h3p's last column tile partly empty.  Same products, same per-stage partial
 // chains folded into the accumulator every three stages, same slab layout as h3h: the slabs equal h3p's up to
 // the order of the three-stage partial sums.  Out-of-image taps read a zero row per lane (the tap's shift is
 // folded into the address, so the lane's address is the shifted row or the zero row).
@@ -2197,26 +2200,20 @@ static void h3p_tiles(int cout, int K, int* bm, int* bn) {
   else { *bm = 32; *bn = h3p_use288(cout, K) ? 288 : 256; }
 }
 
-// h3g (the input-row ring for 128-channel m tiles, Cout a multiple of 128) takes W = 10 / 20 (the ring holds a
-// stage's reach up to a halo of 24 rows: W = 10 at dilation 1 and 2, W = 20 at dilation 1; a W = 20 dilation-2
-// layer falls back to h3p with the same split plan, whose chunks are multiples of both kernels' stages)
+// h3g (the input-row ring for 128-channel m tiles) takes the W = 20 layers with 128 output channels and at most
+// 128 input channels (enc2.conv1, enc2.conv2, dec2.conv2), whose K = 9 Cin leaves h3p's last 256-column tile
+// partly empty; against h3p on the same box (profiles/r06_h3g_ab.txt): enc2.conv1 -16 %, enc2.conv2 -1 %,
+// dec2.conv2 -3 %, but dec2.conv1 (Cin 384) +2 % and the W = 10 layers +5-10 % (12 waves at 164 VGPRs issue
+// 7-8 VALU per MFMA for the per-lane tap masks, against h3p's 4.5 for its DMA bookkeeping), so those keep h3p
 constexpr int H3G_PS = 64, H3G_CAP = 256;
-static bool h3g_shape(int cout, int K, int cin, int w) {
-#ifdef SRPDE_NO_H3G
-  (void)cout; (void)K; (void)cin; (void)w;
-  return false;
-#else
-  return cout % 128 == 0 && K == 9 * cin && cin % 32 == 0 && (w == 10 || w == 20);
-#endif
-}
 static bool h3g_ok(int cout, int K, int cin, int w, int dil) {
-  return h3g_shape(cout, K, cin, w) && (dil == 1 || (dil == 2 && w == 10));
+  return cout == 128 && w == 20 && dil == 1 && cin <= 128 && K == 9 * cin && cin % 32 == 0;
 }
 
 void h3p_split(int P, int cout, int K, int w, int* chunk, int* splits) {
   int bm, bn;
   h3p_tiles(cout, K, &bm, &bn);
-  const bool g = h3g_shape(cout, K, K / 9, w);
+  const bool g = h3g_ok(cout, K, K / 9, w, 1);
   if (g) { bm = 128; bn = 288; }
   const long long tiles = (long long)ceil_div(cout, bm) * ceil_div(K, bn);
   // one workgroup per CU (LDS): ~2 rounds of 256 CUs, chunks a multiple of the 32-pixel stage.
@@ -2321,8 +2318,7 @@ int srpde_conv_wgrad_h3p(const void* dyp, const unsigned* amax_dy, const void* x
   p.part = static_cast<float*>(workspace);
   const H3P q{static_cast<const _Float16*>(dyp), static_cast<const _Float16*>(xp), amax_dy, amax0, c1 ? amax1 : amax0};
   int rc;
-  if (h3g_ok(cout, p.K, p.Cin, w, dil))
-    rc = w == 20 ? launch_h3g<20, 1>(p, q, stream) : dil == 2 ? launch_h3g<10, 2>(p, q, stream) : launch_h3g<10, 1>(p, q, stream);
+  if (h3g_ok(cout, p.K, p.Cin, w, dil)) rc = launch_h3g<20, 1>(p, q, stream);
   else if (cout >= 256) rc = launch_h3p<256, 128, 4, 2>(p, q, stream);
   else if (cout >= 128) rc = launch_h3p<128, 256, 2, 4>(p, q, stream);
   else if (h3h_ok(cout, p.K, p.Cin, w, dil)) rc = cout >= 64 ? launch_h3h<64>(p, q, stream) : launch_h3h<32>(p, q, stream);

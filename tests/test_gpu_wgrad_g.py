@@ -1,10 +1,10 @@
-"""conv_wgrad_h3g_kernel: the deep layers' weight gradient (src/models.py:42-49 bridge, :80-87 enc2/enc3/dec3/dec2
-through aten::convolution_backward's weight gradient) as one 128-channel m tile x one 32-channel input chunk x all
+"""conv_wgrad_h3g_kernel: the W = 20 weight gradients with 128 outputs (src/models.py:80-81, 92: enc2.conv1 / conv2,
+dec2.conv2, through aten::convolution_backward's weight gradient) as one 128-channel m tile x one 32-channel input chunk x all
 nine taps, the input chunk staged once as a ring of pixel rows.  It takes the stored splits the forward and dgrad
-kernels write (srpde_conv_wgrad_h3p with Cout % 128 == 0 at W = 10 / 20).  Held to fp64 with the fp32 bar of the
+kernels write (srpde_conv_wgrad_h3p at the shapes srpde_conv_wgrad_h3g_supported names).  Held to fp64 with the fp32 bar of the
 other split kernels (< 1e-6 relative L2 and within 3x the fp32-MFMA kernel's error), at the model's shapes with
 several split-K chunks, a ragged last chunk and a chunk that ends inside a three-stage group; and it must be
-deterministic (two calls, same bits)."""
+deterministic (two calls, same bits).  (Taken where it beats h3p: W = 20, 128 outputs, at most 128 inputs.)"""
 import pytest
 import torch
 
@@ -23,13 +23,10 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("n,c0,c1,cout,h,dil", [
-    (37, 512, 0, 512, 10, 2),    # bridge.3: dilation 2, several chunks, ragged
-    (23, 256, 0, 512, 10, 2),    # bridge.0
-    (29, 512, 256, 256, 10, 1),  # dec3.conv1: virtual concat
-    (19, 128, 0, 256, 10, 1),    # enc3.conv1
-    (11, 256, 128, 128, 20, 1),  # dec2.conv1 (W = 20)
-    (9, 64, 0, 128, 20, 1),      # enc2.conv1: two input chunks
-    (1, 256, 0, 256, 10, 1),     # one sample: one short chunk
+    (9, 64, 0, 128, 20, 1),      # enc2.conv1: two input chunks, several split-K chunks, ragged
+    (13, 128, 0, 128, 20, 1),    # enc2.conv2 / dec2.conv2
+    (7, 64, 64, 128, 20, 1),     # a virtual concat (two 64-channel inputs)
+    (1, 128, 0, 128, 20, 1),     # one sample: one short chunk
 ])
 def test_wgrad_h3g_matches_fp64(n, c0, c1, cout, h, dil):
     from superresolution_for_pdes_amd import hipops as H
