@@ -407,6 +407,21 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                   const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
                   int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
                   void* workspace, size_t ws_bytes, hipStream_t stream);
+/* dx == NULL: the input gradient is not formed here -- workspace + n*hw floats then holds dm [n][c] (the
+ * channel branch's term) for srpde_att_pool_bn_bwd. */
+/* The gradient of an encoder block's output e = relu(bn(y)) that feeds both an AttentionGate (its x) and a 2x2
+ * max-pool (models.py:79-80, 90/93, 119-130), and that BatchNorm's backward reduction, in one pass: de = (dout * sa)
+ * * ca + dm (srpde_att_bwd's input gradient; dm from the srpde_att_bwd call with dx == NULL) plus dp [n*h/2*w/2][c]
+ * routed to each 2x2 window's first maximum of a (= e; srpde_maxpool2x2_bwd's choice), written once -- bit for bit
+ * srpde_att_bwd(dx) + srpde_maxpool2x2_bwd(accumulate); part [srpde_att_pool_bn_bwd_blocks()][c] float2 receives
+ * (sum dz, sum dz*xhat) per block (dz = de * [bn output > 0], xhat from y, mean, invstd, gamma, beta as in
+ * srpde_bn_relu_bwd) and da_max[block] max|de|: the `part` / `da_max` of srpde_bn_bwd_prepare, which then makes no
+ * pass over y and de of its own.  c / 4 a power of two <= 64; h, w even. */
+int srpde_att_pool_bn_bwd_blocks(int n, int h, int w, int c);
+int srpde_att_pool_bn_bwd(const float* dout, int lddo, const float* ca, const float* sa, const float* dm, const float* a,
+                          int lda, const float* dp, int lddp, const float* y, int ldy, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* de, int ldde, int n, int h,
+                          int w, int c, void* part, float* da_max, hipStream_t stream);
 /* The parameter-gradient half of srpde_att_bwd (dW1, db1, dW2, db2 of the channel MLP, dwg, dbg of
  * the spatial gate: fixed-order reductions over samples / pixel blocks of the per-sample rows it
  * left in `workspace`).  srpde_att_bwd with dw1 == NULL stops before it, so a caller can queue

@@ -770,6 +770,107 @@ __global__ __launch_bounds__(256) void bn_relu_gate_fwd_kernel(const float* __re
   if (amax) block_amax(mx, amax);
 }
 
+// The gradient of an encoder block's output e = relu(bn2(y)) in one pass, and that BatchNorm's backward reduction:
+// e feeds both the AttentionGate of its skip connection (models.py:119-130, :93 / :90) and the 2x2 max-pool of the
+// next block (:79-80), so de = (dout * sa) * ca + dm (the gate's input gradient, att_bwd_dx_kernel's expression) plus
+// the pooled gradient routed to each window's first maximum (maxpool2_bwd_px_kernel's comparison order).  Before:
+// att_bwd_dx wrote de, maxpool2_bwd read it back and rewrote it, and bn_bwd_reduce read it a third time; here it is
+// written once and the partial sums (sum dz, sum dz * xhat; bn_bwd_reduce_kernel's expressions, per thread in a
+// fixed pixel order) and the per-block max|de| leave with it.  de is equal bit for bit to the three-pass result.
+// Block (C / 4, 256 / (C / 4)): one channel quad of one pooling window per thread, a grid-stride walk over windows.
+__global__ __launch_bounds__(256) void att_pool_bn_bwd_kernel(
+    const float* __restrict__ dout, int lddo, const float* __restrict__ ca, const float* __restrict__ sa,
+    const float* __restrict__ dm, const float* __restrict__ a, int lda, const float* __restrict__ dp, int lddp,
+    const float* __restrict__ y, int ldy, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ de, int ldde, int H, int W,
+    unsigned npool, float2* __restrict__ part, float* __restrict__ da_max) {
+  extern __shared__ float4 red4[];   // [2][256]
+  const int C4 = blockDim.x, C = 4 * C4, c = threadIdx.x * 4;
+  const unsigned Wo = W >> 1, Ho = H >> 1, HW = (unsigned)(H * W);
+  const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+  const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+  const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+  const float4 b = *reinterpret_cast<const float4*>(beta + c);
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  float dmax = 0.f;
+  for (unsigned q = blockIdx.x * blockDim.y + threadIdx.y; q < npool; q += gridDim.x * blockDim.y) {
+    const unsigned ox = q % Wo, t = q / Wo, oy = t % Ho, n = t / Ho;
+    const size_t p0 = ((size_t)n * H + 2 * oy) * W + 2 * ox;
+    const size_t p[4] = {p0, p0 + 1, p0 + W, p0 + W + 1};
+    float4 v[4], d[4], yv[4];
+    float sv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = *reinterpret_cast<const float4*>(a + p[k] * lda + c);
+      d[k] = *reinterpret_cast<const float4*>(dout + p[k] * lddo + c);
+      yv[k] = *reinterpret_cast<const float4*>(y + p[k] * ldy + c);
+      sv[k] = sa[p[k]];
+    }
+    const float4 gp = *reinterpret_cast<const float4*>(dp + (size_t)q * lddp + c);
+    const float4 cav = *reinterpret_cast<const float4*>(ca + (size_t)n * C + c);
+    const float4 dmv = *reinterpret_cast<const float4*>(dm + (size_t)n * C + c);
+    (void)HW;
+    float4 o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float s = sv[k];
+      o[k].x = (d[k].x * s) * cav.x + dmv.x; o[k].y = (d[k].y * s) * cav.y + dmv.y;
+      o[k].z = (d[k].z * s) * cav.z + dmv.z; o[k].w = (d[k].w * s) * cav.w + dmv.w;
+    }
+#define ARG(X)                                                     \
+  {                                                                \
+    int am = 0; float mv = v[0].X;                                 \
+    if (v[1].X > mv) { mv = v[1].X; am = 1; }                      \
+    if (v[2].X > mv) { mv = v[2].X; am = 2; }                      \
+    if (v[3].X > mv) { mv = v[3].X; am = 3; }                      \
+    o[am].X += gp.X;                                               \
+  }
+    ARG(x) ARG(y) ARG(z) ARG(w)
+#undef ARG
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      *reinterpret_cast<float4*>(de + p[k] * ldde + c) = o[k];
+      dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(o[k].x), fabsf(o[k].y)), fmaxf(fabsf(o[k].z), fabsf(o[k].w))));
+      float xh, dz;
+#define BN_ACC(X)                                              \
+  xh = (yv[k].X - mu.X) * is.X;                                \
+  dz = (xh * g.X + b.X > 0.f) ? o[k].X : 0.f;                  \
+  s1.X += dz;                                                  \
+  s2.X += dz * xh;
+      BN_ACC(x) BN_ACC(y) BN_ACC(z) BN_ACC(w)
+#undef BN_ACC
+    }
+  }
+  const int tid = threadIdx.y * C4 + threadIdx.x;
+  red4[tid] = s1;
+  red4[256 + tid] = s2;
+  __syncthreads();
+  if (threadIdx.y == 0) {
+    float4 t1 = make_float4(0.f, 0.f, 0.f, 0.f), t2 = t1;
+    for (int r = 0; r < (int)blockDim.y; ++r) {
+      const float4 u1 = red4[r * C4 + threadIdx.x], u2 = red4[256 + r * C4 + threadIdx.x];
+      t1.x += u1.x; t1.y += u1.y; t1.z += u1.z; t1.w += u1.w;
+      t2.x += u2.x; t2.y += u2.y; t2.z += u2.z; t2.w += u2.w;
+    }
+    float2* o2 = part + (size_t)blockIdx.x * C + c;
+    o2[0] = make_float2(t1.x, t2.x); o2[1] = make_float2(t1.y, t2.y);
+    o2[2] = make_float2(t1.z, t2.z); o2[3] = make_float2(t1.w, t2.w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+  __syncthreads();
+  float* wmx = reinterpret_cast<float*>(red4);
+  if ((tid & 63) == 0) wmx[tid >> 6] = dmax;
+  __syncthreads();
+  if (tid == 0) da_max[blockIdx.x] = fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]));
+}
+
+static int att_pool_blocks(int n, int h, int w, int c) {
+  const long long npool = (long long)n * (h / 2) * (w / 2);
+  const int py = 256 / (c / 4);
+  return (int)std::min<long long>(1024, (npool + py - 1) / py);
+}
+
 static int bwd_blocks(long long P, int C, int* rows_per_blk) {
   // ~1024 blocks; rows per block a multiple of the rows a block covers per sweep
   const int rs = 256 / (C >> 2);
@@ -1064,6 +1165,27 @@ int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, con
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(1), dim3(256), 0, stream, sdz, sdzx, P, C, invstd, gamma,
                      (flags & SRPDE_BN_EVAL) ? 1 : 0, da_max, n_da_max, m1, m2, dbias, dy_amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_bwd_prepare(coef)");
+  return 0;
+}
+
+int srpde_att_pool_bn_bwd_blocks(int n, int h, int w, int c) { return att_pool_blocks(n, h, w, c); }
+
+int srpde_att_pool_bn_bwd(const float* dout, int lddo, const float* ca, const float* sa, const float* dm, const float* a,
+                          int lda, const float* dp, int lddp, const float* y, int ldy, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* de, int ldde, int n, int h,
+                          int w, int c, void* part, float* da_max, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && ca && sa && dm && a && dp && y && mean && invstd && gamma && beta && de && part && da_max,
+                  "srpde_att_pool_bn_bwd: null argument");
+  const int c4 = c / 4;
+  SRPDE_CHECK_ARG(c % 4 == 0 && c4 >= 1 && c4 <= 64 && (c4 & (c4 - 1)) == 0 && h % 2 == 0 && w % 2 == 0 &&
+                      lddo % 4 == 0 && lda % 4 == 0 && lddp % 4 == 0 && ldy % 4 == 0 && ldde % 4 == 0 &&
+                      (long long)n * h * w < (1LL << 31),
+                  "srpde_att_pool_bn_bwd: c / 4 a power of two <= 64, even h / w, row strides multiples of 4");
+  const int nb = att_pool_blocks(n, h, w, c);
+  hipLaunchKernelGGL(att_pool_bn_bwd_kernel, dim3(nb), dim3(c4, 256 / c4), 2 * 256 * sizeof(float4), stream, dout,
+                     lddo, ca, sa, dm, a, lda, dp, lddp, y, ldy, mean, invstd, gamma, beta, de, ldde, h, w,
+                     (unsigned)(n * (h / 2) * (w / 2)), static_cast<float2*>(part), da_max);
+  SRPDE_LAUNCH_CHECK("srpde_att_pool_bn_bwd");
   return 0;
 }
 

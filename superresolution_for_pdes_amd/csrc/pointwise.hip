@@ -1334,7 +1334,7 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                   const float* ca, const float* sa, float* dx, int lddx, int dx_accumulate, float* dg, int lddg,
                   int dg_accumulate, float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg,
                   void* workspace, size_t ws_bytes, hipStream_t stream) {
-  SRPDE_CHECK_ARG(dout && x && g && dx && workspace, "srpde_att_bwd: null");
+  SRPDE_CHECK_ARG(dout && x && g && workspace, "srpde_att_bwd: null");
   SRPDE_CHECK_ARG(c % 32 == 0 && gc % 4 == 0, "srpde_att_bwd: channel counts");
   if (ws_bytes < srpde_att_bwd_workspace_size(n, hw, c, gc)) {
     set_error("srpde_att_bwd: workspace too small");
@@ -1364,9 +1364,11 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                        w1, w2, m, hbuf, ca, dm, dw1r, db1r, dw2r, db2r);
     SRPDE_LAUNCH_CHECK("srpde_att_bwd(channel)");
   }
-  hipLaunchKernelGGL(att_bwd_dx_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, lddo, ca, sa, dm,
-                     dx, lddx, P, hw, c, dx_accumulate);
-  SRPDE_LAUNCH_CHECK("srpde_att_bwd(dx)");
+  if (dx != nullptr) {   // else the caller forms dx later from workspace's dm (srpde_att_pool_bn_bwd)
+    hipLaunchKernelGGL(att_bwd_dx_kernel, dim3(grid_for(P * (c / 4))), dim3(256), 0, stream, dout, lddo, ca, sa, dm,
+                       dx, lddx, P, hw, c, dx_accumulate);
+    SRPDE_LAUNCH_CHECK("srpde_att_bwd(dx)");
+  }
   if (dg != nullptr) {   // else the caller folds dg = dsa * wg into its consumer (workspace[0, P) = dsa)
     hipLaunchKernelGGL(att_bwd_gating_kernel, dim3(grid_for(P * (gc / 4))), dim3(256), 0, stream, dsa, wg, dg, lddg,
                        P, gc, dg_accumulate);

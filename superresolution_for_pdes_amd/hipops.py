@@ -830,12 +830,14 @@ def att_gate_fwd(x, g, n, hw, chan, wg, bg, out=None):
 
 
 def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg,
-            defer_params=False, want_dsa=False):
+            defer_params=False, want_dsa=False, want_dm=False):
     """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None, or
     ``want_dsa``) is the gating gradient's per-pixel factor d loss / d(spatial pre-activation), for
     upsample_bwd(gate=...); the spatial bias gradient is its sum; ``params`` (when
     ``defer_params``) is a callable that launches the parameter-gradient reductions on the
-    current stream, to be queued after this call (reads ``ws``, ``g``, ``m``, ``hb``)."""
+    current stream, to be queued after this call (reads ``ws``, ``g``, ``m``, ``hb``).
+    ``dx=None``: the input gradient is left to att_pool_bn_bwd; ``want_dm`` then appends the channel
+    branch's term dm [n, c] (a view into the workspace) to the returned tuple."""
     m, hb, ca, sa = saved
     c, gc = x.shape[1], g.shape[1]
     ws_bytes = int(query("srpde_att_bwd_workspace_size", n, hw, c, gc))
@@ -843,7 +845,7 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
     pdo, lddo = _pl(dout)
     px, ldx = _pl(x)
     pg, ldg = _pl(g)
-    pdx, lddx = _pl(dx)
+    pdx, lddx = _pl(dx) if dx is not None else (0, 0)
     pdg, lddg = _pl(dg) if dg is not None else (0, 0)
     pgrads = (dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr())
     call("srpde_att_bwd", pdo, lddo, px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), w2.data_ptr(), wg.data_ptr(),
@@ -857,7 +859,30 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
         params.keep = (ws,)
     # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
     dsa = ws[:4 * x.shape[0]].view(torch.float32) if dg is None or want_dsa else None
+    if want_dm:   # workspace [P floats of dsa | n * c floats of dm | ...] (srpde_att_bwd_workspace_size)
+        P = x.shape[0]
+        return dsa, params, ws[4 * P:4 * (P + n * c)].view(torch.float32).view(n, c)
     return dsa, params
+
+
+def att_pool_bn_bwd(dout, ca, sa, dm, a, dp, de, y, mean, invstd, gamma, beta, n, h, w):
+    """srpde_att_pool_bn_bwd: de = the AttentionGate's input gradient ((dout * sa) * ca + dm, att_bwd's with
+    dx=None) + the max-pool backward of dp over a, written once, and the BatchNorm (y, mean, invstd, gamma,
+    beta; + ReLU) backward's partial sums of de -> (part [blocks, c, 2], da_max [blocks]) for
+    bn_bwd_prepare(part=..., da_max=...)."""
+    c = a.shape[1]
+    nb = int(query("srpde_att_pool_bn_bwd_blocks", n, h, w, c))
+    part = empty(nb, c, 2, device=a.device)
+    da_max = empty(nb, device=a.device)
+    pdo, lddo = _pl(dout)
+    pa, lda = _pl(a)
+    pdp, lddp = _pl(dp)
+    py, ldy = _pl(y)
+    pde, ldde = _pl(de)
+    call("srpde_att_pool_bn_bwd", pdo, lddo, ca.data_ptr(), sa.data_ptr(), dm.data_ptr(), pa, lda, pdp, lddp, py, ldy,
+         mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pde, ldde, n, h, w, c,
+         part.data_ptr(), da_max.data_ptr(), stream_ptr())
+    return part, da_max
 
 
 # ------------------------------------- head ----------------------------------------

@@ -711,18 +711,41 @@ def _att_channel_early(att, x, n, hw):
     return H.att_channel_fwd(x, n, hw, c1.weight, c1.bias, c3.weight, c3.bias), None
 
 
-def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None):
+def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None, defer_dx=False):
     """``dg=None``: the gating gradient is not applied; returns the gate for upsample_bwd.
-    ``wq``: the parameter-gradient reductions go to the weight-gradient side stream."""
+    ``wq``: the parameter-gradient reductions go to the weight-gradient side stream.
+    ``defer_dx`` (``dx`` None): the input gradient is formed later by att_pool_bn_bwd; returns (gate, dm)."""
     c1, c3, s0 = _att_params(att)
-    dsa, params = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
-                            grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
-                            grads[s0.bias], defer_params=wq is not None, want_dsa=DEBUG_TAPS is not None)
+    out = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
+                    grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
+                    grads[s0.bias], defer_params=wq is not None, want_dsa=DEBUG_TAPS is not None, want_dm=defer_dx)
+    dsa, params = out[0], out[1]
     if DEBUG_TAPS is not None:
         _tap("dsa_pre:" + getattr(att, "_srpde_name", "?"), dsa)
     if params is not None:
         wq.submit(params, params.keep)
-    return None if dsa is None or dg is not None else (dsa, s0.weight)
+    gate = None if dsa is None or dg is not None else (dsa, s0.weight)
+    return (gate, out[2]) if defer_dx else gate
+
+
+def _fuse_enc_out(blk_saved, c, w):
+    """The encoder output's gradient (gate input + max-pool backward) and its BN backward reduction in one pass
+    (srpde_att_pool_bn_bwd): train mode, c / 4 a power of two <= 64 (_FUSE_ENC_OUT False: three passes)"""
+    s2 = blk_saved[1]
+    return _FUSE_ENC_OUT and s2[6] and c in (64, 128, 256) and w % 2 == 0
+
+
+def _enc_out_bwd(blk, blk_saved, att_saved, dout, dm, e, dp, de, n, h, w):
+    """de = the gate's input gradient + the max-pool backward of dp; -> (partials, max|de| slots) of blk.bn2"""
+    _, s2 = blk_saved
+    _, _, y, mean, invstd, _, _ = s2
+    _, _, ca, sa = att_saved
+    return H.att_pool_bn_bwd(dout, ca, sa, dm, e, dp, de, y, mean, invstd, blk.bn2.weight, blk.bn2.bias, n, h, w)
+
+
+# the encoder outputs' gradient in one pass with their BN backward reduction (False: the gate's input gradient,
+# the max-pool backward and the reduction as three passes; tests/test_gpu_fused_bwd.py compares the two)
+_FUSE_ENC_OUT = True
 
 
 def check_input(x):
@@ -840,8 +863,13 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     _tap("e1a", dcat1[:, 128:])
     ready("dec1")
     de1 = H.empty(P1, 64, device=dev)
-    # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below
-    gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, de1, False, None, True, wq=wq)
+    # the gating gradient (into dcat1[:, :128]) is folded into the upsample backward below; with the encoder-output
+    # fusion the gate's input gradient is formed together with the max-pool backward into de1 (enc1's turn, below)
+    fuse1 = _fuse_enc_out(S.enc1, 64, w)
+    gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, None if fuse1 else de1, False, None, True,
+                    wq=wq, defer_dx=fuse1)
+    if fuse1:
+        gate, dm1 = gate
     ready("att1")
     dd2 = H.empty(P2, 128, device=dev)
     H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate)
@@ -854,7 +882,11 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     ready("dec2")
     de2 = H.empty(P2, 128, device=dev)
     # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
-    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, de2, False, None, True, wq=wq)
+    fuse2 = _fuse_enc_out(S.enc2, 128, w2)
+    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, None if fuse2 else de2, False, None,
+                    True, wq=wq, defer_dx=fuse2)
+    if fuse2:
+        gate, dm2 = gate
     ready("att2")
     dd3 = H.empty(P3, 256, device=dev)
     H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate)
@@ -880,15 +912,23 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     dp2 = H.empty(P3, 128, device=dev)
     _block_bwd(m.enc3, S.enc3, de3, n, h3, w3, grads, slots, dp2, wq=wq)
     ready("enc3")
-    H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
+    part = None
+    if fuse2:
+        part = _enc_out_bwd(m.enc2, S.enc2, S.att2, dcat2[:, 256:], dm2, S.e2, dp2, de2, n, h2, w2)
+    else:
+        H.maxpool_bwd(S.e2, dp2, de2, n, h2, w2, True)
     _tap("e2", de2)
     dp1 = H.empty(P2, 64, device=dev)
-    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1, wq=wq)
+    _block_bwd(m.enc2, S.enc2, de2, n, h2, w2, grads, slots, dp1, wq=wq, part=part)
     ready("enc2")
-    H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
+    part = None
+    if fuse1:
+        part = _enc_out_bwd(m.enc1, S.enc1, S.att1, dcat1[:, 128:], dm1, S.e1, dp1, de1, n, h, w)
+    else:
+        H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
     _tap("e1", de1)
     dx4 = H.empty(P1, S.x4.shape[1], device=dev) if want_dx else None
-    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, dx4, wq=wq)
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, dx4, wq=wq, part=part)
     ready("enc1")
     if wq is not None:
         wq.join()
