@@ -17,6 +17,9 @@
  *    between consecutive pixels, so channel slices of a wider tensor (virtual concat) need
  *    no copy.  Channel counts and ld must be multiples of 4; pointers 16-byte aligned.
  *  - Every call is stream-ordered on `stream` (on ROCm torch.cuda.current_stream().cuda_stream).
+ *  - The library holds no global mutable state and reads no environment: every choice (kernel family,
+ *    test hooks) is an argument of the call, so calls are re-entrant from any thread.  (The one piece of
+ *    per-thread state is diagnostic: srpde_last_error / srpde_last_kernel.)
  *  - Return: 0 on success, negative on a bad argument (-1 arg, -2 shape, -3 alignment,
  *    -4 workspace too small), positive hipError_t on a launch failure.  srpde_last_error()
  *    returns the thread-local message of the last failure.
@@ -47,8 +50,21 @@ typedef struct ihipStream_t* hipStream_t;
  *   8  srpde_conv_h3_stats_rows_for, srpde_conv_h5_set (the h5 forward writes 80-row statistics),
  *      srpde_conv_head_eval_supported, srpde_last_kernel
  *   9  srpde_conv_wgrad_h3x, srpde_conv_wgrad_h3x_supported, srpde_bn_train_finalize_ws,
- *      srpde_bn_finalize_workspace_size */
-#define SRPDE_ABI_VERSION 9
+ *      srpde_bn_finalize_workspace_size
+ *  10  no global state: srpde_conv_h5_set / _h4_set / _h3r_set and srpde_poisson_debug_abort removed; the kernel
+ *      family is SRPDE_FAM_* bits of srpde_conv_fwd_h3's / _presplit's accumulate argument and of
+ *      srpde_conv_h3_stats_rows_for's new flags argument, the grid-CG abort hook a negative rtol;
+ *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL */
+#define SRPDE_ABI_VERSION 10
+
+/* Kernel-family bits (per call; bit 0 of the same argument is the accumulate flag): the forward / dgrad
+ * families compute the same outputs, statistics and stored splits bit for bit, so these only route a call to
+ * another kernel -- tests compare the families, tuning times them.  SRPDE_FAM_NO_H5: not the W = 40 h5 kernel
+ * (nor out_conv2's 16-output kernel); SRPDE_FAM_NO_H4: not the h4 one-tap-ring kernel (W = 10 / 20 / 40 tiles);
+ * SRPDE_FAM_NO_H3R: not the 4-wave, two-workgroups-per-CU kernel for <= 64-channel tiles. */
+#define SRPDE_FAM_NO_H5 2
+#define SRPDE_FAM_NO_H4 4
+#define SRPDE_FAM_NO_H3R 8
 
 const char* srpde_last_error(void);
 /* Name of the main kernel the last conv entry point (srpde_conv_fwd*, srpde_conv_dgrad_h3_bnb, srpde_conv_wgrad*,
@@ -96,26 +112,11 @@ int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize)
  * hold ceil(P / rows) blocks); the other conv families use srpde_conv_stats_rows_per_block. */
 int srpde_conv_h3_stats_rows(void);
 /* Rows per BatchNorm-statistics block srpde_conv_fwd_h3 writes for the FORWARD of this shape (input
- * channels c0 + c1 -> cout at h x w, dilation dil): 80 where the h5 kernel takes it (w = 40, h % 8 == 0,
- * cout 64 or 32, c0 + c1 a multiple of 64), else srpde_conv_h3_stats_rows().  Dgrad partials (bn_part)
- * keep srpde_conv_h3_stats_rows(). */
-int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil);
-/* Kernel choice of srpde_conv_fwd_h3 for the shapes above: 1 = the h5 kernel (conv_h5.hip: tiles of 8
- * image rows, weights in registers; default), 0 = h4 / h3.  The conv outputs are equal bit for bit; the
- * statistics come in 80-row instead of 128-row blocks (allocate them with the current choice).  Returns
- * the previous value (on < 0: query only).  Tuning and tests. */
-int srpde_conv_h5_set(int on);
-/* Kernel choice of srpde_conv_fwd_h3 for output tiles of <= 64 channels: 1 = the register-staged
- * 4-wave kernel, two workgroups per CU (default; SRPDE_H3R=0 turns it off), 0 = the 8-wave
- * kernel.  Both compute the same outputs, statistics and stored splits bit for bit (outside a
- * K-split tail).  Returns the previous value.  Tuning and tests. */
-int srpde_conv_h3r_set(int on);
-/* Kernel choice of srpde_conv_fwd_h3 / srpde_conv_fwd_h3_presplit for 128-column output tiles
- * (cout % 128 == 0) at W = 10 (dilation 1 or 2) and W = 20 (dilation 1): 1 = the h4 kernel
- * (conv_h4.hip: one-tap weight ring, fragments read a tap ahead; default, SRPDE_H4=0 turns it
- * off), 0 = the h3 8-wave kernel.  Bit-identical outputs, statistics and stored splits.  Returns
- * the previous value (on < 0: a query, nothing changes).  Tuning and tests. */
-int srpde_conv_h4_set(int on);
+ * channels c0 + c1 -> cout at h x w, dilation dil) and kernel-family bits `flags` (those the forward call
+ * will pass): 80 where the h5 kernel takes it (w = 40, h % 8 == 0, cout 64 or 32, c0 + c1 a multiple of 64,
+ * no SRPDE_FAM_NO_H5), else srpde_conv_h3_stats_rows().  Dgrad partials (bn_part) keep
+ * srpde_conv_h3_stats_rows(). */
+int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil, int flags);
 int srpde_split_weights_h3(const float* w, void* planes, int* wexp, int rows, int K, hipStream_t stream);
 int srpde_absmax(const float* x, int ldx, int c, long long P, unsigned* amax, hipStream_t stream);
 /* every conv layer's forward and dgrad h3 planes in one launch from torch's [Cout][Cin][3][3]
@@ -160,6 +161,8 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
                       const float* x1_ca, const float* x1_sa, const float* x0_up, int up_ld, int up_h, int up_w,
                       void* workspace, size_t ws_bytes, hipStream_t stream);
+/* accumulate: bit 0 = y += conv; the SRPDE_FAM_* bits route the call away from a kernel family (tests /
+ * tuning: the families' outputs are equal bit for bit); srpde_conv_fwd_h3_presplit reads it the same way. */
 /* x1_ca [n][c1] / x1_sa [P] (nullable, together, c1 > 0): the second input is an AttentionGate's
  * input x (models.py:119-130) and the conv reads its gated output (x * ca[sample][c]) * sa[pixel]
  * (srpde_att_apply_fwd's expression, formed in the operand transform; xsplit_out and the statistics
@@ -468,14 +471,13 @@ size_t srpde_poisson_workspace_size(int B, int n);
  * points below (textbook CG) and polls convergence every 128 iterations, synchronising `stream`. */
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* (Test hook: rtol < 0 solves to |rtol| but every cooperative grid-CG launch starts aborted -- iters_out = -1 for
+ * its problems, u undefined -- to exercise a caller's handling of a stuck grid barrier; poisson.solve_batched
+ * raises.  The LDS solver, n <= srpde_poisson_lds_max_n(), has no barrier to abort.) */
 /* Problems per cooperative grid-CG launch at this n with its largest (8192-point) blocks; 0 when one
  * problem does not fit the co-resident grid or n > 1024 (a block's two halo rows, the neighbours'
  * edge rows, take at most two points per thread). */
 int srpde_poisson_coop_problems(int n);
-/* Test hook: 1 = every following cooperative grid-CG launch starts aborted (iters_out = -1 for its
- * problems, u undefined), 0 = normal.  Returns the previous setting.  Exercises callers' handling of
- * a stuck grid barrier (poisson.solve_batched raises). */
-int srpde_poisson_debug_abort(int on);
 int srpde_poisson_cg_lds(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                          int* iters, double* resid, hipStream_t stream);
 int srpde_poisson_cg_grid_init(const double* f, const double* theta, int B, int n, void* ws, size_t ws_bytes,

@@ -817,13 +817,17 @@ __global__ __launch_bounds__(256) void att_pool_bn_bwd_kernel(
       o[k].x = (d[k].x * s) * cav.x + dmv.x; o[k].y = (d[k].y * s) * cav.y + dmv.y;
       o[k].z = (d[k].z * s) * cav.z + dmv.z; o[k].w = (d[k].w * s) * cav.w + dmv.w;
     }
+    // (the routed add by selects, not o[am]: a dynamic index put o in scratch)
 #define ARG(X)                                                     \
   {                                                                \
     int am = 0; float mv = v[0].X;                                 \
     if (v[1].X > mv) { mv = v[1].X; am = 1; }                      \
     if (v[2].X > mv) { mv = v[2].X; am = 2; }                      \
     if (v[3].X > mv) { mv = v[3].X; am = 3; }                      \
-    o[am].X += gp.X;                                               \
+    o[0].X = am == 0 ? o[0].X + gp.X : o[0].X;                     \
+    o[1].X = am == 1 ? o[1].X + gp.X : o[1].X;                     \
+    o[2].X = am == 2 ? o[2].X + gp.X : o[2].X;                     \
+    o[3].X = am == 3 ? o[3].X + gp.X : o[3].X;                     \
   }
     ARG(x) ARG(y) ARG(z) ARG(w)
 #undef ARG

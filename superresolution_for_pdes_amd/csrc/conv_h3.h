@@ -128,16 +128,18 @@ static int launch_tail_fixup(const ConvParams& p, hipStream_t st) {
 bool h4_supported(int w, int dil, int cout, bool bnb);
 bool h4_up_supported(int w, int dil, int cout);   // the upsampled-input forward (H3Args::up_src)
 int launch_fwd_h4(const ConvParams& p, const H3Args& h, bool pre, hipStream_t st, void* ws, size_t ws_bytes);
-bool h4_on();
+
+// kernel-family bits of srpde_conv_fwd_h3's / srpde_conv_fwd_h3_presplit's `accumulate` argument (bit 0 is the
+// accumulate flag itself) and of srpde_conv_h3_stats_rows_for's `flags`: per call, no library state.  The families
+// compute the same outputs bit for bit; the bits let tests compare them and tuning time them.
+constexpr int FAM_NO_H5 = 2, FAM_NO_H4 = 4, FAM_NO_H3R = 8, FAM_MASK = FAM_NO_H5 | FAM_NO_H4 | FAM_NO_H3R;
 
 // the 16-output forward of out_conv2 in training (conv_head.hip): c0 == 32, c1 == 0, cout == 16, w <= 63
-// (with the h5 kernels: srpde_conv_h5_set(0) routes it back to h3r)
+// (taken with the h5 kernels: FAM_NO_H5 routes it back to h3r)
 bool n16_supported(int c0, int c1, int cout, int w, int dil);
 int launch_fwd_n16(const ConvParams& p, const H3Args& h, hipStream_t st);
 // h5 (conv_h5.hip): the W = 40 forward into 64 / 32 channels (8-row tiles, weight taps through an LDS ring)
-bool h5_on();
 bool h5_supported(int c0, int c1, int cout, int h, int w, int dil);
-int h5_set(int on);
 int h5_stats_rows();
 int launch_fwd_h5(const ConvParams& p, const H3Args& h, hipStream_t st);
 

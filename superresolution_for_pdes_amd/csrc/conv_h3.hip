@@ -2108,34 +2108,10 @@ static size_t h3r_lds(int bn, int arows, int tps) {   // zero row | S | weight r
   return 128 + (size_t)arows * 128 + (size_t)H3R_NB * tps * 2 * bn * 64 + 1024;
 }
 static int h3r_tps(int bn) { (void)bn; return 1; }
-static std::atomic<int> g_h3r{-1};
-static bool h3r_on() {
-  int v = g_h3r.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("SRPDE_H3R");   // tuning/diagnostics: 0 = the 8-wave kernel for every shape
-    v = (!e || atoi(e) != 0) ? 1 : 0;
-    int expect = -1;
-    g_h3r.compare_exchange_strong(expect, v);
-    v = g_h3r.load(std::memory_order_relaxed);
-  }
-  return v != 0;
-}
-static std::atomic<int> g_h4{-1};
-bool h4_on() {
-  int v = g_h4.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("SRPDE_H4");   // A/B switch between two bit-identical kernels: 0 = the h3 8-wave kernel
-    v = (!e || atoi(e) != 0) ? 1 : 0;
-    int expect = -1;
-    g_h4.compare_exchange_strong(expect, v);
-    v = g_h4.load(std::memory_order_relaxed);
-  }
-  return v != 0;
-}
 // the h3r kernel takes this shape: an output tile of <= 64 channels, a halo tile that fits the
 // registers, and two workgroups' LDS per CU
-static bool h3r_fits(int bn, int arows) {
-  return h3r_on() && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
+static bool h3r_fits(int bn, int arows, int fam) {
+  return !(fam & FAM_NO_H3R) && bn <= 64 && arows <= H3R_NTK * 256 / 4 && 2 * h3r_lds(bn, arows, h3r_tps(bn)) <= 160 * 1024;
 }
 
 template <int BN, int TPS, bool PRE = false>
@@ -2389,22 +2365,8 @@ extern "C" {
 
 int srpde_conv_h3_stats_rows(void) { return H3_SRB; }
 
-int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil) {
-  return h5_supported(c0, c1, cout, h, w, dil) ? h5_stats_rows() : H3_SRB;
-}
-
-int srpde_conv_h5_set(int on) { return h5_set(on); }
-
-int srpde_conv_h4_set(int on) {
-  const int prev = h4_on() ? 1 : 0;
-  if (on >= 0) g_h4.store(on ? 1 : 0);   // on < 0: query only
-  return prev;
-}
-
-int srpde_conv_h3r_set(int on) {
-  const int prev = h3r_on() ? 1 : 0;
-  g_h3r.store(on ? 1 : 0);
-  return prev;
+int srpde_conv_h3_stats_rows_for(int c0, int c1, int cout, int h, int w, int dil, int flags) {
+  return !(flags & FAM_NO_H5) && h5_supported(c0, c1, cout, h, w, dil) ? h5_stats_rows() : H3_SRB;
 }
 
 int srpde_conv_h3_supported(int c0, int c1, int cout, int w, int dil, int ksize) {
@@ -2451,10 +2413,14 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
                       const float* ep_invstd, const float* ep_gamma, const float* ep_beta, unsigned* ep_amax,
                       const float* x1_ca, const float* x1_sa, const float* x0_up, int up_ld, int up_h, int up_w,
                       void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG((accumulate & ~(1 | FAM_MASK)) == 0, "srpde_conv_fwd_h3: accumulate: bit 0 plus family bits only");
+  const int fam = accumulate & FAM_MASK;
+  accumulate &= 1;
+  const bool h5ok = !(fam & FAM_NO_H5), h4ok = !(fam & FAM_NO_H4);
   SRPDE_CHECK_ARG(x0 && wsplit && wexp && y && amax0, "srpde_conv_fwd_h3: null pointer");
   SRPDE_CHECK_ARG(x0_up == nullptr || (up_h * 2 == h && up_w * 2 == w && up_ld % 4 == 0 && up_ld >= c0 &&
                                        aligned16(x0_up) && in_scale == nullptr && ksize == 3 && sign == 1 &&
-                                       h4_on() && h4_up_supported(w, dil, cout)),
+                                       h4ok && h4_up_supported(w, dil, cout)),
                   "srpde_conv_fwd_h3: an upsampled x0 (x0_up) needs h = 2 up_h, w = 2 up_w, no in_scale, the forward, "
                   "and a shape the h4 kernel is instantiated for (W 20 / 128 columns, W 40 / 64 columns)");
   SRPDE_CHECK_ARG((x1_ca == nullptr) == (x1_sa == nullptr) && (x1_ca == nullptr || c1 > 0),
@@ -2512,10 +2478,10 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   p.ep_amax = ep_mean != nullptr ? ep_amax : nullptr;
   // out_conv2's shape in training (32 -> 16, no epilogue BN): the 16-output kernel, 128-row statistics
   if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr && ep_mean == nullptr && !accumulate &&
-      n16_supported(c0, c1, cout, w, dil) && ldx0 % 4 == 0 && aligned16(x0))
+      h5ok && n16_supported(c0, c1, cout, w, dil) && ldx0 % 4 == 0 && aligned16(x0))
     return launch_fwd_n16(p, a, stream);
   // h5 takes the forward of the shapes srpde_conv_h3_stats_rows_for reports 80-row statistics for
-  if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr &&
+  if (x0_up == nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr && h5ok &&
       h5_supported(c0, c1, cout, h, w, dil)) {
     if (ldy % 4 == 0 && aligned16(y) && (c1 == 0 || ldx1 % 4 == 0)) return launch_fwd_h5(p, a, stream);
     SRPDE_CHECK_ARG(stats == nullptr, "srpde_conv_fwd_h3: the h5 shape (w=40, cout=%d) needs a 16-byte aligned y "
@@ -2523,15 +2489,15 @@ int srpde_conv_fwd_h3(const float* x0, int c0, int ldx0, const float* x1, int c1
   }
   // the eval decoder's dec1.conv1 (upsampled x0, gated x1, BN + ReLU epilogue) at W = 40: h5's UP variant
   if (x0_up != nullptr && sign == 1 && bn_part == nullptr && out_max == nullptr && ep_mean != nullptr &&
-      stats == nullptr && x1_ca != nullptr && !accumulate && h5_supported(c0, c1, cout, h, w, dil) && ldy % 4 == 0 &&
+      stats == nullptr && x1_ca != nullptr && !accumulate && h5ok && h5_supported(c0, c1, cout, h, w, dil) && ldy % 4 == 0 &&
       aligned16(y) && (c1 == 0 || ldx1 % 4 == 0))
     return launch_fwd_h5(p, a, stream);
-  SRPDE_CHECK_ARG(x0_up == nullptr || stats == nullptr || !h5_supported(c0, c1, cout, h, w, dil),
+  SRPDE_CHECK_ARG(x0_up == nullptr || stats == nullptr || !h5ok || !h5_supported(c0, c1, cout, h, w, dil),
                   "srpde_conv_fwd_h3: an upsampled x0 with statistics at an h5 shape (w=40, cout=%d): the statistics "
                   "blocks would not be the srpde_conv_h3_stats_rows_for ones", cout);
-  if (x0_up != nullptr || (h4_on() && h4_supported(w, dil, cout, false)))
+  if (x0_up != nullptr || (h4ok && h4_supported(w, dil, cout, false)))
     return launch_fwd_h4(p, a, false, stream, workspace, ws_bytes);
-  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
+  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows, fam)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1>(p, a, stream, workspace, ws_bytes);
   }
@@ -2557,6 +2523,9 @@ int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, 
                                const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                                const float* bn_beta, void* bn_part, float* out_max, void* workspace, size_t ws_bytes,
                                hipStream_t stream) {
+  SRPDE_CHECK_ARG((accumulate & ~(1 | FAM_MASK)) == 0, "srpde_conv_fwd_h3_presplit: accumulate: bit 0 plus family bits");
+  const int fam = accumulate & FAM_MASK;
+  accumulate &= 1;
   SRPDE_CHECK_ARG(xsplit && amax && wsplit && wexp && y, "srpde_conv_fwd_h3_presplit: null pointer");
   SRPDE_CHECK_ARG(n > 0 && h > 0 && w > 0 && cout > 0 && (sign == 1 || sign == -1), "srpde_conv_fwd_h3_presplit: bad shape");
   SRPDE_CHECK_ARG(srpde_conv_h3_supported(c, 0, cout, w, dil, ksize),
@@ -2589,8 +2558,9 @@ int srpde_conv_fwd_h3_presplit(const void* xsplit, int c, const unsigned* amax, 
   a.xsplit = nullptr;
   a.in_scale = nullptr; a.in_shift = nullptr;
   a.wide = ldy % 4 == 0 && aligned16(y);
-  if (h4_on() && h4_supported(w, dil, cout, false)) return launch_fwd_h4(p, a, true, stream, workspace, ws_bytes);
-  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows)) {
+  if (!(fam & FAM_NO_H4) && h4_supported(w, dil, cout, false))
+    return launch_fwd_h4(p, a, true, stream, workspace, ws_bytes);
+  if (h3r_fits(h3_bn(h3_cfg(cout)), a.arows, fam)) {
     if (h3_cfg(cout) == 2) return launch_fwd_h3r<64, 1, true>(p, a, stream, workspace, ws_bytes);
     return launch_fwd_h3r<32, 1, true>(p, a, stream, workspace, ws_bytes);
   }

@@ -643,19 +643,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h5_kernel(ConvParams p, H3Arg
 }
 
 // ---------------------------------- host side ---------------------------------------
-static std::atomic<int> g_h5{1};
-
-bool h5_on() { return g_h5.load(std::memory_order_relaxed) != 0; }
-int h5_set(int on) {
-  const int prev = h5_on() ? 1 : 0;
-  if (on >= 0) g_h5.store(on ? 1 : 0);
-  return prev;
-}
-
 // the shapes h5 takes (forward; an upsampled input: h5_up_supported): W = 40, H a multiple of 8, Cout 64 or 32, input
 // channels a multiple of 64 (chunk pairs), the first input a multiple of 32
 bool h5_supported(int c0, int c1, int cout, int h, int w, int dil) {
-  return h5_on() && w == kW && h > 0 && h % kTR == 0 && dil == 1 && (cout == 64 || cout == 32) && c0 % 32 == 0 &&
+  return w == kW && h > 0 && h % kTR == 0 && dil == 1 && (cout == 64 || cout == 32) && c0 % 32 == 0 &&
          c1 % 32 == 0 && (c0 + c1) % 64 == 0 && (c0 + c1) > 0;
 }
 

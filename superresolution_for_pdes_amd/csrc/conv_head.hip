@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_n16_kernel(ConvParams p, H3Ar
 }
 
 bool n16_supported(int c0, int c1, int cout, int w, int dil) {
-  return h5_on() && c0 == 32 && c1 == 0 && cout == 16 && dil == 1 && w > 0 && w <= 63 &&
+  return c0 == 32 && c1 == 0 && cout == 16 && dil == 1 && w > 0 && w <= 63 &&
          (size_t)(HEAD_BM + 2 * (w + 1)) * HEAD_SR + 128 + 256 <= 80 * 1024;
 }
 

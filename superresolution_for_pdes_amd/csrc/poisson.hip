@@ -480,7 +480,7 @@ __device__ __forceinline__ void write_part_ag(double v, double* sh, double* dst)
 }
 
 // epoch `epoch` (1, 2, ...) of the grid barrier; false on abort (a wait past ~1 s, or the abort word
-// set before the launch by srpde_poisson_debug_abort).
+// set before the launch by srpde_poisson_cg_batched's test hook, a negative rtol).
 // Memory-model assumption: the barrier pairs `s_waitcnt vmcnt(0)` after each thread's
 // sc1 (L2-bypassing, agent-scope relaxed) stores with sc1 loads after the barrier, instead of an
 // agent-scope release / acquire.  That is correct on gfx950 because every byte handed between blocks
@@ -914,14 +914,10 @@ static int coop_per_launch(int npt, int n) {
 // co-resident grid)
 int srpde_poisson_coop_problems(int n) { return coop_per_launch(8, n); }
 
-// test hook: every cooperative grid-CG launch starts with its abort word set (iters = -1 for every
-// problem of the launch, u undefined), so a caller's abort handling can be exercised
-static std::atomic<int> g_debug_abort{0};
-
 // the whole grid CG of problems [b0, b0 + cnt) in one cooperative launch of gcg_coop_kernel<npt>
 // (workspace carved for B: the polled CG's 2048-point partial arrays hold the larger blocks' too)
 static int coop_solve(const double* f, const double* theta, double* u, int* iters, int b0, int cnt, int B, int n,
-                      int npt, double rtol, int maxit, void* ws, hipStream_t stream) {
+                      int npt, double rtol, int maxit, void* ws, hipStream_t stream, bool start_aborted) {
   const GridCG c = carve(ws, B, n);
   const size_t N2 = (size_t)n * n;
   const int nb = coop_blocks(npt, n);
@@ -940,7 +936,7 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   g.bar = ctl_all;
   g.ctl = reinterpret_cast<unsigned*>(g.bar + 1 + g.ngrp);
   hipError_t e = hipMemsetAsync(g.bar, 0, (g.ngrp + 2) * sizeof(unsigned long long), stream);
-  if (e == hipSuccess && g_debug_abort.load(std::memory_order_relaxed))
+  if (e == hipSuccess && start_aborted)
     e = hipMemsetAsync(g.ctl + 1, 0x01, 1, stream);
   if (e != hipSuccess) { set_error("srpde_poisson_cg_batched: memset: %s", hipGetErrorString(e)); return (int)e; }
   const double* fb = f + b0 * N2;
@@ -956,8 +952,6 @@ static int coop_solve(const double* f, const double* theta, double* u, int* iter
   return 0;
 }
 
-int srpde_poisson_debug_abort(int on) { return g_debug_abort.exchange(on ? 1 : 0); }
-
 // One entry for any n (SURVEY 8(b)'s srpde_poisson_cg_batched), stream-ordered: n <= 128 is one
 // launch of the LDS-resident CG; n > 128 runs the grid CG as cooperative launches (one per group of
 // srpde_poisson_coop_problems(n) problems), whose grid barriers replace the launch boundaries and
@@ -968,6 +962,9 @@ int srpde_poisson_debug_abort(int on) { return g_debug_abort.exchange(on ? 1 : 0
 int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, int B, int n, double rtol, int maxit,
                              int* iters_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
   SRPDE_CHECK_ARG(f && theta && u && B > 0 && n >= 2 && maxit >= 0, "srpde_poisson_cg_batched: bad args");
+  // rtol < 0: the test hook (|rtol| the tolerance) -- every cooperative launch starts with its abort word set
+  const bool start_aborted = rtol < 0;
+  rtol = fabs(rtol);
   if (n <= srpde_poisson_lds_max_n())
     return srpde_poisson_cg_lds(f, theta, u, B, n, rtol, maxit, iters_out, nullptr, stream);
   SRPDE_CHECK_ARG(workspace && ws_bytes >= grid_ws_bytes(B, n), "srpde_poisson_cg_batched: workspace too small");
@@ -988,7 +985,7 @@ int srpde_poisson_cg_batched(const double* f, const double* theta, double* u, in
   if (per > 0) {
     for (int b0 = 0; b0 < B; b0 += per) {
       const int rc = coop_solve(f, theta, u, iters_out, b0, std::min(per, B - b0), B, n, npt, rtol, maxit, workspace,
-                                stream);
+                                stream, start_aborted);
       if (rc != 0) return rc;
     }
     return 0;

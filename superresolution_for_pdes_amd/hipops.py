@@ -32,7 +32,7 @@ def empty(*shape, device):
 
 
 # ---------------------------------- convolution ------------------------------------
-_CONV_MATH = os.environ.get("SRPDE_CONV_MATH", "h3")
+_CONV_MATH = "h3"   # set_conv_math("f32"): the fp32-MFMA kernels (tests, diagnostics)
 
 
 def set_conv_math(mode: str):
@@ -117,7 +117,7 @@ def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
     """BN-statistics partials for the forward conv of input channels (c0, c1) -> cout: the
     kernel family that will run decides the row-block size.  -> (buffer, blocks, rows/block)."""
     h3 = h3_capable(c0, c1, cout, w, dil)
-    rows = (int(query("srpde_conv_h3_stats_rows_for", c0, c1, cout, h, w, dil)) if h3
+    rows = (int(query("srpde_conv_h3_stats_rows_for", c0, c1, cout, h, w, dil, _FAMILY)) if h3
             else int(query("srpde_conv_stats_rows_per_block", cout)))
     nblk = -(-(n * h * w) // rows)
     buf = empty(nblk, cout, 2, device=device)
@@ -125,22 +125,37 @@ def conv_stats_buffer(n, h, w, cout, device, c0, c1=0, dil=1):
     return buf, nblk, rows
 
 
+# kernel-family bits (include/srpde.h SRPDE_FAM_*): srpde_conv_fwd_h3 / _presplit take them in their accumulate
+# argument, srpde_conv_h3_stats_rows_for in its flags -- per call, the library keeps no state.  _FAMILY is the
+# bits this module passes (0: the fastest kernels); set_h3r / set_h4 / set_h5 switch a family off for the tests
+# that compare the bit-identical families and for tuning.
+FAM_NO_H5, FAM_NO_H4, FAM_NO_H3R = 2, 4, 8
+_FAMILY = 0
+
+
+def _set_family(bit, on):
+    global _FAMILY
+    prev = not (_FAMILY & bit)
+    _FAMILY = (_FAMILY & ~bit) if on else (_FAMILY | bit)
+    return prev
+
+
 def set_h3r(on: bool) -> bool:
     """h3 kernel choice for output tiles of <= 64 channels: the register-staged 4-wave kernel
     (two workgroups per CU) or the 8-wave one.  Returns the previous choice."""
-    return bool(query("srpde_conv_h3r_set", int(bool(on))))
+    return _set_family(FAM_NO_H3R, bool(on))
 
 
 def set_h4(on: bool) -> bool:
     """Kernel choice for 128-column h3 tiles at W = 10 / 20: the h4 kernel (conv_h4.hip) or the h3
     8-wave one (bit-identical).  Returns the previous choice."""
-    return bool(query("srpde_conv_h4_set", int(bool(on))))
+    return _set_family(FAM_NO_H4, bool(on))
 
 
 def set_h5(on: bool) -> bool:
     """Kernel choice for the W = 40 forward into 64 / 32 channels: the h5 kernel (conv_h5.hip) or h4 / h3
     (equal conv outputs; 80- vs 128-row statistics blocks).  Returns the previous choice."""
-    return bool(query("srpde_conv_h5_set", int(bool(on))))
+    return _set_family(FAM_NO_H5, bool(on))
 
 
 def h3_capable(c0, c1, cout, w, dil, ksize=3):
@@ -179,7 +194,7 @@ def conv_fwd_up_capable(c0, c1, cout, w, dil):
     """Whether conv_fwd takes an UpsampledInput x0 for this shape (the h4 instantiations)."""
     return (_CONV_MATH == "h3" and dil == 1 and ((w == 20 and cout % 128 == 0) or (w == 40 and cout % 64 == 0))
             and bool(query("srpde_conv_h3_supported", c0, c1, cout, w, dil, 3))
-            and bool(query("srpde_conv_h4_set", -1)))
+            and not (_FAMILY & FAM_NO_H4))
 
 
 def upsample_gate_sa(x, n, h, w, ho, wo, wg, bg):
@@ -211,7 +226,7 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
                                # statistics: the upsampled-input kernel writes h3 row blocks, so a shape whose
                                # statistics blocks are h5's reads the formed tensor
                                and (stats is None or int(query("srpde_conv_h3_stats_rows_for", x0.shape[1], c1_,
-                                                                 cout, h, w, dil))
+                                                                 cout, h, w, dil, _FAMILY))
                                     == int(query("srpde_conv_h3_stats_rows")))):
         x0 = up.materialize()
         up = None
@@ -225,7 +240,7 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
     if _CONV_MATH == "h3" and query("srpde_conv_h3_supported", x0.shape[1], c1, cout, w, dil, ksize):
         planes, wexp = getattr(wpack, "h3", None) or split_weights_h3(wpack, cout)
-        rows_fwd = (int(query("srpde_conv_h3_stats_rows_for", x0.shape[1], c1, cout, h, w, dil)) if sign == 1
+        rows_fwd = (int(query("srpde_conv_h3_stats_rows_for", x0.shape[1], c1, cout, h, w, dil, _FAMILY)) if sign == 1
                     else int(query("srpde_conv_h3_stats_rows")))
         for buf, rows in ((stats, rows_fwd), (bn_bwd[5] if bn_bwd is not None else None,
                                               int(query("srpde_conv_h3_stats_rows")))):
@@ -235,7 +250,7 @@ def conv_fwd(x0, x1, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1, accu
         a0 = amax_of(x0)
         a1 = amax_of(x1) if x1 is not None else None
         _conv_call("srpde_conv_fwd_h3", 2.0 * cout * (x0.shape[1] + c1) * ksize * ksize * n * h * w, p0, x0.shape[1], ld0, p1, c1, ld1, a0.data_ptr(), _p(a1), planes.data_ptr(),
-             wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats),
+             wexp.data_ptr(), _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate) | _FAMILY, _p(stats),
              _p(planes_out), _p(in_affine[0] if in_affine else None), _p(in_affine[1] if in_affine else None),
              *_bn_bwd_args(bn_bwd), _p(out_max), *_ep_args(ep_bn), _p(x1_gate[0] if x1_gate else None),
              _p(x1_gate[1] if x1_gate else None), p0 if up is not None else 0, ld0 if up is not None else 0,
@@ -269,7 +284,7 @@ def conv_fwd_presplit(xp, wpack, bias, y, n, h, w, cout, ksize=3, dil=1, sign=1,
             raise ValueError("statistics buffer not laid out for the h3 kernel")
     ws = _scratch(int(query("srpde_conv_fwd_workspace_size", cout)), y.device)
     _conv_call("srpde_conv_fwd_h3_presplit", 2.0 * cout * c * ksize * ksize * n * h * w, xp.data_ptr(), c, xp._srpde_amax.data_ptr(), planes.data_ptr(), wexp.data_ptr(),
-         _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate), _p(stats), *_bn_bwd_args(bn_bwd),
+         _p(bias), py, ldy, n, h, w, cout, ksize, dil, sign, int(accumulate) | _FAMILY, _p(stats), *_bn_bwd_args(bn_bwd),
          _p(out_max), ws.data_ptr(), ws.numel(), stream_ptr())
 
 
@@ -526,10 +541,10 @@ def _conv_wgrad_h3x(dyp, xs, dw, n, h, w, ksize, dil, accumulate):
 
 
 # ---------------------------------- batch norm -------------------------------------
-# the two-pass finalize (srpde_bn_train_finalize_ws; SRPDE_FIN_SPLIT=0: the one-block-per-channel kernel) from
+# the two-pass finalize (srpde_bn_train_finalize_ws; _FIN_SPLIT False: the one-block-per-channel kernel) from
 # this many partials per channel: the 40 x 40 layers' 20,480 (36 -> 12 us); at 800-3,200 (20 x 20, 10 x 10) the
 # one-pass kernel's 8.5-11.7 us is no slower than the two launches' ~12 (profiles/r05f_bn_finalize_ab.txt)
-_FIN_SPLIT = os.environ.get("SRPDE_FIN_SPLIT", "1") != "0"
+_FIN_SPLIT = True
 _FIN_SPLIT_MIN_BLOCKS = 8192
 
 

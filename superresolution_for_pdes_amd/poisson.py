@@ -42,7 +42,7 @@ class GridBarrierAbort(RuntimeError):
 
 
 def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, device="cuda",
-                  return_iters: bool = False, check: bool = True):
+                  return_iters: bool = False, check: bool = True, _start_aborted: bool = False):
     """u[B, n, n] (float64, on device) with theta*Lap(u) = f per problem.
 
     For n above the LDS solver's limit the solve runs as cooperative launches whose grid barriers
@@ -67,7 +67,9 @@ def solve_batched(f, theta, rtol: float = DEFAULT_RTOL, maxit: int = None, devic
         return (u, iters) if return_iters else u
     ws_bytes = int(query("srpde_poisson_workspace_size", B, n))
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device)
-    call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n, float(rtol), int(maxit),
+    # (_start_aborted, a test hook: the C entry's negative rtol -- every grid-CG launch starts aborted)
+    call("srpde_poisson_cg_batched", f.data_ptr(), theta.data_ptr(), u.data_ptr(), B, n,
+         -float(rtol) if _start_aborted else float(rtol), int(maxit),
          iters.data_ptr(), ws.data_ptr(), ws_bytes, stream_ptr())
     if check and n > int(query("srpde_poisson_lds_max_n")) and not torch.cuda.is_current_stream_capturing():
         bad = int((iters < 0).sum())

@@ -19,7 +19,6 @@ reverse schedule.  Design points:
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -190,9 +189,9 @@ def prepare_h3_weights(m):
     m._srpde_h3w_key = key
 
 
-# the per-step weight split on the side stream (SRPDE_H3W_SIDE=0: in line); its event until the
+# the per-step weight split on the side stream (_H3W_SIDE False: in line); its event until the
 # first h3 convolution of the step waits for it
-_H3W_SIDE = os.environ.get("SRPDE_H3W_SIDE", "1") != "0"
+_H3W_SIDE = True
 _H3W_PENDING = None
 
 
@@ -284,7 +283,7 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
         mom = bn.momentum if bn.momentum is not None else 0.0
         _buffers_ready(dev)
         _RS_EPOCH[0] += 1   # the finalize below rewrites the running statistics torch's version counters miss
-        if not activate:   # the fused consumer's (scale, shift), from the same launch (SRPDE_FIN_AFFINE=0: two)
+        if not activate:   # the fused consumer's (scale, shift), from the same launch (_FIN_AFFINE False: two)
             slot = slots.take()
             if _FIN_AFFINE:
                 mean, invstd, aff = H.bn_train_finalize_affine(stats, nblk, rpb, P, bn.running_mean, bn.running_var,
@@ -405,26 +404,26 @@ def _eval_consumers(a, slot, n, h, w, c, pool, att, gate):
     return a
 
 
-# inference (eval, nothing saved for a backward): BN + ReLU in the conv epilogue (SRPDE_EVAL_EPI=0: the
+# inference (eval, nothing saved for a backward): BN + ReLU in the conv epilogue (_EVAL_EPI False: the
 # separate passes)
-_EVAL_EPI = os.environ.get("SRPDE_EVAL_EPI", "1") != "0"
-# ... also on the register-staged fp32 kernel of enc1.conv1 (SRPDE_EVAL_EPI_F32=0: its separate BN + ReLU pass)
-_EVAL_EPI_F32 = os.environ.get("SRPDE_EVAL_EPI_F32", "1") != "0"
-# the eval forward's per-layer BN (mean, invstd) cached across forwards (SRPDE_EVAL_STATS_CACHE=0: recomputed)
-_EVAL_STATS_CACHE = os.environ.get("SRPDE_EVAL_STATS_CACHE", "1") != "0"
-_FUSE_D1 = os.environ.get("SRPDE_FUSE_D1", "1") != "0"
-_FIN_AFFINE = os.environ.get("SRPDE_FIN_AFFINE", "1") != "0"
+_EVAL_EPI = True
+# ... also on the register-staged fp32 kernel of enc1.conv1 (_EVAL_EPI_F32 False: its separate BN + ReLU pass)
+_EVAL_EPI_F32 = True
+# the eval forward's per-layer BN (mean, invstd) cached across forwards (_EVAL_STATS_CACHE False: recomputed)
+_EVAL_STATS_CACHE = True
+_FUSE_D1 = True
+_FIN_AFFINE = True
 # the gates' spatial attention formed by the upsample that produces their gating input
-# (srpde_upsample_bilinear_gate_fwd; SRPDE_FUSE_SA=0: separate pass over g)
-_FUSE_SA = os.environ.get("SRPDE_FUSE_SA", "1") != "0"
-# inference: out_conv2 + out_bn2 + ReLU + final + residual in one kernel (srpde_conv_head_eval; SRPDE_FUSE_HEAD=0:
+# (srpde_upsample_bilinear_gate_fwd; _FUSE_SA False: separate pass over g)
+_FUSE_SA = True
+# inference: out_conv2 + out_bn2 + ReLU + final + residual in one kernel (srpde_conv_head_eval; _FUSE_HEAD False:
 # out_conv2 on the conv kernels, then srpde_head_fwd)
-_FUSE_HEAD = os.environ.get("SRPDE_FUSE_HEAD", "1") != "0"
-# inference: the decoder's first convs read up(d) from d's rows (H.UpsampledInput; SRPDE_FUSE_UP=0: formed)
-_FUSE_UP = os.environ.get("SRPDE_FUSE_UP", "1") != "0"
+_FUSE_HEAD = True
+# inference: the decoder's first convs read up(d) from d's rows (H.UpsampledInput; _FUSE_UP False: formed)
+_FUSE_UP = True
 # enc1's / enc2's gate channel branch from the BN + ReLU + pool pass (srpde_bn_relu_pool_att_fwd, one
-# block per sample; SRPDE_FUSE_ATT_CH=0: a separate pass over the activation)
-_FUSE_ATT_CH = os.environ.get("SRPDE_FUSE_ATT_CH", "1") != "0"
+# block per sample; _FUSE_ATT_CH False: a separate pass over the activation)
+_FUSE_ATT_CH = True
 
 
 def _per_sample_ok(n, h, w, c):
@@ -434,8 +433,8 @@ def _per_sample_ok(n, h, w, c):
     return _FUSE_ATT_CH and c % 32 == 0 and c <= 256 and (n >= 256 or h * w <= 4096)
 
 
-# a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (SRPDE_FUSE_POOL=0: two)
-_FUSE_POOL = os.environ.get("SRPDE_FUSE_POOL", "1") != "0"
+# a ConvBlock output's BN + ReLU and the max-pool that reads it in one pass (_FUSE_POOL False: two)
+_FUSE_POOL = True
 
 
 class WgradStream:
@@ -472,14 +471,14 @@ class WgradStream:
         self.main.wait_stream(self.side)
 
 
-# weight gradients on a side stream (SRPDE_WGRAD_STREAM=0: in line on the compute stream)
-_WGRAD_STREAM = os.environ.get("SRPDE_WGRAD_STREAM", "1") != "0"
+# weight gradients on a side stream (_WGRAD_STREAM False: in line on the compute stream)
+_WGRAD_STREAM = True
 # the backward's dgrad chain on a high-priority stream: "1" always, "0" never, unset: only under
 # data parallelism.  A high-priority stream never shares a hardware queue with the normal-priority
 # weight-gradient stream; with RCCL's streams present the two normal-priority streams were seen
 # sharing one queue, which serialised wgrad behind dgrad (DataParallel step 37.9 ms -> 35.7 ms,
 # plain step 35.6 ms; without a process group the priority is neutral, 35.74 vs 35.64 ms)
-_BWD_PRIORITY = os.environ.get("SRPDE_BWD_PRIORITY", "auto")
+_BWD_PRIORITY = "auto"
 _PRIO_STREAMS = {}
 
 
@@ -606,27 +605,27 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
 
 
 # the attention gates' output (x * ca) * sa formed inside the decoder conv that reads it (GatedInput;
-# SRPDE_FUSE_ATT_APPLY=0: a separate srpde_att_apply_fwd pass writes it)
-_FUSE_ATT_APPLY = os.environ.get("SRPDE_FUSE_ATT_APPLY", "1") != "0"
+# _FUSE_ATT_APPLY False: a separate srpde_att_apply_fwd pass writes it)
+_FUSE_ATT_APPLY = True
 
 # the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
-# (srpde_conv_dgrad_h3_bnb; SRPDE_FUSE_BN_APPLY=0: off)
-_FUSE_BN_APPLY = os.environ.get("SRPDE_FUSE_BN_APPLY", "1") != "0"
+# (srpde_conv_dgrad_h3_bnb; _FUSE_BN_APPLY False: off)
+_FUSE_BN_APPLY = True
 # layers it is taken for: dgrad output channels <= _BNB_MAX_CIN (one output-column tile), dy channels
 # >= _BNB_MIN_COUT (two input chunks); wider (dec1.conv1's 3-tile dgrad, out_conv1's one-chunk dy)
 # measured +0.5 ms in the step
 _BNB_MAX_CIN, _BNB_MIN_COUT = 64, 64
 
-# the BN backward apply writes dy as its h3 split for a presplit dgrad (SRPDE_PRESPLIT_BWD=0: fp32 dy,
+# the BN backward apply writes dy as its h3 split for a presplit dgrad (_PRESPLIT_BWD False: fp32 dy,
 # split inside the dgrad)
-_PRESPLIT_BWD = os.environ.get("SRPDE_PRESPLIT_BWD", "1") != "0"
+_PRESPLIT_BWD = True
 
 # the 40 x 40 layers' weight gradients split their fp32 input rows themselves (srpde_conv_wgrad_h3x), so
-# their training forwards store no input split (SRPDE_WGRAD_X=0: the forward stores it, h3h reads it)
-_WGRAD_X = os.environ.get("SRPDE_WGRAD_X", "1") != "0"
+# their training forwards store no input split (_WGRAD_X False: the forward stores it, h3h reads it)
+_WGRAD_X = True
 
-# the BN backward reduction of a layer is fused into the dgrad above it (SRPDE_FUSE_BN_BWD=0: off)
-_FUSE_BN_BWD = os.environ.get("SRPDE_FUSE_BN_BWD", "1") != "0"
+# the BN backward reduction of a layer is fused into the dgrad above it (_FUSE_BN_BWD False: off)
+_FUSE_BN_BWD = True
 
 
 def _fuse_pair(conv2, training, w, dil):
@@ -690,9 +689,9 @@ def _att_fwd(att, x, g, n, hw, early=None, sa=None):
 
 
 def _upsample_for_gate(d, att, n, h, w, ho, wo, conv=None, c1=0, fuse=False):
-    """up(d) for the decoder, and (SRPDE_FUSE_SA) the spatial attention of ``att`` whose gate it is.
+    """up(d) for the decoder, and (_FUSE_SA) the spatial attention of ``att`` whose gate it is.
     ``fuse`` (inference; ``conv`` the decoder conv reading up(d) as x0 beside ``c1`` gated channels):
-    up(d) is not formed -- an UpsampledInput the conv interpolates from d's rows (SRPDE_FUSE_UP=0: off),
+    up(d) is not formed -- an UpsampledInput the conv interpolates from d's rows (_FUSE_UP False: off),
     the gate's spatial attention computed from d at low resolution (srpde_upsample_gate_sa)."""
     if (fuse and _FUSE_UP and _FUSE_SA and _FUSE_ATT_APPLY and d.is_cuda and conv is not None
             and H.conv_fwd_up_capable(d.shape[1], c1, conv.out_channels, wo, 1)):
@@ -792,7 +791,7 @@ def unet_forward(m, x, training, save=False):
     u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w, m.dec1.conv1, e1.shape[1], fuse_up)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1, sa=sa1)
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
-    # transform when out_conv1 keeps its input split (d1 itself is never written; SRPDE_FUSE_D1=0: off)
+    # transform when out_conv1 keeps its input split (d1 itself is never written; _FUSE_D1 False: off)
     if _FUSE_D1 and _fuse_pair(m.out_conv1, training, w, 1):
         (d1, d1aff), S.dec1 = _block_fwd(m.dec1, u2, e1a, n, h, w, training, slots, activate=False)
     else:
@@ -962,7 +961,7 @@ class UNetFunction(torch.autograd.Function):
         ends = _group_end_offsets(layout)
         side = _WGRAD_STREAM and dout.is_cuda
         # with the weight gradients on a side stream, the dgrad chain may run on a high-priority
-        # stream (SRPDE_BWD_PRIORITY; on by default under data parallelism, see _BWD_PRIORITY)
+        # stream (_BWD_PRIORITY; on by default under data parallelism, see _BWD_PRIORITY)
         prio = _BWD_PRIORITY == "1" or (_BWD_PRIORITY == "auto" and reducer is not None)
         hi = _priority_stream(dout.device) if side and prio else None
         cur = torch.cuda.current_stream(dout.device) if dout.is_cuda else None

@@ -133,6 +133,22 @@ def test_no_runtime_diagnostic_switch(lib):
     assert b"SRPDE_CONV_DBG" not in data
 
 
+def test_no_global_state_or_environment(lib):
+    """Verdict r5 #8: the library keeps no global mutable state and reads no environment (include/srpde.h
+    conventions): the kernel-family setters and the Poisson abort switch are gone (per-call SRPDE_FAM_* bits and
+    a negative rtol replace them), no SRPDE_* variable name is in its strings, and getenv is not imported."""
+    import subprocess
+    for name in ("srpde_conv_h5_set", "srpde_conv_h4_set", "srpde_conv_h3r_set", "srpde_poisson_debug_abort"):
+        assert not hasattr(lib.lib(), name), name
+    text = open(lib.HEADER).read()
+    for name in ("srpde_conv_h5_set", "srpde_conv_h4_set", "srpde_conv_h3r_set", "srpde_poisson_debug_abort"):
+        assert f"int {name}(" not in text, name   # (the ABI history above names them)
+    data = open(lib.LIB_PATH, "rb").read()
+    assert re.search(rb"SRPDE_[A-Z0-9_]+", data) is None, re.findall(rb"SRPDE_[A-Z0-9_]+", data)[:5]
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "getenv" not in dyn
+
+
 def test_spill_budget(lib):
     """Verdict r4 #9: no kernel of the shipped library spills more than its committed budget
     (tests/spill_budget.json, written by tools/spill_budget.py --write; a kernel not listed has budget 0).

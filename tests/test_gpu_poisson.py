@@ -154,22 +154,17 @@ def test_grid_cg_at_the_cooperative_size_bound(n):
 def test_aborted_grid_barrier_raises():
     """a cooperative grid-CG launch that gives up at a grid barrier marks its problems
     iters = -1 and leaves u unconverged; solve_batched must raise instead of returning that u (the
-    data-generation callers never look at iters).  srpde_poisson_debug_abort starts the launches
-    aborted; the next solve after it is switched off is normal again."""
+    data-generation callers never look at iters).  The C entry's test hook (a negative rtol, per call: the
+    library keeps no state) starts the launches aborted; the next solve without it is normal."""
     from superresolution_for_pdes_amd import poisson as P
-    from superresolution_for_pdes_amd._lib import query
     n, B = 160, 3
     rng = np.random.default_rng(5)
     f = P.forcing_batched(rng.uniform(0.5, 8.0, (B, 2)), n)
     th = torch.ones(B, n, n, dtype=torch.float64, device="cuda")
-    prev = int(query("srpde_poisson_debug_abort", 1))
-    try:
-        with pytest.raises(P.GridBarrierAbort):
-            P.solve_batched(f, th)
-        u, it = P.solve_batched(f, th, return_iters=True, check=False)
-        assert int((it < 0).sum()) == B
-    finally:
-        query("srpde_poisson_debug_abort", prev)
+    with pytest.raises(P.GridBarrierAbort):
+        P.solve_batched(f, th, _start_aborted=True)
+    u, it = P.solve_batched(f, th, return_iters=True, check=False, _start_aborted=True)
+    assert int((it < 0).sum()) == B
     u, it = P.solve_batched(f, th, return_iters=True)
     assert int(it.min()) > 0
 

@@ -3,7 +3,7 @@
 Every kernel on the path is deterministic (fixed-order reductions, no float atomics), so
 moving launches between streams (unet_exec.WgradStream: weight gradients on a side stream)
 or changing which kernel computes a tile (the register-staged h3r kernel against the 8-wave one,
-srpde_conv_h3r_set) must not change a single bit.  Anything else is a race or a
+SRPDE_FAM_NO_H3R) must not change a single bit.  Anything else is a race or a
 wrong tile, which a tolerance-based parity test could hide.
 """
 import os

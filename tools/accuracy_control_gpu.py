@@ -23,6 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/acc")
     ap.add_argument("--epochs", type=int, default=500)
+    ap.add_argument("--torch-seeds", type=int, nargs="*", default=[42],
+                    help="train once per torch seed (model init + batch order; the data split keeps np seed 42): "
+                         "the run-to-run spread of the trained model")
     a = ap.parse_args()
     from superresolution_for_pdes_amd import train_enhanced as T
     os.makedirs(a.out, exist_ok=True)
@@ -32,21 +35,31 @@ def main():
     npz = "/tmp/srpde_acc_dataset.npz"
     np.savez(npz, **data)
     gen_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    hist = T.main(["--data", npz, "--epochs", str(a.epochs), "--results", "/tmp/srpde_acc_runs"])
-    torch.cuda.synchronize()
-    train_s = time.perf_counter() - t0
-    best = sorted(glob.glob("/tmp/srpde_acc_runs/*/best_model.pth"))[-1]
-    sd = torch.load(best, map_location="cpu", weights_only=True)["model_state_dict"]
-    torch.save({k: v.float() if v.is_floating_point() else v for k, v in sd.items()},
-               os.path.join(a.out, f"hip_e{a.epochs}_best_weights.pt"))
-    rec = {"what": "HIP train_enhanced.main on the seed-42 dataset", "epochs_cap": a.epochs,
-           "epochs_run": len(hist["train_loss"]), "best_epoch": hist["best_epoch"],
-           "best_val_loss": hist["best_val_loss"], "train_loss": hist["train_loss"], "val_loss": hist["val_loss"],
-           "generate_s": round(gen_s, 2), "train_s": round(train_s, 1),
-           "dataset_checksum": {k: float(np.asarray(v, dtype=np.float64).sum()) for k, v in data.items()}}
-    json.dump(rec, open(os.path.join(a.out, f"hip_e{a.epochs}_history.json"), "w"))
-    print(json.dumps({k: v for k, v in rec.items() if k not in ("train_loss", "val_loss")}))
+    real_seed, real_cuda_seed = torch.manual_seed, torch.cuda.manual_seed
+    for ts in a.torch_seeds:
+        # main() seeds torch (and the device generator, which draws the device-side init) with 42: this run's seed
+        torch.manual_seed = (lambda _s, ts=ts: real_seed(ts))
+        torch.cuda.manual_seed = (lambda _s, ts=ts: real_cuda_seed(ts))
+        t0 = time.perf_counter()
+        try:
+            hist = T.main(["--data", npz, "--epochs", str(a.epochs), "--results", f"/tmp/srpde_acc_runs_{ts}"])
+        finally:
+            torch.manual_seed, torch.cuda.manual_seed = real_seed, real_cuda_seed
+        torch.cuda.synchronize()
+        train_s = time.perf_counter() - t0
+        best = sorted(glob.glob(f"/tmp/srpde_acc_runs_{ts}/*/best_model.pth"))[-1]
+        sd = torch.load(best, map_location="cpu", weights_only=True)["model_state_dict"]
+        tag = f"hip_e{a.epochs}" + ("" if ts == 42 else f"_s{ts}")
+        torch.save({k: v.float() if v.is_floating_point() else v for k, v in sd.items()},
+                   os.path.join(a.out, f"{tag}_best_weights.pt"))
+        rec = {"what": "HIP train_enhanced.main on the seed-42 dataset", "torch_seed": ts, "epochs_cap": a.epochs,
+               "epochs_run": len(hist["train_loss"]), "best_epoch": hist["best_epoch"],
+               "best_val_loss": hist["best_val_loss"], "train_loss": hist["train_loss"], "val_loss": hist["val_loss"],
+               "generate_s": round(gen_s, 2), "train_s": round(train_s, 1),
+               "dataset_checksum": {k: float(np.asarray(v, dtype=np.float64).sum()) for k, v in data.items()}}
+        json.dump(rec, open(os.path.join(a.out, f"{tag}_history.json"), "w"))
+        print(json.dumps({k: v for k, v in rec.items() if k not in ("train_loss", "val_loss", "dataset_checksum")}),
+              flush=True)
 
 
 if __name__ == "__main__":
