@@ -125,6 +125,71 @@ def test_no_packed_fp32_instructions(lib, tmp_path):
     assert not packed, sorted(set(packed))
 
 
+def _h5_vmem_events(body):
+    """the loader-relevant events of one h5 kernel, in code order: D = weight DMA (buffer_load ... lds), S = the asm
+    epilogue store (buffer_store_dwordx4), X = a scratch access, B = s_barrier, W = a `s_waitcnt vmcnt(N)` right before
+    a barrier (the loaders' counted tap wait); the converters' own buffer loads (no lds) are not on the loader path"""
+    ins = []
+    for line in body.split("\n")[1:]:
+        m = re.match(r"\s+([sv]_\w+|buffer_\w+|ds_\w+|global_\w+|scratch_\w+)\s*(.*?)(//.*)?$", line)
+        if m:
+            ins.append((m.group(1), m.group(2).strip()))
+    ev = []
+    for k, (op, a) in enumerate(ins):
+        if op == "buffer_load_dwordx4" and "lds" in a:
+            ev.append(("D", k))
+        elif op == "buffer_store_dwordx4":
+            ev.append(("S", k))
+        elif op.startswith("scratch_"):
+            ev.append(("X", k))
+        elif op == "s_barrier":
+            ev.append(("B", k))
+        elif op == "s_waitcnt" and re.fullmatch(r"vmcnt\((\d+)\)", a) and k + 1 < len(ins) and ins[k + 1][0] == "s_barrier":
+            ev.append(("W", int(re.fullmatch(r"vmcnt\((\d+)\)", a).group(1))))
+    return ins, ev
+
+
+def test_h5_hand_counted_waits_and_store_wait_states(lib, tmp_path):
+    """Verdict r5 #6: conv_h5.hip manages two hazards by hand, checked here in the SHIPPED binary of every h5 variant.
+    (1) Each inline-asm `buffer_store_dwordx4` is followed by its `s_nop` (>= 1) before anything can write its data
+    registers (the wait state the compiler's hazard pass cannot see: round 5 measured the first data register
+    overwritten without it).  (2) The loader waves' tap wait `s_waitcnt vmcnt(N)` (N = NCB + epi_ns(T - 2) +
+    epi_ns(T - 1) in the source) must let only operations YOUNGER than the weight DMA of tap T + 1 (issued at tap
+    T - 2) stay outstanding: counting the loader path's vector-memory operations in the code (DMAs, asm stores,
+    scratch accesses) after that DMA up to the wait gives exactly N for taps 2..17 of the unrolled 18-tap loop, and
+    at least N for taps 0 / 1 (their window crosses the loop back-edge, where the count here also takes the code
+    after the loop: conservative).  A codegen change that added, dropped or reordered a loader-path memory
+    operation -- a spill, a compiler-inserted load, a merged store -- fails this."""
+    dis = _device_disassembly(lib.LIB_PATH, tmp_path)
+    funcs = [f for f in re.split(r"\n(?=[0-9a-f]+ <_Z)", dis) if "<_ZN5srpde18conv_fwd_h5_kernel" in f.split("\n")[0]]
+    assert len(funcs) >= 10, len(funcs)
+    for f in funcs:
+        name = re.match(r"[0-9a-f]+ <([^>]*)>", f).group(1)
+        ins, ev = _h5_vmem_events(f)
+        for k, (op, _) in enumerate(ins):
+            if op == "buffer_store_dwordx4":
+                nxt = ins[k + 1]
+                assert nxt[0] == "s_nop" and int(nxt[1] or 0) >= 1, (name, k, nxt)
+        tapb = [j for j, e in enumerate(ev) if e[0] == "B" and j > 0 and ev[j - 1][0] == "W"]
+        assert len(tapb) == 18, (name, len(tapb))
+
+        def ops(lo, hi):
+            return [j for j in range(lo, hi) if ev[j][0] in "DSX"]
+        iv = {t: ops(tapb[t], tapb[t + 1] if t < 17 else len(ev)) for t in range(18)}
+        pre = [j for j, e in enumerate(ev[:tapb[0]]) if e[0] == "B"]
+        iv_pre = ops(pre[-1] if pre else 0, tapb[0])
+        for t in range(18):
+            n = ev[tapb[t] - 1][1]
+            a, b = (t - 2) % 18, (t - 1) % 18
+            dmas = [j for j in iv[a] if ev[j][0] == "D"]
+            assert dmas, (name, t, "no weight DMA two taps before")
+            younger = len([j for j in iv[a] if j > dmas[-1]]) + len(iv[b]) + (len(iv_pre) if t < 2 else 0)
+            if t >= 2:
+                assert younger == n, (name, t, n, younger)
+            else:
+                assert younger >= n, (name, t, n, younger)
+
+
 def test_no_runtime_diagnostic_switch(lib):
     """Verdict r3 weak #6: the h3 kernels' phase-ablation switch (SRPDE_CONV_DBG, which skips DMA /
     MFMA / epilogue work and makes results wrong) is a compile-time define for A/B builds only: the
