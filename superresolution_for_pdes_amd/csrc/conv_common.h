@@ -10,7 +10,8 @@
 // 0 in the product build -- an A/B library is built with SRPDE_EXTRA_FLAGS=-DSRPDE_CONV_DBG=<bits>
 // (results wrong when non-zero).  1 = no DMA in the loop, 2 = no stage barrier, 4 = no per-chunk
 // convert, 16 = no epilogue, 32 = no prologue halo DMA, 64 = no prologue convert, 128 = no MFMAs,
-// 256 = phase timestamps past the output (h4; tools/h4_phase_ts.py).
+// 256 = phase timestamps past the output (h4; tools/h4_phase_ts.py), 512 = no input scale / shift loads in
+// the h4 convert (identity BN).
 #ifndef SRPDE_CONV_DBG
 #define SRPDE_CONV_DBG 0
 #endif

@@ -68,6 +68,26 @@ __device__ __forceinline__ void static_for(F&& f) {
 #define H4_BAR2 0
 #endif
 
+typedef float h4f32x4 __attribute__((ext_vector_type(4)));
+__device__ h4f32x4 h4_buffer_load_f4(int32x4 rsrc, int voffset, int soffset,
+                                     int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ __forceinline__ float4 f4_of(h4f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); }
+__device__ float h4_buffer_load_f1(int32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+
+// conv_h3.h gate8 (the same expressions) with buffer loads: the attention vectors' 64-bit base pointers, held
+// in VGPRs across the persistent loop, were the last spilled registers of the 128-column instantiations
+__device__ __forceinline__ void gate8_h4(float4& v0, float4& v1, const H3Args& h, int pix, int P, int HW, int c1,
+                                         int cc1) {
+  if (pix < 0 || pix >= P) return;
+  const int n = pix / HW;
+  const int32x4 rca = make_rsrc(h.x1_ca, (unsigned)((P / HW) * c1 * 4)), rsa = make_rsrc(h.x1_sa, (unsigned)(P * 4));
+  const float4 a0 = f4_of(h4_buffer_load_f4(rca, (n * c1 + cc1) * 4, 0, 0));
+  const float4 a1 = f4_of(h4_buffer_load_f4(rca, (n * c1 + cc1) * 4 + 16, 0, 0));
+  const float s = h4_buffer_load_f1(rsa, pix * 4, 0, 0);
+  v0.x = (v0.x * a0.x) * s; v0.y = (v0.y * a0.y) * s; v0.z = (v0.z * a0.z) * s; v0.w = (v0.w * a0.w) * s;
+  v1.x = (v1.x * a1.x) * s; v1.y = (v1.y * a1.y) * s; v1.z = (v1.z * a1.z) * s; v1.w = (v1.w * a1.w) * s;
+}
+
 template <int W, int DIL, int BN_>
 struct H4Geom {
   static constexpr int BM = 256, BN = BN_;
@@ -305,12 +325,20 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
     float4 s0, s1, t0, t1;
     const int c8 = tid & 3;   // every task of this thread has the same 8 channels
     const bool gate = h.x1_ca != nullptr && ch * BK2 >= p.c0;   // the attention-gated second input
-    if (h.in_scale != nullptr) {
-      const int cc = ch * BK2 + c8 * 8;
-      s0 = *reinterpret_cast<const float4*>(h.in_scale + cc);
-      s1 = *reinterpret_cast<const float4*>(h.in_scale + cc + 4);
-      t0 = *reinterpret_cast<const float4*>(h.in_shift + cc);
-      t1 = *reinterpret_cast<const float4*>(h.in_shift + cc + 4);
+    if constexpr ((SRPDE_CONV_DBG & 512) != 0) {   // diagnostics: 512 = no scale / shift loads (identity BN)
+      s0 = s1 = make_float4(1.f, 1.f, 1.f, 1.f);
+      t0 = t1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (h.in_scale != nullptr) {
+      // buffer loads: the per-lane part of the address is one 32-bit offset (c8 * 32 B), the chunk's in the
+      // scalar offset -- a 64-bit per-lane pointer held across the persistent loop spilled (8 VGPRs) in the
+      // 128-column instantiations
+      const unsigned nb = (unsigned)((p.c0 + p.c1) * 4);
+      const int32x4 rsc = make_rsrc(h.in_scale, nb), rsh = make_rsrc(h.in_shift, nb);
+      const int vo = c8 * 32, so = ch * BK2 * 4;
+      s0 = f4_of(h4_buffer_load_f4(rsc, vo, so, 0));
+      s1 = f4_of(h4_buffer_load_f4(rsc, vo + 16, so, 0));
+      t0 = f4_of(h4_buffer_load_f4(rsh, vo, so, 0));
+      t1 = f4_of(h4_buffer_load_f4(rsh, vo + 16, so, 0));
     }
     // (UP: not unrolled -- unrolled, the interpolating convert spilled 48-50 VGPRs; eval forward -1 %)
 #pragma unroll (UP ? 1 : (AROWS * 4 + 511) / 512)
@@ -349,7 +377,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_h4_kernel(ConvParams p, H3Arg
         v0 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8) * 16);
         v1 = *reinterpret_cast<const float4*>(f + swz(r, 2 * c8 + 1) * 16);
       }
-      if (gate) gate8(v0, v1, h, t.pix0 + r, p.P, p.H * W, p.c1, ch * BK2 - p.c0 + c8 * 8);
+      if (gate) gate8_h4(v0, v1, h, t.pix0 + r, p.P, p.H * W, p.c1, ch * BK2 - p.c0 + c8 * 8);
       if (h.in_scale != nullptr) {   // fused BN + ReLU of the producer; rows outside the tensor stay 0
         const int pix = t.pix0 + r;
         const bool inside = pix >= 0 && pix < p.P;
