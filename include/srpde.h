@@ -54,8 +54,9 @@ typedef struct ihipStream_t* hipStream_t;
  *  10  no global state: srpde_conv_h5_set / _h4_set / _h3r_set and srpde_poisson_debug_abort removed; the kernel
  *      family is SRPDE_FAM_* bits of srpde_conv_fwd_h3's / _presplit's accumulate argument and of
  *      srpde_conv_h3_stats_rows_for's new flags argument, the grid-CG abort hook a negative rtol;
- *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL */
-#define SRPDE_ABI_VERSION 10
+ *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL
+ *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported */
+#define SRPDE_ABI_VERSION 11
 
 /* Kernel-family bits (per call; bit 0 of the same argument is the accumulate flag): the forward / dgrad
  * families compute the same outputs, statistics and stored splits bit for bit, so these only route a call to
@@ -389,6 +390,18 @@ int srpde_att_apply_fwd(const float* x, int ldx, int n, int hw, int c, const flo
 int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
                                       int lddx, int n, int h, int w, int ho, int wo, int c, int accumulate,
                                       hipStream_t stream);
+/* The same (accumulate = 0) with the backward reduction of the BatchNorm (+ ReLU, flags SRPDE_BN_RELU) whose
+ * output gradient dx is -- the decoder block below the upsample (dec2.bn2 under u2, dec3.bn2 under u3,
+ * models.py:88-93): y its pre-BN input, mean / invstd the batch statistics; part receives [n*h][c] float2
+ * partials (sum dz, sum dz*xhat) and da_max[n*h] max|dx| per input row, the (part, da_max) pair
+ * srpde_bn_bwd_prepare / srpde_bn_relu_bwd_part take, so the BN backward does not re-read dx.  Shapes:
+ * srpde_upsample_bwd_bn_supported (the row-blocked kernel). */
+int srpde_upsample_bwd_bn_supported(int h, int w, int ho, int wo, int c, int lddo, int lddx);
+int srpde_upsample_bilinear_bwd_gated_bn(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
+                                         int lddx, int n, int h, int w, int ho, int wo, int c, const float* y, int ldy,
+                                         const float* mean, const float* invstd, const float* gamma,
+                                         const float* beta, int flags, void* part, float* da_max,
+                                         hipStream_t stream);
 
 /* ---- AttentionGate.forward / backward (src/models.py:103-130) ----------------------- */
 int srpde_att_fwd(const float* x, int ldx, const float* g, int ldg, int n, int hw, int c, int gc, const float* w1,

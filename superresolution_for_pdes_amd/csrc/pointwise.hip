@@ -509,13 +509,26 @@ __device__ __forceinline__ void upsample_rows_phase1(const float* __restrict__ d
   }
 }
 
-template <bool GATED>
+// The BatchNorm (+ ReLU) whose output gradient the upsample backward writes (the decoder block below:
+// dec2.bn2 under u2, dec3.bn2 under u3): its backward reduction is formed from the values as they are
+// stored, so the BN backward does not re-read them (bn_bwd_reduce_kernel's expressions; partials per
+// input row block: part[row][C] = (sum dz, sum dz * xhat), da_max[row] = max |dx|)
+struct UpBnArgs {
+  const float* y;
+  int ldy;
+  const float *mean, *invstd, *gamma, *beta;
+  int relu;
+  float2* part;
+  float* da_max;
+};
+
+template <bool GATED, bool BN = false>
 __global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __restrict__ dout, int lddo,
                                                                 float* __restrict__ dx, int lddx, int H, int W, int Ho,
                                                                 int Wo, int C, int accumulate,
                                                                 const float* __restrict__ gsa,
-                                                                const float* __restrict__ gw) {
-  extern __shared__ float4 rrow[];   // [Wo][C/4]
+                                                                const float* __restrict__ gw, UpBnArgs bn = {}) {
+  extern __shared__ float4 rrow[];   // [Wo][C/4]; with BN at least [2][256] for the block reduction
   const int C4 = C >> 2;
   const int cq = threadIdx.x % C4, lx0 = threadIdx.x / C4, nlx = blockDim.x / C4;
   // consecutive workgroups go to different XCDs (each with its own L2): remap so an XCD walks a
@@ -545,6 +558,14 @@ __global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __r
   else if (nrow == 5) upsample_rows_phase1<GATED, 5>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
   else upsample_rows_phase1<GATED, ROWS_NS>(dout, lddo, Ho, Wo, C4, n, iy, H, oy0, hi, gsa, gw, rrow);
   __syncthreads();
+  float4 mu, is, g, b, s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  float dmax = 0.f;
+  if constexpr (BN) {
+    mu = *reinterpret_cast<const float4*>(bn.mean + cq * 4);
+    is = *reinterpret_cast<const float4*>(bn.invstd + cq * 4);
+    g = *reinterpret_cast<const float4*>(bn.gamma + cq * 4);
+    b = *reinterpret_cast<const float4*>(bn.beta + cq * 4);
+  }
   for (int ix = lx0; ix < W; ix += nlx) {
     int xlo, xhi;
     cand_range(ix, W, Wo, &xlo, &xhi);
@@ -563,6 +584,43 @@ __global__ __launch_bounds__(256) void upsample_bwd_rows_kernel(const float* __r
       s.x += old.x; s.y += old.y; s.z += old.z; s.w += old.w;
     }
     *reinterpret_cast<float4*>(o) = s;
+    if constexpr (BN) {
+      const float4 v = *reinterpret_cast<const float4*>(bn.y + ((size_t)blk * W + ix) * bn.ldy + cq * 4);
+      dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(s.x), fabsf(s.y)), fmaxf(fabsf(s.z), fabsf(s.w))));
+      float xh, dz;
+#define UPBN_ACC(X)                                            \
+  xh = (v.X - mu.X) * is.X;                                    \
+  dz = (!(bn.relu & 1) || xh * g.X + b.X > 0.f) ? s.X : 0.f;   \
+  s1.X += dz;                                                  \
+  s2.X += dz * xh;
+      UPBN_ACC(x) UPBN_ACC(y) UPBN_ACC(z) UPBN_ACC(w)
+#undef UPBN_ACC
+    }
+  }
+  if constexpr (BN) {
+    __syncthreads();   // every thread is past its rrow reads
+    const int t = threadIdx.x;
+    if (lx0 < nlx) {
+      rrow[t] = s1;
+      rrow[256 + t] = s2;
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, k, 64));
+    float* wmx = reinterpret_cast<float*>(rrow + 512);
+    if ((t & 63) == 0) wmx[t >> 6] = dmax;
+    __syncthreads();
+    if (t < C4) {
+      float4 t1 = make_float4(0.f, 0.f, 0.f, 0.f), t2 = t1;
+      for (int r = 0; r < nlx; ++r) {
+        const float4 a = rrow[r * C4 + t], a2 = rrow[256 + r * C4 + t];
+        t1.x += a.x; t1.y += a.y; t1.z += a.z; t1.w += a.w;
+        t2.x += a2.x; t2.y += a2.y; t2.z += a2.z; t2.w += a2.w;
+      }
+      float2* op = bn.part + (size_t)blk * C + t * 4;
+      op[0] = make_float2(t1.x, t2.x); op[1] = make_float2(t1.y, t2.y);
+      op[2] = make_float2(t1.z, t2.z); op[3] = make_float2(t1.w, t2.w);
+    }
+    if (t == 0) bn.da_max[blk] = fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]));
   }
 }
 
@@ -583,9 +641,16 @@ static bool upsample_rows_ok(int h, int w, int ho, int wo, int c, int lddo, int 
 template <bool GATED>
 static void launch_upsample_bwd_rows(const float* dout, int lddo, float* dx, int lddx, int n, int h, int w, int ho,
                                      int wo, int c, int accumulate, const float* gsa, const float* gw,
-                                     hipStream_t stream) {
-  hipLaunchKernelGGL(upsample_bwd_rows_kernel<GATED>, dim3((unsigned)(n * h)), dim3(256), (size_t)wo * c * sizeof(float),
-                     stream, dout, lddo, dx, lddx, h, w, ho, wo, c, accumulate, gsa, gw);
+                                     hipStream_t stream, const UpBnArgs* bn = nullptr) {
+  if (bn != nullptr) {
+    const size_t lds = std::max((size_t)wo * c * sizeof(float), (size_t)(512 * sizeof(float4) + 16));
+    hipLaunchKernelGGL((upsample_bwd_rows_kernel<GATED, true>), dim3((unsigned)(n * h)), dim3(256), lds, stream, dout,
+                       lddo, dx, lddx, h, w, ho, wo, c, accumulate, gsa, gw, *bn);
+    return;
+  }
+  hipLaunchKernelGGL((upsample_bwd_rows_kernel<GATED, false>), dim3((unsigned)(n * h)), dim3(256),
+                     (size_t)wo * c * sizeof(float), stream, dout, lddo, dx, lddx, h, w, ho, wo, c, accumulate, gsa, gw,
+                     UpBnArgs{});
 }
 
 // launch geometry of the pixel-blocked kernels, or false when C/4 is not a power of two <= 256
@@ -1244,6 +1309,28 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
   hipLaunchKernelGGL(upsample_bwd_px_kernel, g, b, 0, stream, dout, lddo, dx, lddx, (unsigned)(n * h * w), h, w, ho,
                      wo, accumulate, dsa, wg);
   SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd_gated");
+  return 0;
+}
+
+int srpde_upsample_bwd_bn_supported(int h, int w, int ho, int wo, int c, int lddo, int lddx) {
+  return upsample_gather_ok(h, ho) && upsample_gather_ok(w, wo) && upsample_rows_ok(h, w, ho, wo, c, lddo, lddx) ? 1
+                                                                                                               : 0;
+}
+
+int srpde_upsample_bilinear_bwd_gated_bn(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
+                                         int lddx, int n, int h, int w, int ho, int wo, int c, const float* y, int ldy,
+                                         const float* mean, const float* invstd, const float* gamma,
+                                         const float* beta, int flags, void* part, float* da_max,
+                                         hipStream_t stream) {
+  SRPDE_CHECK_ARG(dout && dsa && wg && dx && y && mean && invstd && gamma && beta && part && da_max && ldy % 4 == 0 &&
+                      aligned16(y) && aligned16(dx) && aligned16(dout),
+                  "srpde_upsample_bilinear_bwd_gated_bn: null argument / alignment");
+  SRPDE_CHECK_ARG(ho >= h && wo >= w && srpde_upsample_bwd_bn_supported(h, w, ho, wo, c, lddo, lddx),
+                  "srpde_upsample_bilinear_bwd_gated_bn: shape outside the row-blocked kernel "
+                  "(srpde_upsample_bwd_bn_supported)");
+  const UpBnArgs bn{y, ldy, mean, invstd, gamma, beta, flags & SRPDE_BN_RELU, static_cast<float2*>(part), da_max};
+  launch_upsample_bwd_rows<true>(dout, lddo, dx, lddx, n, h, w, ho, wo, c, 0, dsa, wg, stream, &bn);
+  SRPDE_LAUNCH_CHECK("srpde_upsample_bilinear_bwd_gated_bn");
   return 0;
 }
 

@@ -782,18 +782,34 @@ def pde_dataset_assemble(u_coarse, u_fine, theta_fine, f_fine, stats, theta_cons
     return inputs, targets
 
 
-def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate, gate=None):
+def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate, gate=None, bn=None):
     """``gate = (dsa, wg)``: the upsampled tensor's gradient is dout + dsa (x) wg (the attention
-    gating gradient left unapplied by att_bwd(dg=None))."""
+    gating gradient left unapplied by att_bwd(dg=None)).  ``bn = (y, mean, invstd, gamma, beta)``: the BN +
+    ReLU whose output gradient dx is; returns its backward reduction (part [n*h, c, 2], da_max [n*h]) formed
+    from the stored values (srpde_upsample_bilinear_bwd_gated_bn), or None when the shape has no fused
+    kernel (the BN backward then reduces on its own)."""
     pdo, lddo = _pl(dout)
     pdx, lddx = _pl(dx)
+    if bn is not None and gate is not None and not accumulate and bool(
+            query("srpde_upsample_bwd_bn_supported", h, w, ho, wo, dx.shape[1], lddo, lddx)):
+        y, mean, invstd, gamma, beta = bn
+        dsa, wg = gate
+        py, ldy = _pl(y)
+        c = dx.shape[1]
+        part = empty(n * h, c, 2, device=dx.device)
+        da_max = empty(n * h, device=dx.device)
+        call("srpde_upsample_bilinear_bwd_gated_bn", pdo, lddo, dsa.data_ptr(), wg.data_ptr(), pdx, lddx, n, h, w, ho,
+             wo, c, py, ldy, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), BN_RELU,
+             part.data_ptr(), da_max.data_ptr(), stream_ptr())
+        return part, da_max
     if gate is not None:
         dsa, wg = gate
         call("srpde_upsample_bilinear_bwd_gated", pdo, lddo, dsa.data_ptr(), wg.data_ptr(), pdx, lddx, n, h, w, ho,
              wo, dx.shape[1], int(accumulate), stream_ptr())
-        return
+        return None
     call("srpde_upsample_bilinear_bwd", pdo, lddo, pdx, lddx, n, h, w, ho, wo, dx.shape[1], int(accumulate),
          stream_ptr())
+    return None
 
 
 # ----------------------------------- attention -------------------------------------

@@ -656,6 +656,19 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True,
                      activate=activate, att=att)
 
 
+# the decoder blocks' bn2 backward reduction formed inside the upsample backward (_FUSE_UP_BN False: a
+# separate reduction pass re-reads the upsample's output)
+_FUSE_UP_BN = True
+
+
+def _up_bn(blk, saved):
+    """(y, mean, invstd, gamma, beta) of ``blk``.bn2 for upsample_bwd(bn=...), or None (_FUSE_UP_BN off)."""
+    if not _FUSE_UP_BN:
+        return None
+    _, _, y, mean, invstd, _, _ = saved[1]
+    return y, mean, invstd, blk.bn2.weight, blk.bn2.bias
+
+
 def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
     """``part``: bn2's backward reduction, when the dgrad that wrote ``da`` produced it."""
     s1, s2 = saved
@@ -871,11 +884,12 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
         gate, dm1 = gate
     ready("att1")
     dd2 = H.empty(P2, 128, device=dev)
-    H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate)
+    # dec2.bn2's backward reduction formed by the upsample backward that writes its output gradient
+    part = H.upsample_bwd(dcat1[:, :128], dd2, n, h2, w2, h, w, False, gate=gate, bn=_up_bn(m.dec2, S.dec2))
     _tap("d2", dd2)
     # dec2: grad of cat[u3 (256), e2a (128)]
     dcat2 = H.empty(P2, 384, device=dev)
-    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2, wq=wq)
+    _block_bwd(m.dec2, S.dec2, dd2, n, h2, w2, grads, slots, dcat2, wq=wq, part=part)
     _tap("u3c", dcat2[:, :256])
     _tap("e2a", dcat2[:, 256:])
     ready("dec2")
@@ -888,11 +902,11 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
         gate, dm2 = gate
     ready("att2")
     dd3 = H.empty(P3, 256, device=dev)
-    H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate)
+    part = H.upsample_bwd(dcat2[:, :256], dd3, n, h3, w3, h2, w2, False, gate=gate, bn=_up_bn(m.dec3, S.dec3))
     _tap("d3", dd3)
     # dec3: grad of cat[b (512), e3a (256)]
     dcat3 = H.empty(P3, 768, device=dev)
-    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq)
+    _block_bwd(m.dec3, S.dec3, dd3, n, h3, w3, grads, slots, dcat3, wq=wq, part=part)
     _tap("e3a", dcat3[:, 512:])
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)

@@ -1,4 +1,4 @@
-"""The encoder outputs' gradient in one pass (srpde_att_pool_bn_bwd): e1 / e2 = relu(bn2(y)) of enc1 / enc2 feed the
+"""Fused backward reductions.  The encoder outputs' gradient in one pass (srpde_att_pool_bn_bwd): e1 / e2 = relu(bn2(y)) of enc1 / enc2 feed the
 AttentionGate of their skip connection and the next block's 2x2 max-pool (src/models.py:79-80, 90, 93, 119-130), so
 their gradient is the gate's input gradient plus the max-pool backward, and enc*.bn2's backward reduces over it.
 The fused kernel writes that gradient once and emits the reduction's partial sums; the executor's three-pass path
@@ -11,11 +11,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _step(model, x, t, fuse):
+def _step(model, x, t, fuse, attr="_FUSE_ENC_OUT", keep=("e1", "e2")):
     from superresolution_for_pdes_amd import unet_exec as X
     from superresolution_for_pdes_amd.functional import mse_loss
-    prev = X._FUSE_ENC_OUT
-    X._FUSE_ENC_OUT = fuse
+    prev = getattr(X, attr)
+    setattr(X, attr, fuse)
     X.DEBUG_TAPS = {}
     try:
         for p in model.parameters():
@@ -26,8 +26,8 @@ def _step(model, x, t, fuse):
         taps = X.DEBUG_TAPS
     finally:
         X.DEBUG_TAPS = None
-        X._FUSE_ENC_OUT = prev
-    return {k: v for k, v in taps.items() if k in ("e1", "e2")}, {n: p.grad.clone() for n, p in model.named_parameters()}
+        setattr(X, attr, prev)
+    return {k: v for k, v in taps.items() if k in keep}, {n: p.grad.clone() for n, p in model.named_parameters()}
 
 
 @pytest.mark.parametrize("n", [4, 37])
@@ -58,3 +58,65 @@ def test_fused_encoder_output_backward_matches_three_passes(n):
         worst = max(worst, rel)
         assert rel < 2e-5, (name, rel)
     print(f"worst parameter-gradient relative difference {worst:.2e}")
+
+
+@pytest.mark.parametrize("n", [3, 33])
+def test_upsample_backward_bn_reduction_matches_separate_pass(n):
+    """dec2.bn2 / dec3.bn2's backward reduction formed by the upsample backward that writes their output
+    gradient (srpde_upsample_bilinear_bwd_gated_bn) against the separate reduction pass: the upsample's output
+    (d2) EQUAL bit for bit, d3 (after dec2's backward) and every parameter gradient within fp32 summation-order rounding."""
+    from oracle import unet_ref as U   # (test infrastructure: the seeded reference initialisation)
+    from superresolution_for_pdes_amd.models import UNet
+    model = UNet()
+    model.load_state_dict(U.kaiming_init_state(5))
+    model = model.to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(7 + n)
+    x = torch.randn(n, 3, 40, 40, device=DEV, generator=g)
+    x[:, 1] = 1.0
+    t = torch.randn(n, 1, 40, 40, device=DEV, generator=g)
+    taps_f, grads_f = _step(model, x, t, True, "_FUSE_UP_BN", ("d2", "d3"))
+    taps_u, grads_u = _step(model, x, t, False, "_FUSE_UP_BN", ("d2", "d3"))
+    assert set(taps_f) == {"d2", "d3"}
+    assert torch.equal(taps_f["d2"], taps_u["d2"])   # written before any changed reduction is read
+    d3 = float((taps_f["d3"] - taps_u["d3"]).double().norm() / taps_u["d3"].double().norm())
+    assert d3 < 1e-5, d3
+    worst = 0.0
+    for name, gu in grads_u.items():
+        if name.endswith(("conv1.bias", "conv2.bias")) or name in ("bridge.0.bias", "bridge.3.bias"):
+            continue   # BN-fed conv biases: true gradient 0, rounding noise only
+        rel = float((grads_f[name] - gu).double().norm() / max(float(gu.double().norm()), 1e-30))
+        worst = max(worst, rel)
+        assert rel < 2e-5, (name, rel)
+    print(f"worst parameter-gradient relative difference {worst:.2e}")
+
+
+def test_upsample_bn_partials_match_bn_reduction():
+    """The kernel's partials and max|dx| slots, summed, equal bn_bwd_prepare's own reduction pass on the same
+    (y, dx) to fp32 rounding: dgamma / dbeta and the m1 / m2 terms."""
+    from superresolution_for_pdes_amd import hipops as H
+    n, h, w, c = 6, 20, 20, 128
+    ho, wo = 2 * h, 2 * w
+    g = torch.Generator(device=DEV).manual_seed(3)
+    dout = torch.randn(n * ho * wo, c, device=DEV, generator=g)
+    dsa = torch.randn(n * ho * wo, device=DEV, generator=g)
+    wg = torch.randn(c, device=DEV, generator=g)
+    y = torch.randn(n * h * w, c, device=DEV, generator=g)
+    mean = y.mean(0)
+    invstd = 1.0 / (y.var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = torch.rand(c, device=DEV, generator=g) + 0.5
+    beta = torch.randn(c, device=DEV, generator=g) * 0.1
+    dx_a, dx_b = H.empty(n * h * w, c, device=DEV), H.empty(n * h * w, c, device=DEV)
+    part, da_max = H.upsample_bwd(dout, dx_a, n, h, w, ho, wo, False, gate=(dsa, wg), bn=(y, mean, invstd, gamma, beta))
+    assert H.upsample_bwd(dout, dx_b, n, h, w, ho, wo, False, gate=(dsa, wg)) is None
+    torch.cuda.synchronize()
+    assert torch.equal(dx_a, dx_b)
+    assert float(da_max.max()) == float(dx_a.abs().max())
+    outs = []
+    for pt in ((part, da_max), None):
+        dg, db, dbias = (torch.empty(c, device=DEV) for _ in range(3))
+        m1, m2, word = H.bn_bwd_prepare(y, dx_a, mean, invstd, gamma, beta, dg, db, dbias,
+                                        part=None if pt is None else pt[0], da_max=None if pt is None else pt[1])
+        outs.append((dg, db, m1, m2))
+    for a, b in zip(*outs):
+        rel = float((a - b).double().norm() / b.double().norm())
+        assert rel < 1e-5, rel
