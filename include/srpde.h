@@ -55,7 +55,7 @@ typedef struct ihipStream_t* hipStream_t;
  *      family is SRPDE_FAM_* bits of srpde_conv_fwd_h3's / _presplit's accumulate argument and of
  *      srpde_conv_h3_stats_rows_for's new flags argument, the grid-CG abort hook a negative rtol;
  *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL
- *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported */
+ *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported, srpde_gating_bn_reduce(_blocks) */
 #define SRPDE_ABI_VERSION 11
 
 /* Kernel-family bits (per call; bit 0 of the same argument is the accumulate flag): the forward / dgrad
@@ -396,6 +396,14 @@ int srpde_upsample_bilinear_bwd_gated(const float* dout, int lddo, const float* 
  * partials (sum dz, sum dz*xhat) and da_max[n*h] max|dx| per input row, the (part, da_max) pair
  * srpde_bn_bwd_prepare / srpde_bn_relu_bwd_part take, so the BN backward does not re-read dx.  Shapes:
  * srpde_upsample_bwd_bn_supported (the row-blocked kernel). */
+/* The attention gate's gating gradient dg[p][c] += dsa[p] * wg[c] (srpde_att_bwd's dg pass, called with dg = NULL
+ * to leave it out) fused with the backward reduction of the BN (+ ReLU) whose output gradient dg is -- the
+ * bridge's last BN under att3's gating signal (models.py:46-48, 88): part [srpde_gating_bn_reduce_blocks][C]
+ * float2 and da_max[blocks], the pair srpde_bn_bwd_prepare / srpde_bn_relu_bwd_part take.  C / 4 divides 256. */
+int srpde_gating_bn_reduce_blocks(long long P, int C);
+int srpde_gating_bn_reduce(const float* dsa, const float* wg, float* dg, int lddg, const float* y, int ldy,
+                           const float* mean, const float* invstd, const float* gamma, const float* beta, long long P,
+                           int C, int flags, void* part, float* da_max, hipStream_t stream);
 int srpde_upsample_bwd_bn_supported(int h, int w, int ho, int wo, int c, int lddo, int lddx);
 int srpde_upsample_bilinear_bwd_gated_bn(const float* dout, int lddo, const float* dsa, const float* wg, float* dx,
                                          int lddx, int n, int h, int w, int ho, int wo, int c, const float* y, int ldy,

@@ -385,6 +385,74 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   }
 }
 
+// The attention gate's gating gradient accumulated into dg (pointwise.hip att_bwd_gating_kernel's
+// expressions: dg[p][c] += dsa[p] * wg[c]) together with the backward reduction of the BN (+ ReLU) whose
+// output gradient dg then is (bn_bwd_reduce_kernel's expressions and partial layout) -- the bridge's last BN
+// under att3's gating signal (src/models.py:46-48, 88): one pass instead of the gating pass plus a
+// reduction pass that re-read dg.
+__global__ __launch_bounds__(256) void gating_bn_reduce_kernel(const float* __restrict__ dsa, const float* __restrict__ wg,
+                                                               float* dg, int lddg, const float* __restrict__ y,
+                                                               int ldy, const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, long long P, int C,
+                                                               int rows_per_blk, int relu, float2* __restrict__ part,
+                                                               float* __restrict__ da_max) {
+  extern __shared__ float4 red4[];  // [2][256]
+  int c4, r0, rs;
+  thread_rc(C, &c4, &r0, &rs);
+  const int active = (C >> 2) * rs;
+  const int c = c4 * 4;
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  float dmax = 0.f;
+  if ((int)threadIdx.x < active) {
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    const float4 w = *reinterpret_cast<const float4*>(wg + c);
+    const long long pb = (long long)blockIdx.x * rows_per_blk;
+    const long long pe = min(P, pb + rows_per_blk);
+    auto row = [&](long long p, const float4& v, const float4& old) {
+      const float sp = dsa[p];
+      float4 d = make_float4(sp * w.x, sp * w.y, sp * w.z, sp * w.w);
+      d.x += old.x; d.y += old.y; d.z += old.z; d.w += old.w;
+      *reinterpret_cast<float4*>(dg + p * lddg + c) = d;
+      dmax = fmaxf(dmax, fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fmaxf(fabsf(d.z), fabsf(d.w))));
+      float xh, dz;
+#define GBN_ACC(X)                                             \
+  xh = (v.X - mu.X) * is.X;                                    \
+  dz = (!(relu & 1) || xh * g.X + b.X > 0.f) ? d.X : 0.f;      \
+  s1.X += dz;                                                  \
+  s2.X += dz * xh;
+      GBN_ACC(x) GBN_ACC(y) GBN_ACC(z) GBN_ACC(w)
+#undef GBN_ACC
+    };
+    bn_rows(pb + r0, pe, rs, y, ldy, dg, lddg, c, row);
+  }
+  red4[threadIdx.x] = s1;
+  red4[256 + threadIdx.x] = s2;
+  __syncthreads();
+  if ((int)threadIdx.x < (C >> 2)) {
+    float4 t1 = make_float4(0.f, 0.f, 0.f, 0.f), t2 = t1;
+    for (int r = 0; r < rs; ++r) {
+      const float4 a = red4[r * (C >> 2) + threadIdx.x], b2 = red4[256 + r * (C >> 2) + threadIdx.x];
+      t1.x += a.x; t1.y += a.y; t1.z += a.z; t1.w += a.w;
+      t2.x += b2.x; t2.y += b2.y; t2.z += b2.z; t2.w += b2.w;
+    }
+    float2* o = part + (size_t)blockIdx.x * C + c;
+    o[0] = make_float2(t1.x, t2.x); o[1] = make_float2(t1.y, t2.y);
+    o[2] = make_float2(t1.z, t2.z); o[3] = make_float2(t1.w, t2.w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+  __syncthreads();
+  float* wmx = reinterpret_cast<float*>(red4);
+  if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = dmax;
+  __syncthreads();
+  if (threadIdx.x == 0) da_max[blockIdx.x] = fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]));
+}
+
 // fp64 column sums of [nblk][C] float2 partials -> out0[C], out1[C]; one block per channel
 __global__ __launch_bounds__(256) void colsum2_kernel(const float2* __restrict__ part, int nblk, int C,
                                                       float* out0, float* out1, double* keep0, double* keep1) {
@@ -1169,6 +1237,28 @@ int srpde_bn_bwd_prepare(const float* y, int ldy, const float* da, int ldda, con
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(1), dim3(256), 0, stream, sdz, sdzx, P, C, invstd, gamma,
                      (flags & SRPDE_BN_EVAL) ? 1 : 0, da_max, n_da_max, m1, m2, dbias, dy_amax);
   SRPDE_LAUNCH_CHECK("srpde_bn_bwd_prepare(coef)");
+  return 0;
+}
+
+int srpde_gating_bn_reduce_blocks(long long P, int C) {
+  int rpb;
+  return bwd_blocks(P, C, &rpb);
+}
+
+int srpde_gating_bn_reduce(const float* dsa, const float* wg, float* dg, int lddg, const float* y, int ldy,
+                           const float* mean, const float* invstd, const float* gamma, const float* beta, long long P,
+                           int C, int flags, void* part, float* da_max, hipStream_t stream) {
+  SRPDE_CHECK_ARG(dsa && wg && dg && y && mean && invstd && gamma && beta && part && da_max && P > 0,
+                  "srpde_gating_bn_reduce: null argument");
+  SRPDE_CHECK_ARG(C % 4 == 0 && C <= 1024 && (256 % (C / 4)) == 0 && lddg % 4 == 0 && ldy % 4 == 0 && aligned16(dg) &&
+                      aligned16(y),
+                  "srpde_gating_bn_reduce: C / 4 must divide 256, row strides multiples of 4, 16-byte aligned");
+  int rpb;
+  const int nblk = bwd_blocks(P, C, &rpb);
+  hipLaunchKernelGGL(gating_bn_reduce_kernel, dim3(nblk), dim3(256), 2 * 256 * sizeof(float4), stream, dsa, wg, dg, lddg,
+                     y, ldy, mean, invstd, gamma, beta, P, C, rpb, flags & SRPDE_BN_RELU, static_cast<float2*>(part),
+                     da_max);
+  SRPDE_LAUNCH_CHECK("srpde_gating_bn_reduce");
   return 0;
 }
 

@@ -812,6 +812,21 @@ def upsample_bwd(dout, dx, n, h, w, ho, wo, accumulate, gate=None, bn=None):
     return None
 
 
+def gating_bn_reduce(dsa, wg, dg, y, mean, invstd, gamma, beta):
+    """dg += dsa (x) wg (the gating gradient att_bwd(dg=None) left out) with the backward reduction of the BN +
+    ReLU whose output gradient dg is -> (part [blocks, C, 2], da_max [blocks]) (srpde_gating_bn_reduce)."""
+    P, C = y.shape
+    pdg, lddg = _pl(dg)
+    py, ldy = _pl(y)
+    nb = int(query("srpde_gating_bn_reduce_blocks", P, C))
+    part = empty(nb, C, 2, device=dg.device)
+    da_max = empty(nb, device=dg.device)
+    call("srpde_gating_bn_reduce", dsa.data_ptr(), wg.data_ptr(), pdg, lddg, py, ldy, mean.data_ptr(),
+         invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, C, BN_RELU, part.data_ptr(), da_max.data_ptr(),
+         stream_ptr())
+    return part, da_max
+
+
 # ----------------------------------- attention -------------------------------------
 def att_fwd(x, g, n, hw, w1, b1, w2, b2, wg, bg, out=None):
     c, gc = x.shape[1], g.shape[1]

@@ -656,6 +656,9 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True,
                      activate=activate, att=att)
 
 
+# bridge[4]'s backward reduction formed with att3's gating gradient (_FUSE_GATING_BN False: the att_bwd dg pass and a
+# separate reduction pass)
+_FUSE_GATING_BN = True
 # the decoder blocks' bn2 backward reduction formed inside the upsample backward (_FUSE_UP_BN False: a
 # separate reduction pass re-reads the upsample's output)
 _FUSE_UP_BN = True
@@ -910,12 +913,20 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     _tap("e3a", dcat3[:, 512:])
     ready("dec3")
     de3 = H.empty(P3, 256, device=dev)
-    _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True, wq=wq)
+    bpart = None
+    if _FUSE_GATING_BN:
+        # the gating gradient into db = dcat3[:, :512] together with bridge[4]'s backward reduction
+        gate = _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, None, True, wq=wq)
+        _, _, yb, mb, ib, _, _ = S.br2
+        bpart = H.gating_bn_reduce(gate[0], gate[1], dcat3[:, :512], yb, mb, ib, m.bridge[4].weight,
+                                   m.bridge[4].bias)
+    else:
+        _att_bwd(m.att3, S.att3, dcat3[:, 512:], S.e3, S.b, n, hw3, grads, de3, False, dcat3[:, :512], True, wq=wq)
     _tap("b", dcat3[:, :512])
     ready("att3")
     # bridge: db = dcat3[:, :512]; its dgrad accumulates into de3
     dab1 = H.empty(P3, 512, device=dev)
-    part = _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1,
+    part = _cbr_bwd(m.bridge[3], m.bridge[4], S.br2, dcat3[:, :512], n, h3, w3, 2, grads, slots, dab1, part=bpart,
                     below=(m.bridge[1], S.br1), wq=wq)
     _tap("b1", dab1)
     _cbr_bwd(m.bridge[0], m.bridge[1], S.br1, dab1, n, h3, w3, 2, grads, slots, de3, True, part=part, wq=wq)

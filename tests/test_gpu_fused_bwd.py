@@ -120,3 +120,62 @@ def test_upsample_bn_partials_match_bn_reduction():
     for a, b in zip(*outs):
         rel = float((a - b).double().norm() / b.double().norm())
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("n", [2, 17])
+def test_gating_bn_reduction_matches_separate_passes(n):
+    """bridge[4]'s backward reduction formed with att3's gating gradient (srpde_gating_bn_reduce) against the
+    att_bwd dg pass plus a separate reduction: db (the bridge output's gradient) within fp32 rounding of the
+    same sum, every parameter gradient within summation-order rounding."""
+    from oracle import unet_ref as U   # (test infrastructure: the seeded reference initialisation)
+    from superresolution_for_pdes_amd.models import UNet
+    model = UNet()
+    model.load_state_dict(U.kaiming_init_state(9))
+    model = model.to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(21 + n)
+    x = torch.randn(n, 3, 40, 40, device=DEV, generator=g)
+    x[:, 1] = 1.0
+    t = torch.randn(n, 1, 40, 40, device=DEV, generator=g)
+    taps_f, grads_f = _step(model, x, t, True, "_FUSE_GATING_BN", ("b",))
+    taps_u, grads_u = _step(model, x, t, False, "_FUSE_GATING_BN", ("b",))
+    db = float((taps_f["b"] - taps_u["b"]).double().norm() / taps_u["b"].double().norm())
+    assert db < 1e-6, db
+    worst = 0.0
+    for name, gu in grads_u.items():
+        if name.endswith(("conv1.bias", "conv2.bias")) or name in ("bridge.0.bias", "bridge.3.bias"):
+            continue   # BN-fed conv biases: true gradient 0, rounding noise only
+        rel = float((grads_f[name] - gu).double().norm() / max(float(gu.double().norm()), 1e-30))
+        worst = max(worst, rel)
+        assert rel < 2e-5, (name, rel)
+    print(f"db {db:.2e}, worst parameter-gradient relative difference {worst:.2e}")
+
+
+def test_gating_bn_partials_match_bn_reduction():
+    """srpde_gating_bn_reduce's dg equals dg + dsa (x) wg formed in fp64 to fp32 rounding, and its partials /
+    max slots give bn_bwd_prepare the terms of its own reduction pass."""
+    from superresolution_for_pdes_amd import hipops as H
+    P, C = 4 * 100, 512
+    g = torch.Generator(device=DEV).manual_seed(4)
+    dsa = torch.randn(P, device=DEV, generator=g)
+    wg = torch.randn(C, device=DEV, generator=g)
+    dg0 = torch.randn(P, C, device=DEV, generator=g)
+    y = torch.randn(P, C, device=DEV, generator=g)
+    mean = y.mean(0)
+    invstd = 1.0 / (y.var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = torch.rand(C, device=DEV, generator=g) + 0.5
+    beta = torch.randn(C, device=DEV, generator=g) * 0.1
+    dg = dg0.clone()
+    part, da_max = H.gating_bn_reduce(dsa, wg, dg, y, mean, invstd, gamma, beta)
+    torch.cuda.synchronize()
+    ref = dg0.double() + dsa.double()[:, None] * wg.double()[None, :]
+    assert float((dg.double() - ref).abs().max()) <= 4e-7 * float(ref.abs().max())
+    assert float(da_max.max()) == float(dg.abs().max())
+    outs = []
+    for pt in ((part, da_max), None):
+        dgm, db, dbias = (torch.empty(C, device=DEV) for _ in range(3))
+        m1, m2, word = H.bn_bwd_prepare(y, dg, mean, invstd, gamma, beta, dgm, db, dbias,
+                                        part=None if pt is None else pt[0], da_max=None if pt is None else pt[1])
+        outs.append((dgm, db, m1, m2))
+    for a, b in zip(*outs):
+        rel = float((a - b).double().norm() / b.double().norm())
+        assert rel < 1e-5, rel
