@@ -672,14 +672,22 @@ def _up_bn(blk, saved):
     return y, mean, invstd, blk.bn2.weight, blk.bn2.bias
 
 
-def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None):
-    """``part``: bn2's backward reduction, when the dgrad that wrote ``da`` produced it."""
+def _block_bwd(blk, saved, da, n, h, w, grads, slots, dx, dx_accumulate=False, wq=None, part=None, last=False):
+    """``part``: bn2's backward reduction, when the dgrad that wrote ``da`` produced it.  ``last``: the backward's
+    final block (enc1): conv1's weight gradient runs in line on the compute stream, which would otherwise sit idle
+    waiting for the side stream's queue (enc1.conv2's weight gradient) at the join (_INLINE_LAST_WGRAD)."""
     s1, s2 = saved
     P = n * h * w
     da1 = H.empty(P, blk.conv1.out_channels, device=da.device)
     part = _cbr_bwd(blk.conv2, blk.bn2, s2, da, n, h, w, 1, grads, slots, da1, part=part, below=(blk.bn1, s1),
                     wq=wq)
-    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part, wq=wq)
+    _cbr_bwd(blk.conv1, blk.bn1, s1, da1, n, h, w, 1, grads, slots, dx, dx_accumulate, part=part,
+             wq=None if last and _INLINE_LAST_WGRAD else wq)
+
+
+# the last block's conv1 weight gradient in line on the compute stream (False: on the side stream, queued behind
+# enc1.conv2's, while the compute stream waits at the join)
+_INLINE_LAST_WGRAD = True
 
 
 def _att_params(att):
@@ -952,7 +960,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
         H.maxpool_bwd(S.e1, dp1, de1, n, h, w, True)
     _tap("e1", de1)
     dx4 = H.empty(P1, S.x4.shape[1], device=dev) if want_dx else None
-    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, dx4, wq=wq, part=part)
+    _block_bwd(m.enc1, S.enc1, de1, n, h, w, grads, slots, dx4, wq=wq, part=part, last=True)
     ready("enc1")
     if wq is not None:
         wq.join()
