@@ -55,7 +55,8 @@ typedef struct ihipStream_t* hipStream_t;
  *      family is SRPDE_FAM_* bits of srpde_conv_fwd_h3's / _presplit's accumulate argument and of
  *      srpde_conv_h3_stats_rows_for's new flags argument, the grid-CG abort hook a negative rtol;
  *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL
- *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported, srpde_gating_bn_reduce(_blocks) */
+ *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported, srpde_gating_bn_reduce(_blocks),
+ *      srpde_att_bwd_params_lowres */
 #define SRPDE_ABI_VERSION 11
 
 /* Kernel-family bits (per call; bit 0 of the same argument is the accumulate flag): the forward / dgrad
@@ -453,6 +454,13 @@ int srpde_att_pool_bn_bwd(const float* dout, int lddo, const float* ca, const fl
 int srpde_att_bwd_params(const float* g, int ldg, int n, int hw, int c, int gc, const float* m, const float* hbuf,
                          float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg, void* workspace,
                          size_t ws_bytes, hipStream_t stream);
+/* srpde_att_bwd_params for a gate whose gating input is the bilinear x2 upsample of d ([n*h*w][gc], the decoder
+ * block's low-res output, models.py:89 / :92, hw = ho*wo the gate's resolution): the spatial conv's weight
+ * gradient sum_p dsa[p] up(d)[p] is formed as sum_q d[q] (up^T dsa)[q] over the low-res rows (4x fewer bytes
+ * read; the same sum regrouped, fp32 rounding apart), the bias gradient as sum_q (up^T dsa)[q]. */
+int srpde_att_bwd_params_lowres(const float* d, int ldd, int n, int h, int w, int ho, int wo, int c, int gc,
+                                const float* m, const float* hbuf, float* dw1, float* db1, float* dw2, float* db2,
+                                float* dwg, float* dbg, void* workspace, size_t ws_bytes, hipStream_t stream);
 
 /* ---- output head: final 1x1 conv + residual x[:,0:1] (models.py:61,74,98,101) ------- */
 int srpde_head_fwd(const float* z, int ldz, int c, const float* wf, const float* bf, const float* xin, int xin_c,

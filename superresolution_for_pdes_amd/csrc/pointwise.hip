@@ -1466,6 +1466,88 @@ int srpde_att_bwd(const float* dout, int lddo, const float* x, int ldx, const fl
                               stream);
 }
 
+// sT[q] = sum of w(p, q) dsa[p] over the output pixels p that interpolate from low-res pixel q: the transpose of the
+// bilinear x2 upsample (align_corners, models.py:89 / :92) on one channel, each low-res pixel gathering its
+// candidate rows and columns in a fixed order (upsample_bwd_rows_kernel's candidate test)
+__global__ __launch_bounds__(256) void upsample_t_scalar_kernel(const float* __restrict__ dsa, float* __restrict__ st,
+                                                                int n, int h, int w, int ho, int wo) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)n * h * w) return;
+  const int ix = (int)(q % w), iy = (int)((q / w) % h), nn = (int)(q / ((long long)w * h));
+  int ylo, yhi, xlo, xhi;
+  cand_range(iy, h, ho, &ylo, &yhi);
+  cand_range(ix, w, wo, &xlo, &xhi);
+  const float* base = dsa + (size_t)nn * ho * wo;
+  float s = 0.f;
+  for (int oy = ylo; oy <= yhi; ++oy) {
+    bool hy;
+    const float wy = cand_weight(oy, iy, h, ho, &hy);
+    if (!hy) continue;
+    float r = 0.f;
+    for (int ox = xlo; ox <= xhi; ++ox) {
+      bool hx;
+      const float wx = cand_weight(ox, ix, w, wo, &hx);
+      if (hx) r += wx * base[(size_t)oy * wo + ox];
+    }
+    s += wy * r;
+  }
+  st[q] = s;
+}
+
+// the channel MLP's parameter gradients of srpde_att_bwd_params (fixed-order sums over samples)
+static void att_params_outer(int n, int c, const float* m, const float* hbuf, const float* db1r, const float* db2r,
+                             float* dw1, float* db1, float* dw2, float* db2, hipStream_t stream) {
+  const int cr = c / 8;
+  // dW1[r][c] = sum_n dh[n][r] m[n][c];  dW2[c][r] = sum_n dpre[n][c] h[n][r]
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(cr, ceil_div(c, 64)), dim3(1024), 0, stream, db1r, cr, m, c, n, dw1);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(c, ceil_div(cr, 64)), dim3(1024), 0, stream, db2r, c, hbuf, cr, n, dw2);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(cr, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
+                     db1r, cr, n, db1);
+  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(c, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
+                     db2r, c, n, db2);
+}
+
+int srpde_att_bwd_params_lowres(const float* d, int ldd, int n, int h, int w, int ho, int wo, int c, int gc,
+                                const float* m, const float* hbuf, float* dw1, float* db1, float* dw2, float* db2,
+                                float* dwg, float* dbg, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(d && m && hbuf && dw1 && db1 && dw2 && db2 && dwg && dbg && workspace && ldd % 4 == 0 && gc % 4 == 0 &&
+                      c % 32 == 0 && ho >= h && wo >= w,
+                  "srpde_att_bwd_params_lowres: bad args");
+  const int hw = ho * wo;
+  if (ws_bytes < srpde_att_bwd_workspace_size(n, hw, c, gc)) {
+    set_error("srpde_att_bwd_params_lowres: workspace too small");
+    return kErrWorkspace;
+  }
+  const long long P = (long long)n * hw, Plo = (long long)n * h * w;
+  const int cr = c / 8;
+  float* dsa = static_cast<float*>(workspace);
+  float* dm = dsa + P;
+  float* dw1r = dm + (size_t)n * c;
+  float* dw2r = dw1r + (size_t)n * cr * c;
+  float* db1r = dw2r + (size_t)n * cr * c;
+  float* db2r = db1r + (size_t)n * cr;
+  float2* part = reinterpret_cast<float2*>(db2r + (size_t)n * c + 2);
+  part = reinterpret_cast<float2*>((reinterpret_cast<uintptr_t>(part) + 15) & ~uintptr_t(15));
+  SRPDE_CHECK_ARG(Plo <= 2LL * n * cr * c, "srpde_att_bwd_params_lowres: low-res field larger than its scratch");
+  float* st = dw1r;   // the per-sample MLP rows' region, unused by the parameter pass
+  att_params_outer(n, c, m, hbuf, db1r, db2r, dw1, db1, dw2, db2, stream);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd_params_lowres(rowsum)");
+  // dwg[k] = sum_p dsa[p] up(d)[p][k] = sum_q d[q][k] sT[q]; dbg = sum_p dsa[p] = sum_q sT[q] (the weights of an
+  // output pixel sum to 1): the weighted column sums run over the low-res d, 1/4 of up(d)'s rows
+  hipLaunchKernelGGL(upsample_t_scalar_kernel, dim3((unsigned)((Plo + 255) / 256)), dim3(256), 0, stream, dsa, st, n, h,
+                     w, ho, wo);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd_params_lowres(transpose)");
+  int rpb;
+  const int nb = colsum_blocks(Plo, gc, &rpb);
+  hipLaunchKernelGGL(weighted_colsum_kernel, dim3(nb), dim3(256), 2 * 256 * sizeof(float4), stream, d, ldd, st, Plo,
+                     gc, rpb, part);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd_params_lowres(colsum)");
+  hipLaunchKernelGGL(partsum_kernel, dim3(gc), dim3(256), 0, stream, part, nb, gc + 1, dwg);
+  hipLaunchKernelGGL(partsum_kernel, dim3(1), dim3(256), 0, stream, part + gc, nb, gc + 1, dbg);
+  SRPDE_LAUNCH_CHECK("srpde_att_bwd_params_lowres(partsum)");
+  return 0;
+}
+
 int srpde_att_bwd_params(const float* g, int ldg, int n, int hw, int c, int gc, const float* m, const float* hbuf,
                          float* dw1, float* db1, float* dw2, float* db2, float* dwg, float* dbg, void* workspace,
                          size_t ws_bytes, hipStream_t stream) {
@@ -1486,14 +1568,8 @@ int srpde_att_bwd_params(const float* g, int ldg, int n, int hw, int c, int gc, 
   float2* part = reinterpret_cast<float2*>(db2r + (size_t)n * c + 2);
   part = reinterpret_cast<float2*>((reinterpret_cast<uintptr_t>(part) + 15) & ~uintptr_t(15));
   // parameter grads: fixed-order sums over samples / pixel blocks
-  (void)dw1r; (void)dw2r;
-  // dW1[r][c] = sum_n dh[n][r] m[n][c];  dW2[c][r] = sum_n dpre[n][c] h[n][r]
-  hipLaunchKernelGGL(outer_sum_kernel, dim3(cr, ceil_div(c, 64)), dim3(1024), 0, stream, db1r, cr, m, c, n, dw1);
-  hipLaunchKernelGGL(outer_sum_kernel, dim3(c, ceil_div(cr, 64)), dim3(1024), 0, stream, db2r, c, hbuf, cr, n, dw2);
-  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(cr, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
-                     db1r, cr, n, db1);
-  hipLaunchKernelGGL(outer_sum_kernel, dim3(1, ceil_div(c, 64)), dim3(1024), 0, stream, (const float*)nullptr, 1,
-                     db2r, c, n, db2);
+  (void)dw1r; (void)dw2r; (void)cr;
+  att_params_outer(n, c, m, hbuf, db1r, db2r, dw1, db1, dw2, db2, stream);
   SRPDE_LAUNCH_CHECK("srpde_att_bwd(rowsum)");
   int rpb;
   const int nb = colsum_blocks(P, gc, &rpb);

@@ -876,14 +876,16 @@ def att_gate_fwd(x, g, n, hw, chan, wg, bg, out=None):
 
 
 def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, db1, dw2, db2, dwg, dbg,
-            defer_params=False, want_dsa=False, want_dm=False):
+            defer_params=False, want_dsa=False, want_dm=False, g_lowres=None):
     """AttentionGate backward.  Returns (dsa or None, params): ``dsa`` (when ``dg`` is None, or
     ``want_dsa``) is the gating gradient's per-pixel factor d loss / d(spatial pre-activation), for
     upsample_bwd(gate=...); the spatial bias gradient is its sum; ``params`` (when
     ``defer_params``) is a callable that launches the parameter-gradient reductions on the
     current stream, to be queued after this call (reads ``ws``, ``g``, ``m``, ``hb``).
     ``dx=None``: the input gradient is left to att_pool_bn_bwd; ``want_dm`` then appends the channel
-    branch's term dm [n, c] (a view into the workspace) to the returned tuple."""
+    branch's term dm [n, c] (a view into the workspace) to the returned tuple.  ``g_lowres = (d, h, w, ho, wo)``:
+    g is up(d), and the spatial conv's weight gradient is formed from the low-res d
+    (srpde_att_bwd_params_lowres)."""
     m, hb, ca, sa = saved
     c, gc = x.shape[1], g.shape[1]
     ws_bytes = int(query("srpde_att_bwd_workspace_size", n, hw, c, gc))
@@ -894,15 +896,28 @@ def att_bwd(dout, x, g, n, hw, w1, w2, wg, saved, dx, dx_acc, dg, dg_acc, dw1, d
     pdx, lddx = _pl(dx) if dx is not None else (0, 0)
     pdg, lddg = _pl(dg) if dg is not None else (0, 0)
     pgrads = (dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), dwg.data_ptr(), dbg.data_ptr())
+    later = defer_params or g_lowres is not None   # the parameter pass as its own call (below)
     call("srpde_att_bwd", pdo, lddo, px, ldx, pg, ldg, n, hw, c, gc, w1.data_ptr(), w2.data_ptr(), wg.data_ptr(),
          m.data_ptr(), hb.data_ptr(), ca.data_ptr(), sa.data_ptr(), pdx, lddx, int(dx_acc), pdg, lddg, int(dg_acc),
-         *((0,) * 6 if defer_params else pgrads), ws.data_ptr(), ws_bytes, stream_ptr())
+         *((0,) * 6 if later else pgrads), ws.data_ptr(), ws_bytes, stream_ptr())
     params = None
-    if defer_params:
-        def params():
-            call("srpde_att_bwd_params", pg, ldg, n, hw, c, gc, m.data_ptr(), hb.data_ptr(), *pgrads, ws.data_ptr(),
-                 ws_bytes, stream_ptr())
-        params.keep = (ws,)
+    if later:
+        if g_lowres is not None:
+            d, h, w, ho, wo = g_lowres
+            pd, ldd = _pl(d)
+
+            def params():
+                call("srpde_att_bwd_params_lowres", pd, ldd, n, h, w, ho, wo, c, gc, m.data_ptr(), hb.data_ptr(),
+                     *pgrads, ws.data_ptr(), ws_bytes, stream_ptr())
+            params.keep = (ws, d)
+        else:
+            def params():
+                call("srpde_att_bwd_params", pg, ldg, n, hw, c, gc, m.data_ptr(), hb.data_ptr(), *pgrads,
+                     ws.data_ptr(), ws_bytes, stream_ptr())
+            params.keep = (ws,)
+        if not defer_params:   # in line: the same parameter pass, now
+            params()
+            params = None
     # the gating gradient's per-pixel factor, for upsample_bwd(gate=(dsa, wg))
     dsa = ws[:4 * x.shape[0]].view(torch.float32) if dg is None or want_dsa else None
     if want_dm:   # workspace [P floats of dsa | n * c floats of dm | ...] (srpde_att_bwd_workspace_size)

@@ -656,6 +656,9 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True,
                      activate=activate, att=att)
 
 
+# the decoder gates' spatial weight gradient from the low-res decoder output d (sum_q d[q] up^T(dsa)[q]) instead of
+# the upsampled g = up(d), a quarter of the rows (False: from g)
+_GATE_WGRAD_LOWRES = True
 # bridge[4]'s backward reduction formed with att3's gating gradient (_FUSE_GATING_BN False: the att_bwd dg pass and a
 # separate reduction pass)
 _FUSE_GATING_BN = True
@@ -734,14 +737,15 @@ def _att_channel_early(att, x, n, hw):
     return H.att_channel_fwd(x, n, hw, c1.weight, c1.bias, c3.weight, c3.bias), None
 
 
-def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None, defer_dx=False):
+def _att_bwd(att, saved, dout, x, g, n, hw, grads, dx, dx_acc, dg, dg_acc, wq=None, defer_dx=False, g_lowres=None):
     """``dg=None``: the gating gradient is not applied; returns the gate for upsample_bwd.
     ``wq``: the parameter-gradient reductions go to the weight-gradient side stream.
     ``defer_dx`` (``dx`` None): the input gradient is formed later by att_pool_bn_bwd; returns (gate, dm)."""
     c1, c3, s0 = _att_params(att)
     out = H.att_bwd(dout, x, g, n, hw, c1.weight, c3.weight, s0.weight, saved, dx, dx_acc, dg, dg_acc,
                     grads[c1.weight], grads[c1.bias], grads[c3.weight], grads[c3.bias], grads[s0.weight],
-                    grads[s0.bias], defer_params=wq is not None, want_dsa=DEBUG_TAPS is not None, want_dm=defer_dx)
+                    grads[s0.bias], defer_params=wq is not None, want_dsa=DEBUG_TAPS is not None, want_dm=defer_dx,
+                    g_lowres=g_lowres if _GATE_WGRAD_LOWRES else None)
     dsa, params = out[0], out[1]
     if DEBUG_TAPS is not None:
         _tap("dsa_pre:" + getattr(att, "_srpde_name", "?"), dsa)
@@ -809,9 +813,11 @@ def unet_forward(m, x, training, save=False):
     e3a, S.att3 = _att_fwd(m.att3, e3, b, n, hw3, early=ch3, sa=sa3)
     d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
     fuse_up = not training and not save   # inference: the decoder convs read up(d) without it being formed
+    S.d3 = d3 if (training and _GATE_WGRAD_LOWRES) else None   # the gate's spatial weight gradient reads it
     u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2, m.dec2.conv1, e2.shape[1], fuse_up)
     e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2, sa=sa2)
     d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
+    S.d2 = d2 if (training and _GATE_WGRAD_LOWRES) else None
     u2, sa1 = _upsample_for_gate(d2, m.att1, n, h2, w2, h, w, m.dec1.conv1, e1.shape[1], fuse_up)
     e1a, S.att1 = _att_fwd(m.att1, e1, u2, n, hw1, early=ch1, sa=sa1)
     # multi-scale head + residual; dec1's output BN + ReLU is applied inside out_conv1's input
@@ -890,7 +896,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     # fusion the gate's input gradient is formed together with the max-pool backward into de1 (enc1's turn, below)
     fuse1 = _fuse_enc_out(S.enc1, 64, w)
     gate = _att_bwd(m.att1, S.att1, dcat1[:, 128:], S.e1, S.u2, n, hw1, grads, None if fuse1 else de1, False, None, True,
-                    wq=wq, defer_dx=fuse1)
+                    wq=wq, defer_dx=fuse1, g_lowres=(S.d2, h2, w2, h, w) if S.d2 is not None else None)
     if fuse1:
         gate, dm1 = gate
     ready("att1")
@@ -908,7 +914,7 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
     fuse2 = _fuse_enc_out(S.enc2, 128, w2)
     gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, None if fuse2 else de2, False, None,
-                    True, wq=wq, defer_dx=fuse2)
+                    True, wq=wq, defer_dx=fuse2, g_lowres=(S.d3, h3, w3, h2, w2) if S.d3 is not None else None)
     if fuse2:
         gate, dm2 = gate
     ready("att2")
