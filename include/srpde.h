@@ -56,7 +56,7 @@ typedef struct ihipStream_t* hipStream_t;
  *      srpde_conv_h3_stats_rows_for's new flags argument, the grid-CG abort hook a negative rtol;
  *      srpde_conv_wgrad_h3g_supported, srpde_att_pool_bn_bwd(_blocks); srpde_att_bwd takes dx == NULL
  *  11  srpde_upsample_bilinear_bwd_gated_bn, srpde_upsample_bwd_bn_supported, srpde_gating_bn_reduce(_blocks),
- *      srpde_att_bwd_params_lowres */
+ *      srpde_att_bwd_params_lowres, srpde_conv_wgrad_bnb */
 #define SRPDE_ABI_VERSION 11
 
 /* Kernel-family bits (per call; bit 0 of the same argument is the accumulate flag): the forward / dgrad
@@ -100,6 +100,14 @@ size_t srpde_conv_wgrad_workspace_size(int n, int h, int w, int cout, int cin, i
 int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx0, const float* x1, int c1,
                      int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout, int ksize,
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* srpde_conv_wgrad (fp32 kernels, one input) whose dY is the BN (+ReLU, flags SRPDE_BN_RELU) backward of the
+ * layer's BatchNorm, applied as the operand is loaded: dy = gamma invstd (dz - m1 - xhat m2), dz = da masked by
+ * the BN output > 0, y the BN input -- srpde_bn_relu_bwd's dy bit for bit from srpde_bn_bwd_prepare's m1 / m2,
+ * never written (enc1.conv1, models.py:16-23 with the input image: no dgrad reads dy). */
+int srpde_conv_wgrad_bnb(const float* da, int ldda, const float* y, int ldy, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, const float* m1, const float* m2, int flags,
+                         const float* x0, int c0, int ldx0, float* dw, int cin_real, int accumulate, int n, int h,
+                         int w, int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream);
 /* h3: the same convolution (forward / dgrad, same output and statistics layout) from
  * two-piece fp16 splits with power-of-two operand scales: three partial products per fp32
  * product on v_mfma_f32_32x32x16_f16, halo-staged activation tiles (conv_h3.hip).

@@ -612,8 +612,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_v2_kernel(ConvParams p) {
 
 constexpr int BKP = 16;  // pixels per stage
 
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
+// The BN (+ReLU) backward applied to the weight gradient's dY operand as it is loaded (enc1.conv1, whose only
+// consumer of dy is this fp32 weight gradient: no dgrad): dy = gamma invstd (dz - m1 - xhat m2), dz = da masked by
+// the recomputed BN output > 0 -- bn_bwd_apply_kernel's expressions with srpde_bn_bwd_prepare's m1 / m2, so the
+// same dy bits, never written.
+struct WgradBn {
+  const float* y; int ldy;
+  const float *mean, *invstd, *gamma, *beta, *m1, *m2;
+  int relu;
+};
+
+template <int BM, int BN, int WM, int WN, bool BNB = false>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p, WgradBn bn = {}) {
   constexpr int TM = BM / WM, TN = BN / WN, TI = TM / 32, TJ = TN / 32;
   constexpr int LDA = BM + 4, LDB = BN + 4;
   constexpr int A_V4_ROW = BM / 4, B_V4_ROW = BN / 4;
@@ -661,8 +671,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
       const int c4 = e % A_V4_ROW, pr = e / A_V4_ROW;
       const int px = pbase + pr, col = m0 + c4 * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < A_TOTAL && px < pend && col < p.Cout)
+      if (e < A_TOTAL && px < pend && col < p.Cout) {
         v = *reinterpret_cast<const float4*>(p.dy + (size_t)px * p.lddy + col);
+        if constexpr (BNB) {
+          const float4 yv = *reinterpret_cast<const float4*>(bn.y + (size_t)px * bn.ldy + col);
+          const float4 mu = *reinterpret_cast<const float4*>(bn.mean + col);
+          const float4 is = *reinterpret_cast<const float4*>(bn.invstd + col);
+          const float4 g = *reinterpret_cast<const float4*>(bn.gamma + col);
+          const float4 bb = *reinterpret_cast<const float4*>(bn.beta + col);
+          const float4 m1 = *reinterpret_cast<const float4*>(bn.m1 + col);
+          const float4 m2 = *reinterpret_cast<const float4*>(bn.m2 + col);
+          float xh, dz;
+#define WG_BN(X)                                                     \
+  xh = (yv.X - mu.X) * is.X;                                         \
+  dz = (!(bn.relu & 1) || xh * g.X + bb.X > 0.f) ? v.X : 0.f;        \
+  v.X = (dz - m1.X - xh * m2.X) * (g.X * is.X);
+          WG_BN(x) WG_BN(y) WG_BN(z) WG_BN(w)
+#undef WG_BN
+        }
+      }
       ra[i] = v;
     }
 #pragma unroll
@@ -1069,10 +1096,13 @@ static int fwd_config(int cout) { return cout % 128 == 0 ? 0 : (cout % 64 == 0 ?
 static int fwd_bm(int cfg) { return cfg == 0 ? 128 : 256; }
 
 template <int BM, int BN, int WM, int WN>
-static int launch_wgrad(const WgradParams& p, hipStream_t st) {
+static int launch_wgrad(const WgradParams& p, hipStream_t st, const WgradBn* bn = nullptr) {
   const int nb = ceil_div(p.Cout, BM) * ceil_div(p.K, BN) * p.splits;
   const size_t lds = (size_t)2 * BKP * ((BM + 4) + (BN + 4)) * sizeof(float);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN>), dim3(nb), dim3(256), lds, st, p);
+  if (bn != nullptr)
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, true>), dim3(nb), dim3(256), lds, st, p, *bn);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, WM, WN, false>), dim3(nb), dim3(256), lds, st, p, WgradBn{});
   SRPDE_LAUNCH_CHECK("srpde_conv_wgrad");
   return 0;
 }
@@ -1185,7 +1215,7 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
                            int ldx1, float* dw, int cin_real, int accumulate, int n, int h, int w, int cout,
                            int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream,
                            const unsigned* amax_dy = nullptr, const unsigned* amax0 = nullptr,
-                           const unsigned* amax1 = nullptr) {
+                           const unsigned* amax1 = nullptr, const WgradBn* bn = nullptr) {
   SRPDE_CHECK_ARG(dy && x0 && dw && workspace, "srpde_conv_wgrad: null pointer");
   SRPDE_CHECK_ARG(c0 % 4 == 0 && c1 % 4 == 0 && lddy % 4 == 0 && ldx0 % 4 == 0 && cout % 4 == 0,
                   "srpde_conv_wgrad: channel counts / strides must be multiples of 4");
@@ -1203,9 +1233,14 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
     return kErrWorkspace;
   }
   p.part = static_cast<float*>(workspace);
-  int bm, bn, rc;
-  wgrad_tiles(cout, p.K, &bm, &bn);
-  if (amax_dy) {
+  int bm, bn_cols, rc;
+  wgrad_tiles(cout, p.K, &bm, &bn_cols);
+  if (bn != nullptr) {   // the fp32 kernel with the BN apply on its dY loads (srpde_conv_wgrad_bnb)
+    if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream, bn);
+    else if (bm == 64)
+      rc = bn_cols == 64 ? launch_wgrad<64, 64, 2, 2>(p, stream, bn) : launch_wgrad<64, 256, 1, 4>(p, stream, bn);
+    else rc = launch_wgrad<32, 256, 1, 4>(p, stream, bn);
+  } else if (amax_dy) {
     SRPDE_CHECK_ARG(c0 % 32 == 0 && c1 % 32 == 0 && cout % 16 == 0 && wgrad_v2_ok(p) && amax0 && (c1 == 0 || amax1),
                     "srpde_conv_wgrad_h3: needs c0, c1 multiples of 32, cout of 16 and the amax words (c0=%d c1=%d cout=%d)",
                     c0, c1, cout);
@@ -1216,7 +1251,7 @@ static int conv_wgrad_impl(const float* dy, int lddy, const float* x0, int c0, i
     else rc = launch_wgrad_v2<32, 256, 1, 4>(p, stream);
   } else {
     if (bm == 128) rc = launch_wgrad<128, 128, 2, 2>(p, stream);
-    else if (bm == 64) rc = bn == 64 ? launch_wgrad<64, 64, 2, 2>(p, stream) : launch_wgrad<64, 256, 1, 4>(p, stream);
+    else if (bm == 64) rc = bn_cols == 64 ? launch_wgrad<64, 64, 2, 2>(p, stream) : launch_wgrad<64, 256, 1, 4>(p, stream);
     else rc = launch_wgrad<32, 256, 1, 4>(p, stream);
   }
   if (rc) return rc;
@@ -1228,6 +1263,17 @@ int srpde_conv_wgrad(const float* dy, int lddy, const float* x0, int c0, int ldx
                      int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
   return conv_wgrad_impl(dy, lddy, x0, c0, ldx0, x1, c1, ldx1, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
                          workspace, ws_bytes, stream);
+}
+
+int srpde_conv_wgrad_bnb(const float* da, int ldda, const float* y, int ldy, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, const float* m1, const float* m2, int flags,
+                         const float* x0, int c0, int ldx0, float* dw, int cin_real, int accumulate, int n, int h,
+                         int w, int cout, int ksize, int dil, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  SRPDE_CHECK_ARG(da && y && mean && invstd && gamma && beta && m1 && m2 && ldy % 4 == 0,
+                  "srpde_conv_wgrad_bnb: null argument / y stride");
+  const WgradBn bn{y, ldy, mean, invstd, gamma, beta, m1, m2, flags & SRPDE_BN_RELU};
+  return conv_wgrad_impl(da, ldda, x0, c0, ldx0, nullptr, 0, 0, dw, cin_real, accumulate, n, h, w, cout, ksize, dil,
+                         workspace, ws_bytes, stream, nullptr, nullptr, nullptr, &bn);
 }
 
 int srpde_conv_wgrad_h3(const float* dy, int lddy, const unsigned* amax_dy, const float* x0, int c0, int ldx0,

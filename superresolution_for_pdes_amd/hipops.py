@@ -448,6 +448,23 @@ def _scratch(nbytes, device):
     return buf
 
 
+def conv_wgrad_bnb(da, y, mean, invstd, gamma, beta, m1, m2, x0, dw, n, h, w, ksize=3, dil=1, relu=True):
+    """srpde_conv_wgrad_bnb: the fp32 weight gradient whose dY is the layer's BN (+ReLU) backward (m1 / m2 of
+    bn_bwd_prepare) applied as it is loaded -- dy is never written."""
+    cout = da.shape[1]
+    pda, ldda = _pl(da)
+    py, ldy = _pl(y)
+    p0, ld0 = _pl(x0)
+    cin = x0.shape[1]
+    cin_real = dw.shape[1]
+    ws_bytes = int(query("srpde_conv_wgrad_workspace_size", n, h, w, cout, cin, ksize))
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=da.device)
+    _conv_call("srpde_conv_wgrad_bnb", 2.0 * cout * cin_real * ksize * ksize * n * h * w, pda, ldda, py, ldy,
+               mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), m1.data_ptr(), m2.data_ptr(),
+               BN_RELU if relu else 0, p0, cin, ld0, dw.data_ptr(), cin_real, 0, n, h, w, cout, ksize, dil,
+               ws.data_ptr(), ws_bytes, stream_ptr())
+
+
 def conv_wgrad(dy, x0, x1, dw, n, h, w, ksize=3, dil=1, accumulate=False):
     cout = dy.shape[1]
     pdy, lddy = _pl(dy)

@@ -568,6 +568,18 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
         else:
             wq.submit(fn, keep)
         return None if out_part is None else (out_part, dx_max)
+    if (_FUSE_WGRAD_BN and train and dx is None and xp is None and x0 is not None and x1 is None
+            and x0.shape[1] % 32 != 0 and DEBUG_TAPS is None):
+        # enc1.conv1 (no dgrad: the input image): the fp32 weight gradient applies the BN backward to its dY loads
+        m1, m2, _ = H.bn_bwd_prepare(y, da, mean, invstd, bn.weight, bn.bias, grads[bn.weight], grads[bn.bias],
+                                     grads[conv.bias], part=part_t, da_max=da_max)
+        dw = grads[conv.weight]
+        fn = lambda: H.conv_wgrad_bnb(da, y, mean, invstd, bn.weight, bn.bias, m1, m2, x0, dw, n, h, w, 3, dil)
+        if wq is None:
+            fn()
+        else:
+            wq.submit(fn, (da, y, m1, m2))
+        return None
     dy = H.empty(P, cout, device=y.device)
     # eval mode: the forward normalised with the running statistics (constants), so the BN
     # backward drops the batch-statistic terms (aten native_batch_norm_backward, training=False)
@@ -607,6 +619,10 @@ def _cbr_bwd(conv, bn, saved, da, n, h, w, dil, grads, slots, dx=None, dx_accumu
 # the attention gates' output (x * ca) * sa formed inside the decoder conv that reads it (GatedInput;
 # _FUSE_ATT_APPLY False: a separate srpde_att_apply_fwd pass writes it)
 _FUSE_ATT_APPLY = True
+
+# enc1.conv1's BN backward applied inside its fp32 weight gradient's dY loads (srpde_conv_wgrad_bnb; False: dy
+# written by bn_relu_bwd, then read)
+_FUSE_WGRAD_BN = True
 
 # the BN (+ReLU) backward apply of a layer fused into its dgrad's operand transform
 # (srpde_conv_dgrad_h3_bnb; _FUSE_BN_APPLY False: off)

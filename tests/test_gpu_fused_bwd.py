@@ -207,3 +207,27 @@ def test_gate_weight_gradient_from_low_res(n):
     gate = {k: v for k, v in worst.items() if "spatial_attention" in k}
     assert len(gate) >= 4 and any(v > 0 for v in gate.values())   # the path really changed those sums
     print({k: f"{v:.1e}" for k, v in gate.items()})
+
+
+@pytest.mark.parametrize("n", [2, 19])
+def test_enc1_conv1_weight_gradient_with_fused_bn_backward(n):
+    """enc1.conv1's fp32 weight gradient applying enc1.bn1's backward to its dY loads (srpde_conv_wgrad_bnb)
+    against dy written by bn_relu_bwd and read back: the same dy bits, so the weight gradient is EQUAL bit for bit,
+    and so is every other gradient but the BN-fed conv bias (formed analytically instead of summed)."""
+    from oracle import unet_ref as U   # (test infrastructure: the seeded reference initialisation)
+    from superresolution_for_pdes_amd.models import UNet
+    model = UNet()
+    model.load_state_dict(U.kaiming_init_state(23))
+    model = model.to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(51 + n)
+    x = torch.randn(n, 3, 40, 40, device=DEV, generator=g)
+    x[:, 1] = 1.0
+    t = torch.randn(n, 1, 40, 40, device=DEV, generator=g)
+    _, grads_f = _step(model, x, t, True, "_FUSE_WGRAD_BN", ())
+    _, grads_u = _step(model, x, t, False, "_FUSE_WGRAD_BN", ())
+    for name, gu in grads_u.items():
+        if name == "enc1.conv1.bias":
+            rel = float((grads_f[name] - gu).double().norm() / max(float(grads_u["enc1.conv1.weight"].norm()), 1e-30))
+            assert rel < 1e-5, rel   # true gradient 0: rounding noise either way
+            continue
+        assert torch.equal(grads_f[name], gu), name
