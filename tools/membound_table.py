@@ -48,6 +48,18 @@ def expect(name, a):
         n, h, w, ho, wo, c, acc = a[6:13]
         return [("upsample_bwd", n * ho * wo * (c + 1) * 4 + n * h * w * c * 4 * (2 if acc else 1),
                  f"{h}->{ho} C={c} gated")]
+    if name == "srpde_upsample_bilinear_bwd_gated_bn":   # + the BN backward reduction of dx (reads y)
+        n, h, w, ho, wo, c = a[6:12]
+        return [("upsample_bwd", n * ho * wo * (c + 1) * 4 + n * h * w * c * 8, f"{h}->{ho} C={c} gated+bn")]
+    if name == "srpde_gating_bn_reduce":
+        P, C = a[10], a[11]
+        return [("gating_bn_reduce_kernel", P * C * 12 + P * 4, f"P={P} C={C}")]
+    if name == "srpde_att_bwd_params_lowres":
+        n, h, w, ho, wo, c, gc = a[2:9]
+        Plo = n * h * w
+        return (_att_params(n, h * w, c, gc)[:4]
+                + [("upsample_t_scalar_kernel", n * ho * wo * 4 + Plo * 4, f"{ho}->{h} n={n}"),
+                   ("weighted_colsum_kernel", Plo * gc * 4 + Plo * 4, f"P={Plo} gc={gc} low-res")])
     if name == "srpde_upsample_bilinear_bwd":
         n, h, w, ho, wo, c, acc = a[4:11]
         return [("upsample_bwd", n * ho * wo * c * 4 + n * h * w * c * 4 * (2 if acc else 1), f"{h}->{ho} C={c}")]
@@ -74,8 +86,11 @@ def expect(name, a):
     if name == "srpde_att_bwd_params":
         n, hw, c, gc = a[2:6]
         return _att_params(n, hw, c, gc)
-    if name in ("srpde_conv_wgrad_h3p", "srpde_conv_wgrad_h3x", "srpde_conv_wgrad", "srpde_conv_wgrad_h3"):
-        if name == "srpde_conv_wgrad_h3p":
+    if name in ("srpde_conv_wgrad_h3p", "srpde_conv_wgrad_h3x", "srpde_conv_wgrad", "srpde_conv_wgrad_h3",
+                "srpde_conv_wgrad_bnb"):
+        if name == "srpde_conv_wgrad_bnb":
+            c0, c1, acc, n, h, w, cout, ks, ws = a[12], 0, a[16], a[17], a[18], a[19], a[20], a[21], a[24]
+        elif name == "srpde_conv_wgrad_h3p":
             c0, c1, acc, n, h, w, cout, ks, ws = a[3], a[5], a[9], a[10], a[11], a[12], a[13], a[14], a[17]
         elif name == "srpde_conv_wgrad_h3x":
             c0, c1, acc, n, h, w, cout, ks, ws = a[4], a[10], a[16], a[17], a[18], a[19], a[20], a[21], a[24]
@@ -109,7 +124,8 @@ def _att_params(n, hw, c, gc):
 MEMBOUND = {"srpde_bn_bwd_apply_split", "srpde_bn_bwd_prepare", "srpde_bn_relu_bwd", "srpde_bn_relu_bwd_part",
             "srpde_upsample_bilinear_bwd_gated", "srpde_upsample_bilinear_bwd", "srpde_maxpool2x2_bwd",
             "srpde_att_bwd", "srpde_att_bwd_params", "srpde_conv_wgrad_h3p", "srpde_conv_wgrad_h3x",
-            "srpde_conv_wgrad", "srpde_conv_wgrad_h3"}
+            "srpde_conv_wgrad", "srpde_conv_wgrad_h3", "srpde_upsample_bilinear_bwd_gated_bn", "srpde_gating_bn_reduce",
+            "srpde_att_bwd_params_lowres", "srpde_conv_wgrad_bnb"}
 MARKER = "bn_eval_prepare_kernel"
 
 
