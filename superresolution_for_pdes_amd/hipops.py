@@ -180,6 +180,10 @@ class UpsampledInput:
         return self.x.device
 
     @property
+    def is_cuda(self):
+        return self.x.is_cuda
+
+    @property
     def _srpde_amax(self):   # a bound on |up(x)|: interpolation is a convex combination
         return amax_of(self.x)
 

@@ -272,7 +272,8 @@ def _cbr_fwd(conv, bn, x0, x1, n, h, w, training, dil, slots, in_affine=None, ac
     if training:
         stats, nblk, rpb = H.conv_stats_buffer(n, h, w, cout, dev, x0.shape[1], c1, dil)
         if _splits_both_ways(x0.shape[1], c1, cout, w, dil):
-            if _WGRAD_X and x0.is_cuda and H.wgrad_x_capable(x0.shape[1], c1, cout, w, dil):
+            if (_WGRAD_X and not isinstance(x0, H.UpsampledInput) and x0.is_cuda
+                    and H.wgrad_x_capable(x0.shape[1], c1, cout, w, dil)):
                 # the weight gradient splits the fp32 input itself (srpde_conv_wgrad_h3x): nothing stored
                 xp = H.XSource(x0, x1, in_affine, x1_gate)
             else:
@@ -672,6 +673,9 @@ def _block_fwd(blk, x0, x1, n, h, w, training, slots, pool=False, activate=True,
                      activate=activate, att=att)
 
 
+# training: up(d3) interpolated inside dec2.conv1's forward (h4 upsampled-input kernel with statistics and the stored
+# split) and att2's spatial attention from d3 at low resolution, as in inference: u3 is never written (False: formed)
+_TRAIN_UP3 = True
 # the decoder gates' spatial weight gradient from the low-res decoder output d (sum_q d[q] up^T(dsa)[q]) instead of
 # the upsampled g = up(d), a quarter of the rows (False: from g)
 _GATE_WGRAD_LOWRES = True
@@ -830,7 +834,10 @@ def unet_forward(m, x, training, save=False):
     d3, S.dec3 = _block_fwd(m.dec3, b, e3a, n, h3, w3, training, slots)
     fuse_up = not training and not save   # inference: the decoder convs read up(d) without it being formed
     S.d3 = d3 if (training and _GATE_WGRAD_LOWRES) else None   # the gate's spatial weight gradient reads it
-    u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2, m.dec2.conv1, e2.shape[1], fuse_up)
+    # training: dec2.conv1 interpolates up(d3) itself as well (its forward stores the input split the weight
+    # gradient reads, and the gate's weight gradient reads d3), so u3 is never formed (_TRAIN_UP3)
+    u3, sa2 = _upsample_for_gate(d3, m.att2, n, h3, w3, h2, w2, m.dec2.conv1, e2.shape[1],
+                                 fuse_up or (training and _TRAIN_UP3 and _GATE_WGRAD_LOWRES))
     e2a, S.att2 = _att_fwd(m.att2, e2, u3, n, hw2, early=ch2, sa=sa2)
     d2, S.dec2 = _block_fwd(m.dec2, u3, e2a, n, h2, w2, training, slots)
     S.d2 = d2 if (training and _GATE_WGRAD_LOWRES) else None
@@ -929,7 +936,8 @@ def unet_backward(m, S, dout, grads, grad_ready=None, wq=None, want_dx=False):
     de2 = H.empty(P2, 128, device=dev)
     # the gating gradient (into dcat2[:, :256]) is folded into the upsample backward below
     fuse2 = _fuse_enc_out(S.enc2, 128, w2)
-    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, S.u3, n, hw2, grads, None if fuse2 else de2, False, None,
+    u3 = S.u3.x if isinstance(S.u3, H.UpsampledInput) else S.u3   # (the low-res rows: only g's width is read)
+    gate = _att_bwd(m.att2, S.att2, dcat2[:, 256:], S.e2, u3, n, hw2, grads, None if fuse2 else de2, False, None,
                     True, wq=wq, defer_dx=fuse2, g_lowres=(S.d3, h3, w3, h2, w2) if S.d3 is not None else None)
     if fuse2:
         gate, dm2 = gate
