@@ -350,7 +350,8 @@ def bn_bwd_prepare(y, da, mean, invstd, gamma, beta, dgamma, dbeta, dbias, relu=
     py, ldy = _pl(y)
     pda, ldda = _pl(da)
     m1, m2 = empty(C, device=y.device), empty(C, device=y.device)
-    word = torch.zeros(1, dtype=torch.int32, device=y.device)
+    # the bound word is written whole by the coefficient kernel: no zero fill (a kernel launch per BN backward)
+    word = torch.empty(1, dtype=torch.int32, device=y.device)
     ws_bytes = int(query("srpde_bn_bwd_prepare_workspace_size", P, C))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=y.device)
     if part is not None and da_max is None:
